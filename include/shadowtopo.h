@@ -1,0 +1,149 @@
+/*
+ * shadowtopo.h -- C ABI of libshadowtopo_hip, the MI355X (gfx950) engine behind
+ * Shadow's topology path computation.
+ *
+ * It replaces, below the unchanged topology.h API (topology_hip.h in this repo), the
+ * reference's igraph-based per-source lazy path computation:
+ *   - igraph_get_shortest_paths_dijkstra call      /root/reference/src/main/routing/topology.c:1754-1775
+ *   - _topology_computeSourcePaths                  topology.c:1655-1875
+ *   - _topology_computePathProperties               topology.c:1407-1523
+ *   - _topology_computeShortestPathToSelf           topology.c:1545-1653
+ *   - _topology_lookupDirectPath                    topology.c:1877-1927
+ *   - the dispatch of _topology_getPathEntry        topology.c:2019-2031
+ *   - the two-level path cache                      topology.c:42-47, 1284-1386
+ * with one eager, batched, many-source computation of the attached-pair matrix
+ * (A x A latency / reliability / hop count) on the GPU.
+ *
+ * Plain C: int status codes, no exceptions, caller-owned buffers, no torch types.
+ * Not thread-safe per engine: callers serialise calls on one engine (the topology shim
+ * does so with a mutex / pthread_once).
+ */
+#ifndef SHADOWTOPO_H
+#define SHADOWTOPO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct shadowtopo_engine shadowtopo_engine;
+
+/* status codes */
+#define SHADOWTOPO_OK 0
+#define SHADOWTOPO_EINVAL (-1)   /* bad argument / malformed graph */
+#define SHADOWTOPO_ENOMEM (-2)   /* host or device allocation failed */
+#define SHADOWTOPO_EDEVICE (-3)  /* HIP runtime error, or no GPU */
+#define SHADOWTOPO_ESTATE (-4)   /* call out of order (e.g. compute before set_attached) */
+#define SHADOWTOPO_EINTERNAL (-5) /* iteration guard tripped */
+
+/* graph flags (topology.c:751-790: isDirected, isComplete, prefersDirectPaths) */
+#define SHADOWTOPO_F_DIRECTED 0x1u
+#define SHADOWTOPO_F_COMPLETE 0x2u
+#define SHADOWTOPO_F_PREFER_DIRECT 0x4u
+/* alternative self-pair rule: the [s] path igraph >= 0.7 returns for the
+ * source itself, i.e. the source's self-loop edge (topology.c:1456-1499); default is the
+ * version-independent _topology_computeShortestPathToSelf rule (topology.c:1545-1653). */
+#define SHADOWTOPO_F_SELF_DIJKSTRA_LOOP 0x8u
+/* let the engine decide F_COMPLETE with the reference's rule (_topology_isComplete,
+ * topology.c:450-552) instead of trusting the caller's F_COMPLETE bit */
+#define SHADOWTOPO_F_AUTO_COMPLETE 0x10u
+
+/* where compute_rows' output buffers live */
+#define SHADOWTOPO_MEM_HOST 0
+#define SHADOWTOPO_MEM_DEVICE 1
+
+/* per-pair kind codes (optional output) */
+#define SHADOWTOPO_KIND_NONE 0     /* unroutable: lat = rel = -1 (topology.c:2073, 2085) */
+#define SHADOWTOPO_KIND_DIRECT 1   /* _topology_lookupDirectPath, isDirect = TRUE */
+#define SHADOWTOPO_KIND_SELF 2     /* _topology_computeShortestPathToSelf */
+#define SHADOWTOPO_KIND_DIJKSTRA 3 /* shortest path */
+
+/* options for shadowtopo_set_option */
+#define SHADOWTOPO_OPT_BATCHES_IN_FLIGHT 1 /* source batches (64 sources each) relaxed together */
+#define SHADOWTOPO_OPT_TIMING 2            /* 1 = record HIP events around every relax launch */
+#define SHADOWTOPO_OPT_MAX_ROUNDS 3        /* iteration guard (default 4*V+64) */
+#define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
+
+typedef struct shadowtopo_stats {
+    int64_t n_vertices;
+    int64_t n_edges;
+    int64_t n_arcs;          /* non-loop arcs of the relaxation in-CSR after merging parallel edges */
+    int64_t n_attached;
+    int64_t sources;         /* source rows computed since the last reset */
+    int64_t batches;
+    int64_t rounds;          /* relaxation rounds (summed over batch groups) */
+    int64_t relax_launches;
+    int64_t replayed_sources;/* sources resolved by the heap-exact kernel (tie-tainted) */
+    int64_t tainted_pairs;
+    double relax_ms;         /* HIP-event time of relax launches (OPT_TIMING=1) */
+    double compose_ms;
+    double replay_ms;
+    double wall_ms;          /* host wall time inside compute calls */
+    int32_t device;
+    int32_t multigraph;
+} shadowtopo_stats;
+
+/* Number of visible HIP devices (0 if none). */
+int shadowtopo_device_count(void);
+
+/* Message for the last failing call on this thread. */
+const char* shadowtopo_last_error(void);
+
+/*
+ * Build the device-resident graph from the GraphML edge list, in the reference's edge
+ * order (edge index = <edge> element order, igraph_read_graph_graphml at topology.c:386).
+ *   edge_source/edge_target : vertex indices in [0, n_vertices)
+ *   edge_latency            : ms, > 0 (validated as topology.c:1066-1082 does)
+ *   edge_packetloss         : in [0,1]
+ *   vertex_packetloss       : nullable; NaN = attribute absent on that vertex
+ *                             (topology.c:330-347, 1441-1462)
+ *   flags                   : SHADOWTOPO_F_*
+ *   device                  : HIP device ordinal
+ */
+int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_source, const int32_t* edge_target,
+                      const double* edge_latency, const double* edge_packetloss, const double* vertex_packetloss,
+                      uint32_t flags, int32_t device, shadowtopo_engine** out);
+
+void shadowtopo_destroy(shadowtopo_engine* eng);
+
+/* The unique attached vertices (sources and targets), topology.c:1525-1543.  Row/column
+ * i of every matrix refers to attached[i]. */
+int shadowtopo_set_attached(shadowtopo_engine* eng, const int32_t* attached, int32_t count);
+
+int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value);
+
+/*
+ * Attached-pair rows [row_begin, row_end) x count: lat (ms), rel, hops, kind.
+ * Buffers are row-major with leading dimension `count`; kind may be NULL.
+ * mem = SHADOWTOPO_MEM_DEVICE: device pointers on the engine's device, written on
+ * `stream` (a hipStream_t, NULL = the engine's own stream); the call returns after the
+ * stream work is complete.  mem = SHADOWTOPO_MEM_HOST: host pointers.
+ */
+int shadowtopo_compute_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
+                            uint32_t* hops, uint8_t* kind, int32_t mem, void* stream);
+
+/*
+ * Parity tooling: full single-source results for arbitrary source vertices (row-major
+ * [n_sources][n_vertices], host buffers, any may be NULL): distance (f64, +inf if
+ * unreached), predecessor vertex (-1 for the source / unreached), hop count, and a
+ * tie flag (1 if the vertex's shortest-path tree path crosses a heap-order tie).
+ */
+int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_sources, double* dist, int32_t* pred,
+                    uint32_t* hops, uint8_t* tie);
+
+int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out);
+void shadowtopo_reset_stats(shadowtopo_engine* eng);
+
+/* effective completeness (caller's F_COMPLETE, or the reference rule under F_AUTO_COMPLETE) */
+int shadowtopo_is_complete(const shadowtopo_engine* eng);
+
+/* igraph_get_eid(directed = graph's, error = FALSE) as _topology_getEdgeHelper uses it
+ * (topology.c:401-444): lowest edge id joining (from, to), or -1. */
+int64_t shadowtopo_get_eid(const shadowtopo_engine* eng, int32_t from, int32_t to);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SHADOWTOPO_H */

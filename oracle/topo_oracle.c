@@ -1,0 +1,530 @@
+/*
+ * topo_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's topology path computation, used exclusively as
+ * the checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+ * It is never linked into, loaded by, or called from the product library
+ * (shadow_amd/csrc -> libshadowtopo_hip.so).
+ *
+ * What it restates (all citations relative to /root/reference):
+ *   - igraph_get_eid(directed|undirected, error=FALSE) as used by
+ *     _topology_getEdgeHelper (src/main/routing/topology.c:401-444): lowest edge id
+ *     among the edges joining the pair, -1 if none.
+ *   - _topology_isComplete (topology.c:450-552).
+ *   - igraph_get_shortest_paths_dijkstra(mode=OUT, weights=latency) as called at
+ *     topology.c:1754-1775.  igraph is a third-party system library that is NOT vendored
+ *     in the reference (cmake/FindIGRAPH.cmake accepts any version; CI installs distro
+ *     libigraph0-dev = igraph 0.7.1 / 0.8.0, .github/workflows/build_shadow.yml:30).
+ *     Restated from igraph's published source: dists init -1, parent_eids = edge+1,
+ *     indexed 2-way binary max-heap keyed on -dist (igraph_2wheap: shift_up moves equal
+ *     keys up, sink prefers the left child when left >= right, modify = set+sink+shift_up),
+ *     strict '<' relax, lazy incidence list in igraph_incident() order, early exit once
+ *     every target has been popped.
+ *   - _topology_computePathProperties (topology.c:1407-1523): latency left fold from 0.0
+ *     and reliability product 1*(1-ls)*(1-lt)*prod(1-loss_e) in path order, each hop's
+ *     edge re-fetched with get_eid.
+ *   - _topology_computeShortestPathToSelf (topology.c:1545-1653).
+ *   - _topology_lookupDirectPath (topology.c:1877-1927).
+ *   - _topology_getPathEntry dispatch (topology.c:1969-2051) and the 0 ms -> 1 ms clamp
+ *     (topology.c:1848-1852).
+ *
+ * PARITY STATUS: the direct-path rule is pinned by the reference's own test topologies
+ * (src/test/ * / *.test.shadow.config.xml, 1-vertex self-loop graphs) and the shipped
+ * resource/topology.graphml.xml.xz.  The SSSP branch is "parity unpinned": no reference
+ * test exercises it and igraph is absent from this container.
+ * Distances are cross-checked against scipy.sparse.csgraph / networkx in tests/.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define OG_DIRECTED 1u
+#define OG_COMPLETE 2u
+#define OG_PREFER_DIRECT 4u
+#define OG_SELF_DIJKSTRA_LOOP 8u /* alternative self-pair rule, see SURVEY 8.0 */
+
+typedef struct og {
+    int32_t n;
+    int64_t m;
+    int directed;
+    int32_t* from; /* igraph storage: undirected edges kept as from=max, to=min */
+    int32_t* to;
+    double* lat;
+    double* loss;
+    double* vloss; /* NaN = attribute absent on that vertex */
+    /* igraph "oi"/"ii" indices: edges ordered by (from,to,eid) / (to,from,eid) */
+    int64_t* os;
+    int64_t* is;
+    int64_t* oi;
+    int64_t* ii;
+    /* incidence list in igraph_incident(mode=OUT) order */
+    int64_t* inc_ptr;
+    int64_t* inc;
+} og;
+
+/* stable counting sort of edge ids by key[] (0..n-1); perm in/out */
+static void og_stable_sort(int64_t m, int32_t n, const int32_t* key, const int64_t* in, int64_t* out,
+                           int64_t* cnt /* n+1 scratch */) {
+    memset(cnt, 0, sizeof(int64_t) * (size_t)(n + 1));
+    for (int64_t i = 0; i < m; i++) cnt[key[in[i]] + 1]++;
+    for (int32_t v = 0; v < n; v++) cnt[v + 1] += cnt[v];
+    for (int64_t i = 0; i < m; i++) out[cnt[key[in[i]]]++] = in[i];
+}
+
+og* og_new(int32_t n, int64_t m, int directed, const int32_t* src, const int32_t* dst, const double* lat,
+           const double* loss, const double* vloss) {
+    og* g = (og*)calloc(1, sizeof(og));
+    if (!g) return NULL;
+    g->n = n;
+    g->m = m;
+    g->directed = directed;
+    g->from = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m ? m : 1));
+    g->to = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m ? m : 1));
+    g->lat = (double*)malloc(sizeof(double) * (size_t)(m ? m : 1));
+    g->loss = (double*)malloc(sizeof(double) * (size_t)(m ? m : 1));
+    g->vloss = (double*)malloc(sizeof(double) * (size_t)(n ? n : 1));
+    for (int64_t e = 0; e < m; e++) {
+        int32_t a = src[e], b = dst[e];
+        /* igraph_add_edges: undirected edges stored with from >= to */
+        if (directed || a > b) {
+            g->from[e] = a;
+            g->to[e] = b;
+        } else {
+            g->from[e] = b;
+            g->to[e] = a;
+        }
+        g->lat[e] = lat[e];
+        g->loss[e] = loss[e];
+    }
+    for (int32_t v = 0; v < n; v++) g->vloss[v] = vloss ? vloss[v] : NAN;
+
+    int64_t* cnt = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 1));
+    int64_t* tmp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m ? m : 1));
+    int64_t* ident = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m ? m : 1));
+    for (int64_t e = 0; e < m; e++) ident[e] = e;
+    g->oi = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m ? m : 1));
+    g->ii = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m ? m : 1));
+    /* igraph_vector_order(from, to): primary from, secondary to, stable in eid */
+    og_stable_sort(m, n, g->to, ident, tmp, cnt);
+    og_stable_sort(m, n, g->from, tmp, g->oi, cnt);
+    og_stable_sort(m, n, g->from, ident, tmp, cnt);
+    og_stable_sort(m, n, g->to, tmp, g->ii, cnt);
+    g->os = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    g->is = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    for (int64_t e = 0; e < m; e++) {
+        g->os[g->from[e] + 1]++;
+        g->is[g->to[e] + 1]++;
+    }
+    for (int32_t v = 0; v < n; v++) {
+        g->os[v + 1] += g->os[v];
+        g->is[v + 1] += g->is[v];
+    }
+    /* igraph_incident(v, OUT): directed -> out part only; undirected -> mode ALL,
+     * out part (edges with from==v) followed by in part (edges with to==v). */
+    g->inc_ptr = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+    for (int32_t v = 0; v < n; v++) {
+        int64_t deg = g->os[v + 1] - g->os[v];
+        if (!directed) deg += g->is[v + 1] - g->is[v];
+        g->inc_ptr[v + 1] = g->inc_ptr[v] + deg;
+    }
+    g->inc = (int64_t*)malloc(sizeof(int64_t) * (size_t)(g->inc_ptr[n] ? g->inc_ptr[n] : 1));
+    for (int32_t v = 0; v < n; v++) {
+        int64_t k = g->inc_ptr[v];
+        for (int64_t i = g->os[v]; i < g->os[v + 1]; i++) g->inc[k++] = g->oi[i];
+        if (!directed)
+            for (int64_t i = g->is[v]; i < g->is[v + 1]; i++) g->inc[k++] = g->ii[i];
+    }
+    free(cnt);
+    free(tmp);
+    free(ident);
+    return g;
+}
+
+void og_free(og* g) {
+    if (!g) return;
+    free(g->from);
+    free(g->to);
+    free(g->lat);
+    free(g->loss);
+    free(g->vloss);
+    free(g->os);
+    free(g->is);
+    free(g->oi);
+    free(g->ii);
+    free(g->inc_ptr);
+    free(g->inc);
+    free(g);
+}
+
+/* igraph BINSEARCH: lower bound over an index sorted by the other endpoint, then eid */
+static int64_t og_binsearch(int64_t start, int64_t end, int32_t value, const int64_t* iindex,
+                            const int32_t* edgelist) {
+    int64_t n = end;
+    while (start < end) {
+        int64_t mid = start + (end - start) / 2;
+        if (edgelist[iindex[mid]] < value)
+            start = mid + 1;
+        else
+            end = mid;
+    }
+    if (start < n && edgelist[iindex[start]] == value) return iindex[start];
+    return -1;
+}
+
+/* igraph_get_eid(graph, &eid, from, to, directed=isDirected, error=FALSE), topology.c:416-420 */
+int64_t og_get_eid(const og* g, int32_t a, int32_t b) {
+    int32_t xf = a, xt = b;
+    if (!g->directed && a < b) {
+        xf = b;
+        xt = a;
+    }
+    int64_t s1 = g->os[xf], e1 = g->os[xf + 1];
+    int64_t s2 = g->is[xt], e2 = g->is[xt + 1];
+    if (e1 - s1 < e2 - s2) return og_binsearch(s1, e1, xt, g->oi, g->to);
+    return og_binsearch(s2, e2, xf, g->ii, g->from);
+}
+
+static inline int32_t og_other(const og* g, int64_t e, int32_t v) { return g->from[e] == v ? g->to[e] : g->from[e]; }
+
+/* _topology_isComplete, topology.c:450-552 */
+int og_is_complete(const og* g) {
+    for (int32_t v = 0; v < g->n; v++) {
+        int64_t ecount = g->inc_ptr[v + 1] - g->inc_ptr[v];
+        if (!g->directed && og_get_eid(g, v, v) >= 0) ecount -= 1;
+        if (ecount < g->n) return 0;
+    }
+    return 1;
+}
+
+/* ---- igraph_2wheap restated (max-heap on -dist) ---- */
+typedef struct {
+    double* data;
+    int32_t* index;  /* heap position -> vertex */
+    int64_t* index2; /* vertex -> position+2, 0 = not in heap */
+    int64_t size;
+} wheap;
+
+#define WH_PARENT(x) (((x) + 1) / 2 - 1)
+#define WH_LEFT(x) (((x) + 1) * 2 - 1)
+#define WH_RIGHT(x) (((x) + 1) * 2)
+
+static void wh_switch(wheap* h, int64_t e1, int64_t e2) {
+    if (e1 == e2) return;
+    double td = h->data[e1];
+    h->data[e1] = h->data[e2];
+    h->data[e2] = td;
+    int32_t t1 = h->index[e1], t2 = h->index[e2];
+    h->index[e1] = t2;
+    h->index[e2] = t1;
+    h->index2[t1] = e2 + 2;
+    h->index2[t2] = e1 + 2;
+}
+
+static void wh_shift_up(wheap* h, int64_t elem) {
+    while (!(elem == 0 || h->data[elem] < h->data[WH_PARENT(elem)])) {
+        wh_switch(h, elem, WH_PARENT(elem));
+        elem = WH_PARENT(elem);
+    }
+}
+
+static void wh_sink(wheap* h, int64_t head) {
+    for (;;) {
+        int64_t l = WH_LEFT(head), r = WH_RIGHT(head);
+        if (l >= h->size) return;
+        if (r == h->size || h->data[l] >= h->data[r]) {
+            if (h->data[head] < h->data[l]) {
+                wh_switch(h, head, l);
+                head = l;
+            } else
+                return;
+        } else {
+            if (h->data[head] < h->data[r]) {
+                wh_switch(h, head, r);
+                head = r;
+            } else
+                return;
+        }
+    }
+}
+
+static void wh_push(wheap* h, int32_t idx, double elem) {
+    int64_t pos = h->size++;
+    h->data[pos] = elem;
+    h->index[pos] = idx;
+    h->index2[idx] = pos + 2;
+    wh_shift_up(h, pos);
+}
+
+static int32_t wh_delete_max(wheap* h, double* key) {
+    int32_t tmpidx = h->index[0];
+    *key = h->data[0];
+    wh_switch(h, 0, h->size - 1);
+    h->size--;
+    h->index2[tmpidx] = 0;
+    wh_sink(h, 0);
+    return tmpidx;
+}
+
+static void wh_modify(wheap* h, int32_t idx, double elem) {
+    int64_t pos = h->index2[idx] - 2;
+    h->data[pos] = elem;
+    wh_sink(h, pos);
+    wh_shift_up(h, pos);
+}
+
+/*
+ * igraph_get_shortest_paths_dijkstra(mode=OUT) restated.
+ * dist[v] = -1 if never reached; parent[v] = parent edge id or -1.
+ * targets may be NULL (then no early exit: every reachable vertex is settled).
+ * pop_order (nullable) receives the settle order; returns the number of pops.
+ */
+int64_t og_dijkstra(const og* g, int32_t source, const int32_t* targets, int32_t nt, double* dist,
+                    int64_t* parent, int32_t* pop_order) {
+    int32_t n = g->n;
+    wheap h;
+    h.data = (double*)malloc(sizeof(double) * (size_t)n);
+    h.index = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    h.index2 = (int64_t*)calloc((size_t)n, sizeof(int64_t));
+    h.size = 0;
+    uint8_t* is_target = (uint8_t*)calloc((size_t)n, 1);
+    int64_t to_reach = 0;
+    if (targets) {
+        to_reach = nt;
+        for (int32_t i = 0; i < nt; i++) {
+            if (!is_target[targets[i]])
+                is_target[targets[i]] = 1;
+            else
+                to_reach--;
+        }
+    }
+    for (int32_t v = 0; v < n; v++) {
+        dist[v] = -1.0;
+        parent[v] = -1;
+    }
+    dist[source] = 0.0;
+    wh_push(&h, source, 0.0);
+    int64_t npop = 0;
+    while (h.size > 0 && (!targets || to_reach > 0)) {
+        double key;
+        int32_t minnei = wh_delete_max(&h, &key);
+        double mindist = -key;
+        if (pop_order) pop_order[npop] = minnei;
+        npop++;
+        if (targets && is_target[minnei]) {
+            is_target[minnei] = 0;
+            to_reach--;
+        }
+        for (int64_t i = g->inc_ptr[minnei]; i < g->inc_ptr[minnei + 1]; i++) {
+            int64_t edge = g->inc[i];
+            int32_t tto = og_other(g, edge, minnei);
+            double altdist = mindist + g->lat[edge];
+            double curdist = dist[tto];
+            if (curdist < 0) {
+                dist[tto] = altdist;
+                parent[tto] = edge;
+                wh_push(&h, tto, -altdist);
+            } else if (altdist < curdist) {
+                dist[tto] = altdist;
+                parent[tto] = edge;
+                wh_modify(&h, tto, -altdist);
+            }
+        }
+    }
+    free(h.data);
+    free(h.index);
+    free(h.index2);
+    free(is_target);
+    return npop;
+}
+
+/* vertex path [source .. node] from igraph parent edges; returns length (0 if unreachable
+ * and node != source).  For node == source the path is [source] (igraph >= 0.7). */
+int32_t og_path(const og* g, int32_t source, int32_t node, const int64_t* parent, int32_t* out, int32_t cap) {
+    int32_t size = 0, act = node;
+    while (parent[act] >= 0) {
+        size++;
+        act = og_other(g, parent[act], act);
+    }
+    if (size == 0 && node != source) return 0;
+    if (size + 1 > cap) return -1;
+    out[size] = node;
+    act = node;
+    int32_t k = size;
+    while (parent[act] >= 0) {
+        act = og_other(g, parent[act], act);
+        out[--k] = act;
+    }
+    return size + 1;
+}
+
+static inline int og_has_vloss(const og* g, int32_t v) { return !isnan(g->vloss[v]); }
+
+/* _topology_computePathProperties, topology.c:1407-1523.  Returns 1 on success. */
+int og_path_properties(const og* g, int32_t src, const int32_t* path, int32_t len, double* lat_out,
+                       double* rel_out) {
+    double total_latency = 0.0;
+    double total_rel = 1.0;
+    if (len <= 0) return 0;
+    if (og_has_vloss(g, src)) total_rel *= (1.0 - g->vloss[src]);
+    int32_t target = path[len - 1];
+    if ((src != target) || (src == target && len > 2)) {
+        if (og_has_vloss(g, target)) total_rel *= (1.0 - g->vloss[target]);
+    }
+    int32_t start = (len == 1) ? 0 : 1;
+    int32_t from = src;
+    for (int32_t i = start; i < len; i++) {
+        int32_t to = path[i];
+        int64_t e = og_get_eid(g, from, to);
+        if (e < 0) return 0;
+        total_latency += g->lat[e];
+        total_rel *= (1.0 - g->loss[e]);
+        from = to;
+    }
+    *lat_out = total_latency;
+    *rel_out = total_rel;
+    return 1;
+}
+
+/* _topology_computeShortestPathToSelf, topology.c:1545-1653 */
+int og_self_path(const og* g, int32_t v, double* lat_out, double* rel_out) {
+    double min_latency = 0.0, rel_min = 0.0;
+    if (g->inc_ptr[v + 1] == g->inc_ptr[v]) return 0; /* igraph_edge(0) fails */
+    for (int64_t i = g->inc_ptr[v]; i < g->inc_ptr[v + 1]; i++) {
+        int64_t e = g->inc[i];
+        double l = g->lat[e];
+        if (min_latency == 0 || l < min_latency) {
+            min_latency = l;
+            rel_min = 1.0 - g->loss[e];
+        }
+    }
+    *lat_out = 2.0 * min_latency;
+    *rel_out = rel_min * rel_min;
+    return 1;
+}
+
+/* _topology_lookupDirectPath, topology.c:1877-1927 (edge index -1 = failure here; the
+ * reference reads attributes at index -1, undefined behaviour). */
+int og_direct_path(const og* g, int32_t s, int32_t t, double* lat_out, double* rel_out) {
+    double total_latency = 0.0, total_rel = 1.0;
+    if (og_has_vloss(g, s)) total_rel *= (1.0 - g->vloss[s]);
+    if (og_has_vloss(g, t)) total_rel *= (1.0 - g->vloss[t]);
+    int64_t e = og_get_eid(g, s, t);
+    if (e < 0) return 0;
+    total_latency += g->lat[e];
+    total_rel *= (1.0 - g->loss[e]);
+    *lat_out = total_latency;
+    *rel_out = total_rel;
+    return 1;
+}
+
+/*
+ * Canonical order-independent attached-pair matrix: for every
+ * ordered pair (attached[i], attached[j]) the value _topology_getPathEntry would store
+ * for that ordered pair from its own source's computation.
+ * lat = -1 / rel = -1 / hops = 0 for pairs the reference cannot route.
+ * kind[i*A+j]: 0 = failure, 1 = direct, 2 = self rule, 3 = dijkstra.
+ * Sources [row_begin,row_end) only; nthreads > 1 uses OpenMP over sources.
+ */
+int og_pair_rows(const og* g, uint32_t flags, const int32_t* attached, int32_t A, int32_t row_begin, int32_t row_end,
+                 double* lat, double* rel, uint32_t* hops, uint8_t* kind, int nthreads) {
+    int complete = (flags & OG_COMPLETE) != 0;
+    int prefer = (flags & OG_PREFER_DIRECT) != 0;
+    int self_loop_rule = (flags & OG_SELF_DIJKSTRA_LOOP) != 0;
+    int32_t n = g->n;
+    int failures = 0;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : failures)
+#endif
+    {
+        double* dist = (double*)malloc(sizeof(double) * (size_t)n);
+        int64_t* parent = (int64_t*)malloc(sizeof(int64_t) * (size_t)n);
+        int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int32_t i = row_begin; i < row_end; i++) {
+            int32_t s = attached[i];
+            int have_sssp = 0;
+            for (int32_t j = 0; j < A; j++) {
+                int32_t t = attached[j];
+                size_t o = (size_t)(i - row_begin) * (size_t)A + (size_t)j;
+                double l = -1.0, r = -1.0;
+                uint32_t h = 0;
+                uint8_t k = 0;
+                int adjacent = (prefer && !complete) ? (og_get_eid(g, s, t) >= 0) : 0;
+                if (complete || (prefer && adjacent)) {
+                    if (og_direct_path(g, s, t, &l, &r)) {
+                        h = 1;
+                        k = 1;
+                    }
+                } else if (s == t && !self_loop_rule) {
+                    if (og_self_path(g, s, &l, &r)) {
+                        h = 2;
+                        k = 2;
+                    }
+                } else {
+                    if (!have_sssp) {
+                        og_dijkstra(g, s, attached, A, dist, parent, NULL);
+                        have_sssp = 1;
+                    }
+                    int32_t len = og_path(g, s, t, parent, path, n + 1);
+                    if (len > 0 && og_path_properties(g, s, path, len, &l, &r)) {
+                        if (l == 0) l = 1; /* topology.c:1848-1852 */
+                        h = (uint32_t)(len == 1 ? 1 : len - 1);
+                        k = 3;
+                    } else {
+                        l = -1.0;
+                        r = -1.0;
+                    }
+                }
+                if (k == 0) failures++;
+                lat[o] = l;
+                rel[o] = r;
+                hops[o] = h;
+                if (kind) kind[o] = k;
+            }
+        }
+        free(dist);
+        free(parent);
+        free(path);
+    }
+    return failures;
+}
+
+/*
+ * For parity analysis of the GPU tie flag: per vertex v != source, 1 if two distinct
+ * in-neighbours u1 != u2 with identical d(u) both satisfy fl(d(u)+w) == d(v) with that d(u)
+ * minimal among such candidates, or a candidate has d(u) == d(v) (heap-order dependent).
+ */
+void og_tie_vertices(const og* g, int32_t source, const double* dist, uint8_t* tie) {
+    for (int32_t v = 0; v < g->n; v++) tie[v] = 0;
+    double* best_du = (double*)malloc(sizeof(double) * (size_t)g->n);
+    int32_t* best_u = (int32_t*)malloc(sizeof(int32_t) * (size_t)g->n);
+    for (int32_t v = 0; v < g->n; v++) {
+        best_du[v] = INFINITY;
+        best_u[v] = -1;
+    }
+    for (int pass = 0; pass < 2; pass++) {
+        for (int64_t e = 0; e < g->m; e++) {
+            for (int dir = 0; dir < (g->directed ? 1 : 2); dir++) {
+                int32_t u = dir ? g->to[e] : g->from[e];
+                int32_t v = dir ? g->from[e] : g->to[e];
+                if (u == v || v == source) continue;
+                if (dist[u] < 0 || dist[v] < 0) continue;
+                if (dist[u] + g->lat[e] != dist[v]) continue;
+                if (pass == 0) {
+                    if (dist[u] < best_du[v]) {
+                        best_du[v] = dist[u];
+                        best_u[v] = u;
+                    }
+                } else {
+                    if (dist[u] == best_du[v] && u != best_u[v]) tie[v] = 1;
+                    if (dist[u] == dist[v]) tie[v] = 1;
+                }
+            }
+        }
+    }
+    free(best_du);
+    free(best_u);
+}

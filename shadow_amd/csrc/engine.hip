@@ -1,0 +1,1335 @@
+// engine.hip -- libshadowtopo_hip: batched many-source shortest-latency routing for
+// Shadow's topology (gfx950 / MI355X).  C ABI: include/shadowtopo.h.
+//
+// What this replaces in the reference (/root/reference/src/main/routing/topology.c):
+// one igraph Dijkstra per unique attached source, run lazily on a cache miss under the
+// global graphLock (:1655-1875, :1747-1781), followed by a per-target path walk that
+// re-fetches every hop's edge with igraph_get_eid (:1407-1523), the self-path rule
+// (:1545-1653), the direct-path rule (:1877-1927) and the dispatch of
+// _topology_getPathEntry (:2019-2031).
+//
+// How (see DESIGN.md for the full argument):
+//  * A batch = 64 sources = one wavefront's lanes.  Per-batch state is laid out
+//    [vertex][lane] (source-minor), so the 64 distances of one vertex are one 512-byte
+//    row: every relaxation step is one fully coalesced global_load_dwordx2 per wave.
+//  * k_relax: pull-style label-correcting rounds.  One wave owns one destination v and
+//    walks v's in-arcs (scalar loads: the arc list is wave-uniform); each lane keeps the
+//    lexicographic minimum of (fl(d(u)+w), d(u)).  In exact IEEE arithmetic every
+//    relaxation order converges to the same fixed point as igraph's Dijkstra, and the
+//    (candidate, d(u)) minimum is igraph's "first popped predecessor" whenever no two
+//    candidates share d(u) -- that case is flagged (tie taint) and resolved by k_replay,
+//    a heap-exact re-execution of igraph's algorithm on the device.
+//  * Hop count and the reliability product are carried along the predecessor tree in
+//    the same rounds (H, R), so the common case needs no path walk at all.
+//  * Frontier: a vertex is recomputed only when an in-neighbour changed (byte flags).
+//  * k_compose applies the reference's pair dispatch and writes the attached-pair rows
+//    through an LDS transpose (coalesced row stores).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "shadowtopo.h"
+
+namespace {
+
+constexpr int KL = 64;                    // sources per batch = wave width
+constexpr uint32_t TAINT = 0x80000000u;   // H bit: tree path crosses a heap-order tie
+constexpr uint32_t HMASK = 0x7fffffffu;
+constexpr int REPLAY_SLOTS = 64;
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return fail(SHADOWTOPO_EDEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                     \
+    } while (0)
+
+struct GraphDev {
+    int32_t V;
+    uint32_t flags;
+    int32_t multigraph;
+    int32_t pad_;
+    const int64_t* in_ptr;   // [V+1] relaxation in-CSR (no loops, parallel edges merged)
+    const int32_t* in_src;   // [arcs] tail u, ascending within a row
+    const double* in_w;      // [arcs] min latency over the merged parallel edges
+    const double* in_r;      // [arcs] 1 - packetloss of the get_eid edge
+    const int32_t* in_eid;   // [arcs] get_eid edge (lowest edge id)
+    const int64_t* out_ptr;  // [V+1] out-neighbours (== in-CSR for undirected graphs)
+    const int32_t* out_dst;
+    const int64_t* inc_ptr;  // [V+1] igraph_incident(OUT) order, loops included
+    const int32_t* inc_eid;
+    const int32_t* efrom;    // igraph storage (undirected: from = max, to = min)
+    const int32_t* eto;
+    const double* elat;
+    const double* erel;      // 1.0 - packetloss (topology.c:437)
+    const double* vfac;      // 1.0 - vertex packetloss, 1.0 when absent (topology.c:1441-1462)
+    const int32_t* loop_eid; // lowest-id self-loop per vertex, -1 if none
+};
+
+struct BatchDev {
+    double* D;       // [V][64] distance
+    uint32_t* H;     // [V][64] hops | TAINT
+    double* R;       // [V][64] reliability fold along the tree path
+    int32_t* P;      // [V][64] predecessor in-arc
+    uint8_t* act[2]; // [V] frontier flags, alternating rounds
+    int32_t srcv[KL];
+    int32_t row[KL];
+    unsigned long long replay_mask;
+};
+
+struct ReplayDev {
+    double* dist;     // [slot][V]
+    int32_t* parent;  // [slot][V] parent edge id
+    double* hdata;    // [slot][V] heap keys
+    int32_t* hidx;    // [slot][V] heap position -> vertex
+    int32_t* hidx2;   // [slot][V] vertex -> position + 2 (0 = not in heap)
+    uint8_t* tgt;     // [slot][V]
+    int32_t srcv[REPLAY_SLOTS];
+    int32_t row[REPLAY_SLOTS];
+};
+
+// global-address-space view of a pointer loaded from memory (lets the compiler emit
+// global_load instead of flat_load for the per-batch state arrays)
+typedef __attribute__((address_space(1))) double gdouble;
+
+__device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000000000000LL); }
+
+__device__ __forceinline__ int64_t find_arc(const GraphDev& g, int32_t v, int32_t u) {
+    int64_t lo = g.in_ptr[v], end = g.in_ptr[v + 1], hi = end;
+    while (lo < hi) {
+        int64_t mid = lo + ((hi - lo) >> 1);
+        if (g.in_src[mid] < u)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return (lo < end && g.in_src[lo] == u) ? lo : -1;
+}
+
+// igraph_get_eid(from, to, directed=graph's, error=FALSE) -- topology.c:416-420
+__device__ __forceinline__ int32_t get_eid(const GraphDev& g, int32_t from, int32_t to) {
+    if (from == to) return g.loop_eid[from];
+    int64_t a = find_arc(g, to, from);
+    return a < 0 ? -1 : g.in_eid[a];
+}
+
+// ---------------------------------------------------------------- batch state init
+__global__ void k_init(BatchDev* __restrict__ batches, int32_t V) {
+    BatchDev& B = batches[blockIdx.y];
+    const size_t total = (size_t)V * KL;
+    const double inf = dinf();
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        B.D[i] = inf;
+        B.H[i] = 0;
+        B.R[i] = 0.0;
+        B.P[i] = -1;
+    }
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
+        B.act[0][i] = 0;
+        B.act[1][i] = 0;
+    }
+}
+
+// sources: d(s) = 0, R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445); activate out-neighbours
+__global__ void k_seed(GraphDev g, BatchDev* __restrict__ batches) {
+    BatchDev& B = batches[blockIdx.y];
+    const int j = blockIdx.x;
+    const int32_t s = B.srcv[j];
+    if (s < 0) return;
+    if (threadIdx.x == 0) {
+        const size_t idx = (size_t)s * KL + j;
+        B.D[idx] = 0.0;
+        B.H[idx] = 0;
+        B.R[idx] = g.vfac[s];
+        B.P[idx] = -1;
+    }
+    for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act[0][g.out_dst[x]] = 1;
+}
+
+__device__ __forceinline__ void relax_one(double du, double w, int32_t e, double& bc, double& bdu, int32_t& be,
+                                          bool& tie) {
+    const double c = du + w;  // igraph: altdist = mindist + weights[edge]
+    if (c <= bc && du < dinf()) {
+        if (c < bc || du < bdu) {
+            bc = c;
+            bdu = du;
+            be = e;
+            tie = false;
+        } else if (du == bdu) {
+            tie = true;  // two predecessors at the same d(u): heap pop order decides
+        }
+    }
+}
+
+// One relaxation round over every active destination vertex of every batch in flight.
+// Grid: 1-D, remapped so that all blocks sharing an XCD (blockIdx % 8) work on the same
+// batch (its [V][64] state then stays in that XCD's L2).  Placement is a speed hint only.
+__global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                               const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                               const int64_t* __restrict__ out_ptr,
+                                               const int32_t* __restrict__ out_dst, BatchDev* __restrict__ batches,
+                                               int32_t V, int32_t nb, int32_t nvb, int32_t parity,
+                                               int32_t* __restrict__ cnt) {
+    const int32_t L = blockIdx.x;
+    const int32_t xcd = L & 7;
+    const int32_t q = L >> 3;
+    const int32_t b = xcd + 8 * (q / nvb);
+    if (b >= nb) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v = (q % nvb) * 4 + wave;
+    if (v >= V) return;
+    const int lane = threadIdx.x & 63;
+    BatchDev& B = batches[b];
+    uint8_t* act_cur = B.act[parity];
+    if (act_cur[v] == 0) return;
+    if (lane == 0) act_cur[v] = 0;
+
+    const int32_t sv = B.srcv[lane];
+    const gdouble* Dl = (const gdouble*)(B.D + lane);
+    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
+    double bc = dinf(), bdu = dinf();
+    int32_t be = -1;
+    bool tie = false;
+    int32_t e = beg;
+    for (; e + 8 <= end; e += 8) {
+        int32_t u[8];
+        double w[8], du[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u[k] = in_src[e + k];
+            w[k] = in_w[e + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) du[k] = Dl[(size_t)u[k] * KL];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) relax_one(du[k], w[k], e + k, bc, bdu, be, tie);
+    }
+    for (; e < end; ++e) relax_one(Dl[(size_t)in_src[e] * KL], in_w[e], e, bc, bdu, be, tie);
+
+    bool ch = false;
+    if (be >= 0 && sv >= 0 && sv != v) {
+        const size_t idx = (size_t)v * KL + lane;
+        const int32_t u = in_src[be];
+        const size_t uidx = (size_t)u * KL + lane;
+        const uint32_t hu = B.H[uidx];
+        const double ru = B.R[uidx];
+        const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? TAINT : 0u);
+        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
+        const double r = ru * in_r[be];  // topology.c:1499 totalReliability *= edgeReliability
+        if (bc != B.D[idx] || h != B.H[idx] || r != B.R[idx] || be != B.P[idx]) {
+            B.D[idx] = bc;
+            B.H[idx] = h;
+            B.R[idx] = r;
+            B.P[idx] = be;
+            ch = true;
+        }
+    }
+    if (__ballot(ch)) {
+        uint8_t* act_nxt = B.act[parity ^ 1];
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) atomicAdd(&cnt[b], 1);
+    }
+}
+
+// ---------------------------------------------------------------- self pairs
+// _topology_computeShortestPathToSelf (topology.c:1545-1653): first strict minimum of the
+// OUT-incident edges in igraph order, used twice; or (F_SELF_DIJKSTRA_LOOP) the [s] path
+// through the source's self-loop (topology.c:1456-1499).
+__global__ void k_self(GraphDev g, const int32_t* __restrict__ attached, int32_t A, double* self_lat,
+                       double* self_rel, uint32_t* self_hops, uint8_t* self_kind) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A) return;
+    const int32_t v = attached[i];
+    double lat = -1.0, rel = -1.0;
+    uint32_t hops = 0;
+    uint8_t kind = SHADOWTOPO_KIND_NONE;
+    if (g.flags & SHADOWTOPO_F_SELF_DIJKSTRA_LOOP) {
+        const int32_t le = g.loop_eid[v];
+        if (le >= 0) {
+            lat = 0.0 + g.elat[le];
+            if (lat == 0) lat = 1;
+            rel = g.vfac[v] * g.erel[le];
+            hops = 1;
+            kind = SHADOWTOPO_KIND_DIJKSTRA;
+        }
+    } else if (g.inc_ptr[v + 1] > g.inc_ptr[v]) {
+        double minl = 0.0, rmin = 0.0;
+        for (int64_t x = g.inc_ptr[v]; x < g.inc_ptr[v + 1]; ++x) {
+            const int32_t e = g.inc_eid[x];
+            const double l = g.elat[e];
+            if (minl == 0 || l < minl) {
+                minl = l;
+                rmin = g.erel[e];
+            }
+        }
+        lat = 2.0 * minl;
+        rel = rmin * rmin;
+        hops = 2;
+        kind = SHADOWTOPO_KIND_SELF;
+    }
+    self_lat[i] = lat;
+    self_rel[i] = rel;
+    self_hops[i] = hops;
+    self_kind[i] = kind;
+}
+
+// ---------------------------------------------------------------- pair dispatch
+struct PairOut {
+    double lat, rel;
+    uint32_t hops;
+    uint8_t kind;
+    bool taint;
+};
+
+// _topology_lookupDirectPath (topology.c:1877-1927)
+__device__ __forceinline__ void direct_pair(const GraphDev& g, int32_t s, int32_t t, PairOut& o) {
+    const int32_t eid = get_eid(g, s, t);
+    if (eid < 0) return;  // reference: undefined (attribute read at edge -1)
+    o.lat = 0.0 + g.elat[eid];
+    o.rel = (g.vfac[s] * g.vfac[t]) * g.erel[eid];
+    o.hops = 1;
+    o.kind = SHADOWTOPO_KIND_DIRECT;
+}
+
+// returns true if the pair is not a shortest-path pair (handled here)
+__device__ __forceinline__ bool dispatch_pair(const GraphDev& g, int32_t s, int32_t t, int32_t ti,
+                                              const double* self_lat, const double* self_rel,
+                                              const uint32_t* self_hops, const uint8_t* self_kind, PairOut& o) {
+    o.lat = -1.0;
+    o.rel = -1.0;
+    o.hops = 0;
+    o.kind = SHADOWTOPO_KIND_NONE;
+    o.taint = false;
+    const bool complete = g.flags & SHADOWTOPO_F_COMPLETE;
+    if (complete) {
+        direct_pair(g, s, t, o);
+        return true;
+    }
+    if (g.flags & SHADOWTOPO_F_PREFER_DIRECT) {
+        if (get_eid(g, s, t) >= 0) {
+            direct_pair(g, s, t, o);
+            return true;
+        }
+    }
+    if (s == t) {
+        o.lat = self_lat[ti];
+        o.rel = self_rel[ti];
+        o.hops = self_hops[ti];
+        o.kind = self_kind[ti];
+        return true;
+    }
+    return false;
+}
+
+// forward fold over the tree path (topology.c:1473-1499): lat from 0.0, rel from
+// (1-ls)*(1-lt), each hop's edge = get_eid edge; O(h^2) walk, used only when the target
+// carries vertex loss != 0 or the graph has parallel edges of different latency.
+__device__ void walk_tree(const GraphDev& g, const BatchDev& B, int lane, int32_t s, int32_t t, uint32_t h,
+                          PairOut& o) {
+    double lat = 0.0, rel = g.vfac[s] * g.vfac[t];
+    for (uint32_t i = 0; i < h; ++i) {
+        int32_t x = t;
+        for (uint32_t k = 0; k + 1 + i < h; ++k) x = g.in_src[B.P[(size_t)x * KL + lane]];
+        const int32_t arc = B.P[(size_t)x * KL + lane];
+        lat += g.elat[g.in_eid[arc]];
+        rel *= g.in_r[arc];
+    }
+    if (g.multigraph) o.lat = (lat == 0) ? 1.0 : lat;
+    o.rel = rel;
+}
+
+__global__ __launch_bounds__(256) void k_compose(GraphDev g, BatchDev* __restrict__ batches,
+                                                 const int32_t* __restrict__ attached, int32_t A,
+                                                 const double* __restrict__ self_lat,
+                                                 const double* __restrict__ self_rel,
+                                                 const uint32_t* __restrict__ self_hops,
+                                                 const uint8_t* __restrict__ self_kind, double* out_lat,
+                                                 double* out_rel, uint32_t* out_hops, uint8_t* out_kind,
+                                                 int32_t row_base) {
+    __shared__ double sd[64 * 65];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    BatchDev& B = batches[blockIdx.y];
+    const int32_t t0 = blockIdx.x * 64;
+    const int32_t s = B.srcv[lane];
+    double vl[16], vr[16];
+    uint32_t vh[16];
+    uint8_t vk[16];
+    bool taint_any = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int32_t ti = t0 + wave * 16 + i;
+        PairOut o;
+        o.lat = -1.0;
+        o.rel = -1.0;
+        o.hops = 0;
+        o.kind = 0;
+        o.taint = false;
+        if (ti < A && s >= 0) {
+            const int32_t t = attached[ti];
+            if (!dispatch_pair(g, s, t, ti, self_lat, self_rel, self_hops, self_kind, o)) {
+                const size_t idx = (size_t)t * KL + lane;
+                const double d = B.D[idx];
+                if (d < dinf()) {
+                    const uint32_t h = B.H[idx];
+                    o.taint = (h & TAINT) != 0;
+                    o.hops = h & HMASK;
+                    o.lat = (d == 0) ? 1.0 : d;  // topology.c:1848-1852
+                    o.kind = SHADOWTOPO_KIND_DIJKSTRA;
+                    if (g.multigraph || g.vfac[t] != 1.0)
+                        walk_tree(g, B, lane, s, t, o.hops, o);
+                    else
+                        o.rel = B.R[idx];
+                }
+            }
+        }
+        taint_any |= o.taint;
+        vl[i] = o.lat;
+        vr[i] = o.rel;
+        vh[i] = o.hops;
+        vk[i] = o.kind;
+    }
+    if (taint_any) atomicOr(&B.replay_mask, 1ull << lane);
+
+    const int32_t nrow = 64;
+    // lat
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sd[lane * 65 + wave * 16 + i] = vl[i];
+    __syncthreads();
+    for (int k = threadIdx.x; k < nrow * 64; k += 256) {
+        const int j = k >> 6, tl = k & 63;
+        const int32_t r = B.row[j], ti = t0 + tl;
+        if (r >= 0 && ti < A) out_lat[(size_t)(r - row_base) * A + ti] = sd[j * 65 + tl];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sd[lane * 65 + wave * 16 + i] = vr[i];
+    __syncthreads();
+    for (int k = threadIdx.x; k < nrow * 64; k += 256) {
+        const int j = k >> 6, tl = k & 63;
+        const int32_t r = B.row[j], ti = t0 + tl;
+        if (r >= 0 && ti < A) out_rel[(size_t)(r - row_base) * A + ti] = sd[j * 65 + tl];
+    }
+    __syncthreads();
+    uint32_t* su = reinterpret_cast<uint32_t*>(sd);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        su[lane * 65 + wave * 16 + i] = vh[i];
+        su[64 * 65 + lane * 65 + wave * 16 + i] = vk[i];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nrow * 64; k += 256) {
+        const int j = k >> 6, tl = k & 63;
+        const int32_t r = B.row[j], ti = t0 + tl;
+        if (r >= 0 && ti < A) {
+            out_hops[(size_t)(r - row_base) * A + ti] = su[j * 65 + tl];
+            if (out_kind) out_kind[(size_t)(r - row_base) * A + ti] = (uint8_t)su[64 * 65 + j * 65 + tl];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- heap-exact replay
+// igraph_get_shortest_paths_dijkstra (mode OUT) re-executed exactly for one source per
+// wave (lane 0): dists init -1, indexed 2-way max-heap on -dist with igraph_2wheap's
+// shift_up / sink / modify, strict '<' relax in igraph_incident order, early exit once all
+// attached targets are popped.  Used for sources whose tree crosses a d(u) tie.
+struct Heap {
+    double* data;
+    int32_t* idx;
+    int32_t* idx2;
+    int32_t size;
+};
+
+__device__ __forceinline__ void hp_switch(Heap& h, int32_t a, int32_t b) {
+    if (a == b) return;
+    const double td = h.data[a];
+    h.data[a] = h.data[b];
+    h.data[b] = td;
+    const int32_t i1 = h.idx[a], i2 = h.idx[b];
+    h.idx[a] = i2;
+    h.idx[b] = i1;
+    h.idx2[i1] = b + 2;
+    h.idx2[i2] = a + 2;
+}
+__device__ __forceinline__ void hp_shift_up(Heap& h, int32_t e) {
+    while (!(e == 0 || h.data[e] < h.data[(e + 1) / 2 - 1])) {
+        const int32_t p = (e + 1) / 2 - 1;
+        hp_switch(h, e, p);
+        e = p;
+    }
+}
+__device__ __forceinline__ void hp_sink(Heap& h, int32_t head) {
+    for (;;) {
+        const int32_t l = (head + 1) * 2 - 1, r = (head + 1) * 2;
+        if (l >= h.size) return;
+        int32_t c;
+        if (r == h.size || h.data[l] >= h.data[r])
+            c = l;
+        else
+            c = r;
+        if (h.data[head] < h.data[c]) {
+            hp_switch(h, head, c);
+            head = c;
+        } else
+            return;
+    }
+}
+
+__global__ void k_replay(GraphDev g, ReplayDev rp, const int32_t* __restrict__ attached, int32_t A, int32_t njobs) {
+    const int32_t slot = blockIdx.x;
+    if (slot >= njobs || threadIdx.x != 0) return;
+    const int32_t V = g.V;
+    const size_t off = (size_t)slot * V;
+    double* dist = rp.dist + off;
+    int32_t* parent = rp.parent + off;
+    uint8_t* tgt = rp.tgt + off;
+    Heap h{rp.hdata + off, rp.hidx + off, rp.hidx2 + off, 0};
+    for (int32_t v = 0; v < V; ++v) {
+        dist[v] = -1.0;
+        parent[v] = -1;
+        tgt[v] = 0;
+        h.idx2[v] = 0;
+    }
+    int32_t to_reach = A;
+    for (int32_t i = 0; i < A; ++i) {
+        if (!tgt[attached[i]])
+            tgt[attached[i]] = 1;
+        else
+            to_reach--;
+    }
+    const int32_t s = rp.srcv[slot];
+    dist[s] = 0.0;
+    h.data[0] = 0.0;
+    h.idx[0] = s;
+    h.idx2[s] = 2;
+    h.size = 1;
+    while (h.size > 0 && to_reach > 0) {
+        const int32_t minnei = h.idx[0];
+        const double mindist = -h.data[0];
+        hp_switch(h, 0, h.size - 1);
+        h.size--;
+        h.idx2[minnei] = 0;
+        hp_sink(h, 0);
+        if (tgt[minnei]) {
+            tgt[minnei] = 0;
+            to_reach--;
+        }
+        for (int64_t x = g.inc_ptr[minnei]; x < g.inc_ptr[minnei + 1]; ++x) {
+            const int32_t edge = g.inc_eid[x];
+            const int32_t tto = (g.efrom[edge] == minnei) ? g.eto[edge] : g.efrom[edge];
+            const double altdist = mindist + g.elat[edge];
+            const double curdist = dist[tto];
+            if (curdist < 0) {
+                dist[tto] = altdist;
+                parent[tto] = edge;
+                const int32_t pos = h.size++;
+                h.data[pos] = -altdist;
+                h.idx[pos] = tto;
+                h.idx2[tto] = pos + 2;
+                hp_shift_up(h, pos);
+            } else if (altdist < curdist) {
+                dist[tto] = altdist;
+                parent[tto] = edge;
+                const int32_t pos = h.idx2[tto] - 2;
+                h.data[pos] = -altdist;
+                hp_sink(h, pos);
+                hp_shift_up(h, pos);
+            }
+        }
+    }
+}
+
+// pair rows for replayed sources: same dispatch, shortest paths from the exact parents
+__global__ void k_compose_replay(GraphDev g, ReplayDev rp, const int32_t* __restrict__ attached, int32_t A,
+                                 const double* __restrict__ self_lat, const double* __restrict__ self_rel,
+                                 const uint32_t* __restrict__ self_hops, const uint8_t* __restrict__ self_kind,
+                                 double* out_lat, double* out_rel, uint32_t* out_hops, uint8_t* out_kind,
+                                 int32_t row_base) {
+    const int32_t slot = blockIdx.y;
+    const int32_t ti = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ti >= A) return;
+    const int32_t s = rp.srcv[slot];
+    const int32_t t = attached[ti];
+    PairOut o;
+    if (!dispatch_pair(g, s, t, ti, self_lat, self_rel, self_hops, self_kind, o)) {
+        const size_t off = (size_t)slot * g.V;
+        const double* dist = rp.dist + off;
+        const int32_t* parent = rp.parent + off;
+        if (dist[t] >= 0) {
+            // vertex path length
+            uint32_t h = 0;
+            for (int32_t x = t; parent[x] >= 0; ++h) {
+                const int32_t e = parent[x];
+                x = (g.efrom[e] == x) ? g.eto[e] : g.efrom[e];
+            }
+            double lat = 0.0, rel = g.vfac[s] * g.vfac[t];
+            bool ok = true;
+            for (uint32_t i = 0; i < h && ok; ++i) {
+                // hop i: (x_i -> x_{i+1}); walk back from t to x_{i+1}
+                int32_t x = t;
+                for (uint32_t k = 0; k + 1 + i < h; ++k) {
+                    const int32_t e = parent[x];
+                    x = (g.efrom[e] == x) ? g.eto[e] : g.efrom[e];
+                }
+                const int32_t e = parent[x];
+                const int32_t u = (g.efrom[e] == x) ? g.eto[e] : g.efrom[e];
+                const int32_t ge = get_eid(g, u, x);
+                if (ge < 0) {
+                    ok = false;
+                    break;
+                }
+                lat += g.elat[ge];
+                rel *= g.erel[ge];
+            }
+            if (ok) {
+                o.lat = (lat == 0) ? 1.0 : lat;
+                o.rel = rel;
+                o.hops = h;
+                o.kind = SHADOWTOPO_KIND_DIJKSTRA;
+            }
+        }
+    }
+    const size_t w = (size_t)(rp.row[slot] - row_base) * A + ti;
+    out_lat[w] = o.lat;
+    out_rel[w] = o.rel;
+    out_hops[w] = o.hops;
+    if (out_kind) out_kind[w] = o.kind;
+}
+
+// parity tooling: [V][64] -> per-source rows
+__global__ void k_extract(GraphDev g, BatchDev* __restrict__ batches, int32_t nsrc, double* dist, int32_t* pred,
+                          uint32_t* hops, uint8_t* tie) {
+    const int32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t j = blockIdx.y;
+    if (v >= g.V || j >= nsrc) return;
+    BatchDev& B = batches[0];
+    const size_t idx = (size_t)v * KL + j;
+    const size_t o = (size_t)j * g.V + v;
+    dist[o] = B.D[idx];
+    const int32_t p = B.P[idx];
+    pred[o] = p >= 0 ? g.in_src[p] : -1;
+    hops[o] = B.H[idx] & HMASK;
+    tie[o] = (B.H[idx] & TAINT) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- host side
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct shadowtopo_engine {
+    int32_t V = 0;
+    int64_t E = 0;
+    int64_t n_arcs = 0;
+    uint32_t flags = 0;
+    int32_t multigraph = 0;
+    int32_t device = 0;
+    GraphDev g{};
+    std::vector<void*> graph_allocs;
+    // host mirrors for get_eid
+    std::vector<int64_t> h_in_ptr;
+    std::vector<int32_t> h_in_src, h_in_eid, h_loop_eid;
+    hipStream_t own_stream = nullptr;
+    // attached
+    int32_t A = 0;
+    std::vector<int32_t> h_attached;
+    int32_t* d_attached = nullptr;
+    double* d_self_lat = nullptr;
+    double* d_self_rel = nullptr;
+    uint32_t* d_self_hops = nullptr;
+    uint8_t* d_self_kind = nullptr;
+    bool self_ready = false;
+    // batch pool
+    int32_t nb_cap = 0;
+    std::vector<BatchDev> h_batches;
+    BatchDev* d_batches = nullptr;
+    std::vector<void*> batch_allocs;
+    int32_t* d_cnt = nullptr;
+    int32_t* h_cnt = nullptr;  // pinned
+    // staging for host outputs
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+    // replay scratch
+    ReplayDev rp{};
+    bool rp_ready = false;
+    std::vector<void*> rp_allocs;
+    // options
+    int32_t opt_nb = 0;
+    int32_t opt_timing = 0;
+    int64_t opt_max_rounds = 0;
+    int32_t opt_force_replay = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    shadowtopo_stats st{};
+};
+
+namespace {
+
+int dev_alloc(std::vector<void*>& owner, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 8;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(SHADOWTOPO_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    owner.push_back(*p);
+    return SHADOWTOPO_OK;
+}
+
+template <typename T>
+int upload(shadowtopo_engine* eng, const std::vector<T>& h, const T** out) {
+    void* p = nullptr;
+    int rc = dev_alloc(eng->graph_allocs, &p, h.size() * sizeof(T));
+    if (rc) return rc;
+    if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = static_cast<const T*>(p);
+    return SHADOWTOPO_OK;
+}
+
+// stable counting sort of `idx` by key[idx]
+void counting_sort(const std::vector<int32_t>& key, int32_t nkeys, std::vector<int64_t>& idx,
+                   std::vector<int64_t>& tmp) {
+    std::vector<int64_t> cnt((size_t)nkeys + 1, 0);
+    for (int64_t i : idx) cnt[(size_t)key[i] + 1]++;
+    for (int32_t k = 0; k < nkeys; ++k) cnt[(size_t)k + 1] += cnt[k];
+    tmp.resize(idx.size());
+    for (int64_t i : idx) tmp[(size_t)cnt[key[i]]++] = i;
+    idx.swap(tmp);
+}
+
+void free_batches(shadowtopo_engine* eng) {
+    for (void* p : eng->batch_allocs) (void)hipFree(p);
+    eng->batch_allocs.clear();
+    eng->d_batches = nullptr;
+    eng->d_cnt = nullptr;
+    if (eng->h_cnt) (void)hipHostFree(eng->h_cnt);
+    eng->h_cnt = nullptr;
+    eng->h_batches.clear();
+    eng->nb_cap = 0;
+}
+
+int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
+    if (eng->nb_cap >= nb) return SHADOWTOPO_OK;
+    free_batches(eng);
+    const size_t VK = (size_t)eng->V * KL;
+    eng->h_batches.assign(nb, BatchDev{});
+    for (int32_t b = 0; b < nb; ++b) {
+        BatchDev& B = eng->h_batches[b];
+        int rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.D, VK * sizeof(double)))) return rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.H, VK * sizeof(uint32_t)))) return rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.R, VK * sizeof(double)))) return rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.P, VK * sizeof(int32_t)))) return rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.act[0], (size_t)eng->V))) return rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.act[1], (size_t)eng->V))) return rc;
+        for (int j = 0; j < KL; ++j) {
+            B.srcv[j] = -1;
+            B.row[j] = -1;
+        }
+    }
+    int rc;
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_batches, sizeof(BatchDev) * nb))) return rc;
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * nb))) return rc;
+    HIP_TRY(hipHostMalloc((void**)&eng->h_cnt, sizeof(int32_t) * nb, hipHostMallocDefault));
+    eng->nb_cap = nb;
+    return SHADOWTOPO_OK;
+}
+
+int ensure_replay(shadowtopo_engine* eng) {
+    if (eng->rp_ready) return SHADOWTOPO_OK;
+    const size_t n = (size_t)REPLAY_SLOTS * eng->V;
+    ReplayDev& r = eng->rp;
+    int rc;
+    if ((rc = dev_alloc(eng->rp_allocs, (void**)&r.dist, n * sizeof(double)))) return rc;
+    if ((rc = dev_alloc(eng->rp_allocs, (void**)&r.parent, n * sizeof(int32_t)))) return rc;
+    if ((rc = dev_alloc(eng->rp_allocs, (void**)&r.hdata, n * sizeof(double)))) return rc;
+    if ((rc = dev_alloc(eng->rp_allocs, (void**)&r.hidx, n * sizeof(int32_t)))) return rc;
+    if ((rc = dev_alloc(eng->rp_allocs, (void**)&r.hidx2, n * sizeof(int32_t)))) return rc;
+    if ((rc = dev_alloc(eng->rp_allocs, (void**)&r.tgt, n))) return rc;
+    eng->rp_ready = true;
+    return SHADOWTOPO_OK;
+}
+
+int32_t default_nb(const shadowtopo_engine* eng) {
+    if (eng->opt_nb > 0) return eng->opt_nb;
+    const double per_batch = (double)eng->V * KL * 24.0 + 2.0 * eng->V;
+    const double budget = 24.0e9;
+    int32_t nb = (int32_t)std::max(1.0, std::min(16.0, std::floor(budget / per_batch)));
+    return nb;
+}
+
+int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
+    if (eng->self_ready) return SHADOWTOPO_OK;
+    if (eng->A > 0) {
+        hipLaunchKernelGGL(k_self, dim3((eng->A + 255) / 256), dim3(256), 0, s, eng->g, eng->d_attached, eng->A,
+                           eng->d_self_lat, eng->d_self_rel, eng->d_self_hops, eng->d_self_kind);
+        HIP_TRY(hipGetLastError());
+    }
+    eng->self_ready = true;
+    return SHADOWTOPO_OK;
+}
+
+// relax rounds for the batch slots [0, nbg) until no vertex changes
+int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
+    const int32_t V = eng->V;
+    const GraphDev& g = eng->g;
+    {
+        const size_t total = (size_t)V * KL;
+        int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->d_batches, V);
+        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->d_batches);
+        HIP_TRY(hipGetLastError());
+    }
+    const int32_t nvb = (V + 3) / 4;
+    const int64_t nblocks = (int64_t)8 * nvb * ((nbg + 7) / 8);
+    if (nblocks > 0x7fffffff) return fail(SHADOWTOPO_EINVAL, "grid too large");
+    const int64_t max_rounds = eng->opt_max_rounds > 0 ? eng->opt_max_rounds : 4LL * V + 64;
+    for (int64_t round = 0;; ++round) {
+        if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
+                                            (long long)max_rounds);
+        HIP_TRY(hipMemsetAsync(eng->d_cnt, 0, sizeof(int32_t) * nbg, s));
+        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
+        hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
+                           g.out_ptr, g.out_dst, eng->d_batches, V, nbg, nvb, (int32_t)(round & 1), eng->d_cnt);
+        HIP_TRY(hipGetLastError());
+        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev1, s));
+        HIP_TRY(hipMemcpyAsync(eng->h_cnt, eng->d_cnt, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        eng->st.relax_launches++;
+        eng->st.rounds++;
+        if (eng->opt_timing) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
+            eng->st.relax_ms += ms;
+        }
+        int64_t changed = 0;
+        for (int32_t b = 0; b < nbg; ++b) changed += eng->h_cnt[b];
+        if (changed == 0) break;
+    }
+    return SHADOWTOPO_OK;
+}
+
+int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
+                      uint32_t* hops, uint8_t* kind, int32_t mem, hipStream_t s) {
+    const int32_t A = eng->A;
+    const bool complete = (eng->flags & SHADOWTOPO_F_COMPLETE) != 0;
+    int rc;
+    if ((rc = ensure_self(eng, s))) return rc;
+    const int32_t nb = default_nb(eng);
+    if ((rc = ensure_batches(eng, nb))) return rc;
+    const int32_t group = nb * KL;
+    // device destinations (user buffers or staging)
+    double *dl = lat, *dr = rel;
+    uint32_t* dh = hops;
+    uint8_t* dk = kind;
+    if (mem == SHADOWTOPO_MEM_HOST) {
+        const size_t need = (size_t)group * A * (8 + 8 + 4 + 1) + 64;
+        if (eng->stage_bytes < need) {
+            if (eng->stage) (void)hipFree(eng->stage);
+            eng->stage = nullptr;
+            eng->stage_bytes = 0;
+            HIP_TRY(hipMalloc(&eng->stage, need));
+            eng->stage_bytes = need;
+        }
+    }
+    for (int32_t r0 = row_begin; r0 < row_end; r0 += group) {
+        const int32_t r1 = std::min(row_end, r0 + group);
+        const int32_t nbg = (r1 - r0 + KL - 1) / KL;
+        int32_t row_base = row_begin;
+        if (mem == SHADOWTOPO_MEM_HOST) {
+            char* p = static_cast<char*>(eng->stage);
+            const size_t n = (size_t)group * A;
+            dl = reinterpret_cast<double*>(p);
+            dr = reinterpret_cast<double*>(p + n * 8);
+            dh = reinterpret_cast<uint32_t*>(p + n * 16);
+            dk = kind ? reinterpret_cast<uint8_t*>(p + n * 20) : nullptr;
+            row_base = r0;
+        }
+        for (int32_t b = 0; b < nbg; ++b) {
+            BatchDev& B = eng->h_batches[b];
+            for (int j = 0; j < KL; ++j) {
+                const int32_t row = r0 + b * KL + j;
+                B.srcv[j] = row < r1 ? eng->h_attached[row] : -1;
+                B.row[j] = row < r1 ? row : -1;
+            }
+            B.replay_mask = 0;
+        }
+        HIP_TRY(hipMemcpyAsync(eng->d_batches, eng->h_batches.data(), sizeof(BatchDev) * nbg,
+                               hipMemcpyHostToDevice, s));
+        if (!complete) {
+            if ((rc = run_rounds(eng, nbg, s))) return rc;
+        }
+        auto t0 = std::chrono::steady_clock::now();
+        if (A > 0) {
+            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(256), 0, s, eng->g, eng->d_batches,
+                               eng->d_attached, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
+                               eng->d_self_kind, dl, dr, dh, dk, row_base);
+            HIP_TRY(hipGetLastError());
+        }
+        // collect tie-tainted sources
+        std::vector<unsigned long long> masks(nbg);
+        for (int32_t b = 0; b < nbg; ++b)
+            HIP_TRY(hipMemcpyAsync(&masks[b], &eng->d_batches[b].replay_mask, sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        eng->st.compose_ms +=
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::vector<std::pair<int32_t, int32_t>> jobs;  // (vertex, row)
+        for (int32_t b = 0; b < nbg; ++b) {
+            for (int j = 0; j < KL; ++j) {
+                const int32_t row = r0 + b * KL + j;
+                if (row >= r1) continue;
+                if (complete) continue;
+                if (eng->opt_force_replay || (masks[b] >> j) & 1ull) jobs.emplace_back(eng->h_attached[row], row);
+            }
+        }
+        if (!jobs.empty()) {
+            auto t1 = std::chrono::steady_clock::now();
+            if ((rc = ensure_replay(eng))) return rc;
+            for (size_t k0 = 0; k0 < jobs.size(); k0 += REPLAY_SLOTS) {
+                const int32_t nj = (int32_t)std::min<size_t>(REPLAY_SLOTS, jobs.size() - k0);
+                for (int32_t k = 0; k < nj; ++k) {
+                    eng->rp.srcv[k] = jobs[k0 + k].first;
+                    eng->rp.row[k] = jobs[k0 + k].second;
+                }
+                hipLaunchKernelGGL(k_replay, dim3(nj), dim3(64), 0, s, eng->g, eng->rp, eng->d_attached, A, nj);
+                HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(k_compose_replay, dim3((A + 255) / 256, nj), dim3(256), 0, s, eng->g, eng->rp,
+                                   eng->d_attached, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
+                                   eng->d_self_kind, dl, dr, dh, dk, row_base);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipStreamSynchronize(s));
+            eng->st.replayed_sources += (int64_t)jobs.size();
+            eng->st.replay_ms +=
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        }
+        if (mem == SHADOWTOPO_MEM_HOST) {
+            const size_t n = (size_t)(r1 - r0) * A;
+            const size_t o = (size_t)(r0 - row_begin) * A;
+            HIP_TRY(hipMemcpyAsync(lat + o, dl, n * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(rel + o, dr, n * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(hops + o, dh, n * 4, hipMemcpyDeviceToHost, s));
+            if (kind) HIP_TRY(hipMemcpyAsync(kind + o, dk, n, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        eng->st.sources += r1 - r0;
+        eng->st.batches += nbg;
+    }
+    return SHADOWTOPO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int shadowtopo_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* shadowtopo_last_error(void) { return g_err.c_str(); }
+
+int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_source, const int32_t* edge_target,
+                      const double* edge_latency, const double* edge_packetloss, const double* vertex_packetloss,
+                      uint32_t flags, int32_t device, shadowtopo_engine** out) {
+    if (!out) return fail(SHADOWTOPO_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (n_vertices <= 0 || n_edges < 0) return fail(SHADOWTOPO_EINVAL, "empty graph");
+    if (n_edges > 0 && (!edge_source || !edge_target || !edge_latency || !edge_packetloss))
+        return fail(SHADOWTOPO_EINVAL, "NULL edge array");
+    const int32_t V = n_vertices;
+    const bool directed = flags & SHADOWTOPO_F_DIRECTED;
+    for (int64_t e = 0; e < n_edges; ++e) {
+        if (edge_source[e] < 0 || edge_source[e] >= V || edge_target[e] < 0 || edge_target[e] >= V)
+            return fail(SHADOWTOPO_EINVAL, "edge %lld endpoint out of range", (long long)e);
+        if (!(edge_latency[e] > 0.0) || std::isinf(edge_latency[e]))
+            return fail(SHADOWTOPO_EINVAL, "edge %lld latency must be > 0 (topology.c:1070)", (long long)e);
+        if (!(edge_packetloss[e] >= 0.0 && edge_packetloss[e] <= 1.0))
+            return fail(SHADOWTOPO_EINVAL, "edge %lld packetloss out of [0,1] (topology.c:1090)", (long long)e);
+    }
+    int ndev = shadowtopo_device_count();
+    if (ndev <= 0) return fail(SHADOWTOPO_EDEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(SHADOWTOPO_EINVAL, "device %d out of range", device);
+    HIP_TRY(hipSetDevice(device));
+
+    auto* eng = new (std::nothrow) shadowtopo_engine();
+    if (!eng) return fail(SHADOWTOPO_ENOMEM, "engine alloc");
+    eng->V = V;
+    eng->E = n_edges;
+    eng->device = device;
+
+    // igraph storage of the edges
+    std::vector<int32_t> efrom(n_edges), eto(n_edges);
+    std::vector<double> elat(edge_latency, edge_latency + n_edges), erel(n_edges);
+    for (int64_t e = 0; e < n_edges; ++e) {
+        int32_t a = edge_source[e], b = edge_target[e];
+        if (directed || a > b) {
+            efrom[e] = a;
+            eto[e] = b;
+        } else {
+            efrom[e] = b;
+            eto[e] = a;
+        }
+        erel[e] = 1.0 - edge_packetloss[e];
+    }
+    std::vector<double> vfac(V, 1.0);
+    if (vertex_packetloss)
+        for (int32_t v = 0; v < V; ++v)
+            if (!std::isnan(vertex_packetloss[v])) vfac[v] = 1.0 - vertex_packetloss[v];
+    std::vector<int32_t> loop_eid(V, -1);
+    for (int64_t e = n_edges - 1; e >= 0; --e)
+        if (efrom[e] == eto[e]) loop_eid[efrom[e]] = (int32_t)e;
+
+    // relaxation in-CSR: arcs (u -> v) sorted by (v, u, eid), parallel arcs merged
+    std::vector<int32_t> au, av;
+    std::vector<int32_t> ae;
+    au.reserve((size_t)n_edges * (directed ? 1 : 2));
+    for (int64_t e = 0; e < n_edges; ++e) {
+        if (efrom[e] == eto[e]) continue;
+        au.push_back(efrom[e]);
+        av.push_back(eto[e]);
+        ae.push_back((int32_t)e);
+        if (!directed) {
+            au.push_back(eto[e]);
+            av.push_back(efrom[e]);
+            ae.push_back((int32_t)e);
+        }
+    }
+    if (au.size() >= 0x7fffffffULL) {
+        delete eng;
+        return fail(SHADOWTOPO_EINVAL, "too many arcs");
+    }
+    // arcs were generated in eid order: stable sort by u, then by v
+    {
+        std::vector<int64_t> idx(au.size()), tmp;
+        for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
+        counting_sort(au, V, idx, tmp);
+        counting_sort(av, V, idx, tmp);
+        std::vector<int32_t> su(idx.size()), sv(idx.size()), se(idx.size());
+        for (size_t i = 0; i < idx.size(); ++i) {
+            su[i] = au[idx[i]];
+            sv[i] = av[idx[i]];
+            se[i] = ae[idx[i]];
+        }
+        au.swap(su);
+        av.swap(sv);
+        ae.swap(se);
+    }
+    std::vector<int64_t> in_ptr(V + 1, 0);
+    std::vector<int32_t> in_src;
+    std::vector<double> in_w, in_r;
+    std::vector<int32_t> in_eid;
+    in_src.reserve(au.size());
+    in_w.reserve(au.size());
+    in_r.reserve(au.size());
+    in_eid.reserve(au.size());
+    int32_t multigraph = 0;
+    for (size_t i = 0; i < au.size();) {
+        size_t j = i;
+        double w = elat[ae[i]];
+        while (j + 1 < au.size() && av[j + 1] == av[i] && au[j + 1] == au[i]) {
+            ++j;
+            w = std::min(w, elat[ae[j]]);
+        }
+        const int32_t low = ae[i];  // lowest eid of the run (stable order)
+        if (w != elat[low]) multigraph = 1;
+        in_src.push_back(au[i]);
+        in_w.push_back(w);
+        in_r.push_back(erel[low]);
+        in_eid.push_back(low);
+        in_ptr[(size_t)av[i] + 1]++;
+        i = j + 1;
+    }
+    for (int32_t v = 0; v < V; ++v) in_ptr[(size_t)v + 1] += in_ptr[v];
+    std::vector<int64_t> out_ptr;
+    std::vector<int32_t> out_dst;
+    if (directed) {
+        out_ptr.assign((size_t)V + 1, 0);
+        for (int32_t v = 0; v < V; ++v)
+            for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) out_ptr[(size_t)in_src[x] + 1]++;
+        for (int32_t v = 0; v < V; ++v) out_ptr[(size_t)v + 1] += out_ptr[v];
+        out_dst.resize(in_src.size());
+        std::vector<int64_t> fill(out_ptr.begin(), out_ptr.end() - 1);
+        for (int32_t v = 0; v < V; ++v)
+            for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) out_dst[(size_t)fill[in_src[x]]++] = v;
+    }
+    // igraph_incident(OUT) order: edges with from==v by (to, eid), then (undirected) edges
+    // with to==v by (from, eid)
+    std::vector<int64_t> inc_ptr(V + 1, 0);
+    std::vector<int32_t> inc_eid;
+    {
+        std::vector<int64_t> oi(n_edges), ii, tmp;
+        for (int64_t e = 0; e < n_edges; ++e) oi[e] = e;
+        ii = oi;
+        counting_sort(eto, V, oi, tmp);
+        counting_sort(efrom, V, oi, tmp);
+        if (!directed) {
+            counting_sort(efrom, V, ii, tmp);
+            counting_sort(eto, V, ii, tmp);
+        }
+        std::vector<int64_t> os(V + 1, 0), is(V + 1, 0);
+        for (int64_t e = 0; e < n_edges; ++e) {
+            os[(size_t)efrom[e] + 1]++;
+            is[(size_t)eto[e] + 1]++;
+        }
+        for (int32_t v = 0; v < V; ++v) {
+            os[(size_t)v + 1] += os[v];
+            is[(size_t)v + 1] += is[v];
+        }
+        for (int32_t v = 0; v < V; ++v) {
+            int64_t d = os[(size_t)v + 1] - os[v];
+            if (!directed) d += is[(size_t)v + 1] - is[v];
+            inc_ptr[(size_t)v + 1] = inc_ptr[v] + d;
+        }
+        inc_eid.resize((size_t)inc_ptr[V]);
+        for (int32_t v = 0; v < V; ++v) {
+            int64_t k = inc_ptr[v];
+            for (int64_t x = os[v]; x < os[(size_t)v + 1]; ++x) inc_eid[(size_t)k++] = (int32_t)oi[x];
+            if (!directed)
+                for (int64_t x = is[v]; x < is[(size_t)v + 1]; ++x) inc_eid[(size_t)k++] = (int32_t)ii[x];
+        }
+    }
+    // completeness, topology.c:450-552
+    if (flags & SHADOWTOPO_F_AUTO_COMPLETE) {
+        bool complete = true;
+        for (int32_t v = 0; v < V && complete; ++v) {
+            int64_t ecount = inc_ptr[(size_t)v + 1] - inc_ptr[v];
+            if (!directed && loop_eid[v] >= 0) ecount -= 1;
+            if (ecount < V) complete = false;
+        }
+        flags = (flags & ~SHADOWTOPO_F_COMPLETE) | (complete ? SHADOWTOPO_F_COMPLETE : 0u);
+    }
+    eng->flags = flags;
+    eng->multigraph = multigraph;
+    eng->n_arcs = (int64_t)in_src.size();
+
+    GraphDev& g = eng->g;
+    g.V = V;
+    g.flags = flags;
+    g.multigraph = multigraph;
+    int rc = 0;
+    if ((rc = upload(eng, in_ptr, &g.in_ptr)) || (rc = upload(eng, in_src, &g.in_src)) ||
+        (rc = upload(eng, in_w, &g.in_w)) || (rc = upload(eng, in_r, &g.in_r)) ||
+        (rc = upload(eng, in_eid, &g.in_eid)) || (rc = upload(eng, inc_ptr, &g.inc_ptr)) ||
+        (rc = upload(eng, inc_eid, &g.inc_eid)) || (rc = upload(eng, efrom, &g.efrom)) ||
+        (rc = upload(eng, eto, &g.eto)) || (rc = upload(eng, elat, &g.elat)) || (rc = upload(eng, erel, &g.erel)) ||
+        (rc = upload(eng, vfac, &g.vfac)) || (rc = upload(eng, loop_eid, &g.loop_eid))) {
+        shadowtopo_destroy(eng);
+        return rc;
+    }
+    if (directed) {
+        if ((rc = upload(eng, out_ptr, &g.out_ptr)) || (rc = upload(eng, out_dst, &g.out_dst))) {
+            shadowtopo_destroy(eng);
+            return rc;
+        }
+    } else {
+        g.out_ptr = g.in_ptr;
+        g.out_dst = g.in_src;
+    }
+    eng->h_in_ptr.swap(in_ptr);
+    eng->h_in_src.swap(in_src);
+    eng->h_in_eid.swap(in_eid);
+    eng->h_loop_eid.swap(loop_eid);
+    if (hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess) {
+        shadowtopo_destroy(eng);
+        return fail(SHADOWTOPO_EDEVICE, "stream/event create failed");
+    }
+    eng->st.n_vertices = V;
+    eng->st.n_edges = n_edges;
+    eng->st.n_arcs = eng->n_arcs;
+    eng->st.device = device;
+    eng->st.multigraph = multigraph;
+    *out = eng;
+    return SHADOWTOPO_OK;
+}
+
+void shadowtopo_destroy(shadowtopo_engine* eng) {
+    if (!eng) return;
+    (void)hipSetDevice(eng->device);
+    if (eng->own_stream) (void)hipStreamSynchronize(eng->own_stream);
+    free_batches(eng);
+    for (void* p : eng->graph_allocs) (void)hipFree(p);
+    for (void* p : eng->rp_allocs) (void)hipFree(p);
+    if (eng->d_attached) (void)hipFree(eng->d_attached);
+    if (eng->d_self_lat) (void)hipFree(eng->d_self_lat);
+    if (eng->d_self_rel) (void)hipFree(eng->d_self_rel);
+    if (eng->d_self_hops) (void)hipFree(eng->d_self_hops);
+    if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
+    if (eng->stage) (void)hipFree(eng->stage);
+    if (eng->ev0) (void)hipEventDestroy(eng->ev0);
+    if (eng->ev1) (void)hipEventDestroy(eng->ev1);
+    if (eng->own_stream) (void)hipStreamDestroy(eng->own_stream);
+    delete eng;
+}
+
+int shadowtopo_set_attached(shadowtopo_engine* eng, const int32_t* attached, int32_t count) {
+    if (!eng || count < 0 || (count > 0 && !attached)) return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    for (int32_t i = 0; i < count; ++i)
+        if (attached[i] < 0 || attached[i] >= eng->V) return fail(SHADOWTOPO_EINVAL, "attached[%d] out of range", i);
+    HIP_TRY(hipSetDevice(eng->device));
+    HIP_TRY(hipStreamSynchronize(eng->own_stream));
+    if (eng->d_attached) (void)hipFree(eng->d_attached);
+    if (eng->d_self_lat) (void)hipFree(eng->d_self_lat);
+    if (eng->d_self_rel) (void)hipFree(eng->d_self_rel);
+    if (eng->d_self_hops) (void)hipFree(eng->d_self_hops);
+    if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
+    eng->d_attached = nullptr;
+    eng->d_self_lat = eng->d_self_rel = nullptr;
+    eng->d_self_hops = nullptr;
+    eng->d_self_kind = nullptr;
+    eng->h_attached.assign(attached, attached + count);
+    eng->A = count;
+    const size_t n = (size_t)std::max(count, 1);
+    HIP_TRY(hipMalloc((void**)&eng->d_attached, n * sizeof(int32_t)));
+    HIP_TRY(hipMalloc((void**)&eng->d_self_lat, n * sizeof(double)));
+    HIP_TRY(hipMalloc((void**)&eng->d_self_rel, n * sizeof(double)));
+    HIP_TRY(hipMalloc((void**)&eng->d_self_hops, n * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&eng->d_self_kind, n));
+    if (count > 0)
+        HIP_TRY(hipMemcpy(eng->d_attached, attached, sizeof(int32_t) * count, hipMemcpyHostToDevice));
+    eng->self_ready = false;
+    eng->st.n_attached = count;
+    return SHADOWTOPO_OK;
+}
+
+int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
+    if (!eng) return fail(SHADOWTOPO_EINVAL, "NULL engine");
+    switch (key) {
+        case SHADOWTOPO_OPT_BATCHES_IN_FLIGHT:
+            if (value < 0 || value > 64) return fail(SHADOWTOPO_EINVAL, "batches in flight out of range");
+            eng->opt_nb = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_TIMING:
+            eng->opt_timing = value ? 1 : 0;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_MAX_ROUNDS:
+            eng->opt_max_rounds = value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_FORCE_REPLAY:
+            eng->opt_force_replay = value ? 1 : 0;
+            return SHADOWTOPO_OK;
+        default:
+            return fail(SHADOWTOPO_EINVAL, "unknown option %d", key);
+    }
+}
+
+int shadowtopo_compute_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
+                            uint32_t* hops, uint8_t* kind, int32_t mem, void* stream) {
+    if (!eng) return fail(SHADOWTOPO_EINVAL, "NULL engine");
+    if (!eng->d_attached) return fail(SHADOWTOPO_ESTATE, "shadowtopo_set_attached not called");
+    if (row_begin < 0 || row_end > eng->A || row_begin > row_end) return fail(SHADOWTOPO_EINVAL, "bad row range");
+    if (row_begin == row_end) return SHADOWTOPO_OK;
+    if (!lat || !rel || !hops) return fail(SHADOWTOPO_EINVAL, "NULL output");
+    if (mem != SHADOWTOPO_MEM_HOST && mem != SHADOWTOPO_MEM_DEVICE) return fail(SHADOWTOPO_EINVAL, "bad mem kind");
+    HIP_TRY(hipSetDevice(eng->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = compute_rows_impl(eng, row_begin, row_end, lat, rel, hops, kind, mem, s);
+    eng->st.wall_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_sources, double* dist, int32_t* pred,
+                    uint32_t* hops, uint8_t* tie) {
+    if (!eng || n_sources < 0 || (n_sources > 0 && !sources)) return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    for (int32_t i = 0; i < n_sources; ++i)
+        if (sources[i] < 0 || sources[i] >= eng->V) return fail(SHADOWTOPO_EINVAL, "source out of range");
+    HIP_TRY(hipSetDevice(eng->device));
+    hipStream_t s = eng->own_stream;
+    int rc;
+    if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
+    const size_t V = (size_t)eng->V;
+    double* d_dist = nullptr;
+    int32_t* d_pred = nullptr;
+    uint32_t* d_hops = nullptr;
+    uint8_t* d_tie = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_dist, KL * V * 8));
+    HIP_TRY(hipMalloc((void**)&d_pred, KL * V * 4));
+    HIP_TRY(hipMalloc((void**)&d_hops, KL * V * 4));
+    HIP_TRY(hipMalloc((void**)&d_tie, KL * V));
+    for (int32_t i0 = 0; i0 < n_sources && rc == 0; i0 += KL) {
+        const int32_t n = std::min(KL, n_sources - i0);
+        BatchDev& B = eng->h_batches[0];
+        for (int j = 0; j < KL; ++j) {
+            B.srcv[j] = j < n ? sources[i0 + j] : -1;
+            B.row[j] = -1;
+        }
+        B.replay_mask = 0;
+        if (hipMemcpyAsync(eng->d_batches, &B, sizeof(BatchDev), hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
+            break;
+        }
+        if ((rc = run_rounds(eng, 1, s))) break;
+        hipLaunchKernelGGL(k_extract, dim3((eng->V + 255) / 256, n), dim3(256), 0, s, eng->g, eng->d_batches, n,
+                           d_dist, d_pred, d_hops, d_tie);
+        const size_t cnt = (size_t)n * V;
+        const size_t o = (size_t)i0 * V;
+        bool ok = hipGetLastError() == hipSuccess;
+        if (ok && dist) ok = hipMemcpyAsync(dist + o, d_dist, cnt * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (ok && pred) ok = hipMemcpyAsync(pred + o, d_pred, cnt * 4, hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (ok && hops) ok = hipMemcpyAsync(hops + o, d_hops, cnt * 4, hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (ok && tie) ok = hipMemcpyAsync(tie + o, d_tie, cnt, hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (ok) ok = hipStreamSynchronize(s) == hipSuccess;
+        if (!ok) rc = fail(SHADOWTOPO_EDEVICE, "sssp extract failed");
+    }
+    (void)hipFree(d_dist);
+    (void)hipFree(d_pred);
+    (void)hipFree(d_hops);
+    (void)hipFree(d_tie);
+    return rc;
+}
+
+int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out) {
+    if (!eng || !out) return fail(SHADOWTOPO_EINVAL, "NULL argument");
+    *out = eng->st;
+    return SHADOWTOPO_OK;
+}
+
+void shadowtopo_reset_stats(shadowtopo_engine* eng) {
+    if (!eng) return;
+    shadowtopo_stats keep = eng->st;
+    eng->st = shadowtopo_stats{};
+    eng->st.n_vertices = keep.n_vertices;
+    eng->st.n_edges = keep.n_edges;
+    eng->st.n_arcs = keep.n_arcs;
+    eng->st.n_attached = keep.n_attached;
+    eng->st.device = keep.device;
+    eng->st.multigraph = keep.multigraph;
+}
+
+int shadowtopo_is_complete(const shadowtopo_engine* eng) {
+    return eng && (eng->flags & SHADOWTOPO_F_COMPLETE) ? 1 : 0;
+}
+
+int64_t shadowtopo_get_eid(const shadowtopo_engine* eng, int32_t from, int32_t to) {
+    if (!eng || from < 0 || to < 0 || from >= eng->V || to >= eng->V) return -1;
+    if (from == to) return eng->h_loop_eid[from];
+    const int64_t b = eng->h_in_ptr[to], e = eng->h_in_ptr[(size_t)to + 1];
+    auto it = std::lower_bound(eng->h_in_src.begin() + b, eng->h_in_src.begin() + e, from);
+    if (it == eng->h_in_src.begin() + e || *it != from) return -1;
+    return eng->h_in_eid[(size_t)(it - eng->h_in_src.begin())];
+}
+
+}  // extern "C"

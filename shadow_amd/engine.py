@@ -1,0 +1,205 @@
+"""ctypes binding of libshadowtopo_hip (include/shadowtopo.h).
+
+This is the Python-side mirror a maintainer would use to drive the engine (the C host
+shim, topology_hip.c, is the drop-in for Shadow itself).  There is no CPU fallback:
+if the HIP library is missing or no GPU is visible every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libshadowtopo_hip.so")
+
+F_DIRECTED = 0x1
+F_COMPLETE = 0x2
+F_PREFER_DIRECT = 0x4
+F_SELF_DIJKSTRA_LOOP = 0x8
+F_AUTO_COMPLETE = 0x10
+
+MEM_HOST = 0
+MEM_DEVICE = 1
+
+KIND_NONE, KIND_DIRECT, KIND_SELF, KIND_DIJKSTRA = 0, 1, 2, 3
+
+OPT_BATCHES_IN_FLIGHT = 1
+OPT_TIMING = 2
+OPT_MAX_ROUNDS = 3
+OPT_FORCE_REPLAY = 4
+
+# every symbol include/shadowtopo.h declares
+ENGINE_SYMBOLS = (
+    "shadowtopo_device_count", "shadowtopo_last_error", "shadowtopo_create", "shadowtopo_destroy",
+    "shadowtopo_set_attached", "shadowtopo_set_option", "shadowtopo_compute_rows", "shadowtopo_sssp",
+    "shadowtopo_get_stats", "shadowtopo_reset_stats", "shadowtopo_is_complete", "shadowtopo_get_eid",
+)
+
+
+class ShadowTopoError(RuntimeError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("n_vertices", ctypes.c_int64), ("n_edges", ctypes.c_int64), ("n_arcs", ctypes.c_int64),
+        ("n_attached", ctypes.c_int64), ("sources", ctypes.c_int64), ("batches", ctypes.c_int64),
+        ("rounds", ctypes.c_int64), ("relax_launches", ctypes.c_int64), ("replayed_sources", ctypes.c_int64),
+        ("tainted_pairs", ctypes.c_int64), ("relax_ms", ctypes.c_double), ("compose_ms", ctypes.c_double),
+        ("replay_ms", ctypes.c_double), ("wall_ms", ctypes.c_double), ("device", ctypes.c_int32),
+        ("multigraph", ctypes.c_int32),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+
+
+def lib():
+    """Load the in-tree HIP library (built by __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ShadowTopoError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        vp = ctypes.c_void_p
+        L.shadowtopo_device_count.restype = ctypes.c_int
+        L.shadowtopo_last_error.restype = ctypes.c_char_p
+        L.shadowtopo_create.restype = ctypes.c_int
+        L.shadowtopo_create.argtypes = [ctypes.c_int32, ctypes.c_int64, vp, vp, vp, vp, vp, ctypes.c_uint32,
+                                        ctypes.c_int32, ctypes.POINTER(vp)]
+        L.shadowtopo_destroy.argtypes = [vp]
+        L.shadowtopo_set_attached.argtypes = [vp, vp, ctypes.c_int32]
+        L.shadowtopo_set_option.argtypes = [vp, ctypes.c_int32, ctypes.c_int64]
+        L.shadowtopo_compute_rows.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int32, vp]
+        L.shadowtopo_sssp.argtypes = [vp, vp, ctypes.c_int32, vp, vp, vp, vp]
+        L.shadowtopo_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+        L.shadowtopo_reset_stats.argtypes = [vp]
+        L.shadowtopo_is_complete.argtypes = [vp]
+        L.shadowtopo_get_eid.restype = ctypes.c_int64
+        L.shadowtopo_get_eid.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().shadowtopo_last_error()
+        raise ShadowTopoError(f"shadowtopo error {rc}: {msg.decode() if msg else ''}")
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count():
+    return int(lib().shadowtopo_device_count())
+
+
+class Engine:
+    """Device-resident topology graph + attached-pair computation."""
+
+    def __init__(self, n, src, dst, latency, packetloss, vertex_packetloss=None, directed=False,
+                 prefer_direct=False, complete=None, self_dijkstra_loop=False, device=0):
+        L = lib()
+        self._keep = []
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        lat = np.ascontiguousarray(latency, np.float64)
+        loss = np.ascontiguousarray(packetloss, np.float64)
+        vl = None if vertex_packetloss is None else np.ascontiguousarray(vertex_packetloss, np.float64)
+        flags = 0
+        if directed:
+            flags |= F_DIRECTED
+        if prefer_direct:
+            flags |= F_PREFER_DIRECT
+        if self_dijkstra_loop:
+            flags |= F_SELF_DIJKSTRA_LOOP
+        if complete is None:
+            flags |= F_AUTO_COMPLETE
+        elif complete:
+            flags |= F_COMPLETE
+        h = ctypes.c_void_p()
+        _check(L.shadowtopo_create(int(n), len(src), _ptr(src), _ptr(dst), _ptr(lat), _ptr(loss), _ptr(vl), flags,
+                                   int(device), ctypes.byref(h)))
+        self._h = h
+        self.n = int(n)
+        self.device = int(device)
+        self.A = 0
+
+    @classmethod
+    def from_synth(cls, g, device=0, **kw):
+        return cls(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss, directed=g.directed,
+                   prefer_direct=g.prefer_direct, device=device, **kw)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().shadowtopo_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def complete(self):
+        return bool(lib().shadowtopo_is_complete(self._h))
+
+    def get_eid(self, a, b):
+        return int(lib().shadowtopo_get_eid(self._h, int(a), int(b)))
+
+    def set_attached(self, attached):
+        att = np.ascontiguousarray(attached, np.int32)
+        _check(lib().shadowtopo_set_attached(self._h, _ptr(att), len(att)))
+        self.A = len(att)
+        self.attached = att
+
+    def set_option(self, key, value):
+        _check(lib().shadowtopo_set_option(self._h, int(key), int(value)))
+
+    def compute_rows(self, row_begin=0, row_end=None, want_kind=True):
+        """host numpy outputs: lat, rel, hops, kind for rows [row_begin, row_end)"""
+        if row_end is None:
+            row_end = self.A
+        R = row_end - row_begin
+        lat = np.empty((R, self.A), np.float64)
+        rel = np.empty((R, self.A), np.float64)
+        hops = np.empty((R, self.A), np.uint32)
+        kind = np.empty((R, self.A), np.uint8) if want_kind else None
+        _check(lib().shadowtopo_compute_rows(self._h, int(row_begin), int(row_end), _ptr(lat), _ptr(rel), _ptr(hops),
+                                             _ptr(kind), MEM_HOST, None))
+        return lat, rel, hops, kind
+
+    def compute_rows_device(self, row_begin, row_end, lat_ptr, rel_ptr, hops_ptr, kind_ptr=None, stream=None):
+        """device outputs (raw pointers, e.g. torch tensors' data_ptr()) on `stream`"""
+        vp = ctypes.c_void_p
+        _check(lib().shadowtopo_compute_rows(self._h, int(row_begin), int(row_end), vp(lat_ptr), vp(rel_ptr),
+                                             vp(hops_ptr), vp(kind_ptr) if kind_ptr else None, MEM_DEVICE,
+                                             vp(stream) if stream else None))
+
+    def sssp(self, sources):
+        s = np.ascontiguousarray(sources, np.int32)
+        k = len(s)
+        dist = np.empty((k, self.n), np.float64)
+        pred = np.empty((k, self.n), np.int32)
+        hops = np.empty((k, self.n), np.uint32)
+        tie = np.empty((k, self.n), np.uint8)
+        _check(lib().shadowtopo_sssp(self._h, _ptr(s), k, _ptr(dist), _ptr(pred), _ptr(hops), _ptr(tie)))
+        return dist, pred, hops, tie
+
+    def stats(self):
+        st = Stats()
+        _check(lib().shadowtopo_get_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def reset_stats(self):
+        lib().shadowtopo_reset_stats(self._h)

@@ -1,0 +1,123 @@
+"""GPU parity: libshadowtopo_hip (through its C ABI) against the CPU oracle.
+
+Bar: latency, hop count, pair kind and reliability bit-exact (the engine folds in the
+reference's order, topology.c:1429-1499); the north-star tolerance for reliability is
+1e-9 relative, which bit-exactness satisfies.
+"""
+import numpy as np
+import pytest
+
+from paritylib import compare, oracle_for
+from shadow_amd import engine as E
+from shadow_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_sparse_undirected(seed):
+    g = synth.random_sparse(V=400, avg_deg=5, seed=seed)
+    st = compare(g)
+    assert st["replayed_sources"] == 0
+
+
+def test_random_sparse_subset_attached():
+    g = synth.random_sparse(V=900, avg_deg=3, seed=7, A=150)
+    compare(g)
+
+
+def test_more_than_one_batch_group():
+    g = synth.random_sparse(V=300, avg_deg=4, seed=9)
+    # 300 sources -> 5 batches; force 2 batches in flight -> 3 groups
+    compare(g, batches_in_flight=2)
+
+
+def test_directed():
+    g = synth.random_sparse(V=300, avg_deg=4, seed=5, directed=True)
+    compare(g)
+
+
+def test_no_self_loops():
+    g = synth.random_sparse(V=250, avg_deg=4, seed=4, loops=False)
+    compare(g)
+
+
+def test_vertex_loss_walk():
+    rng = np.random.default_rng(3)
+    vl = np.where(rng.random(300) < 0.5, rng.uniform(0, 0.1, 300), np.nan)
+    g = synth.random_sparse(V=300, avg_deg=4, seed=12, vloss=vl)
+    compare(g)
+
+
+def test_prefer_direct():
+    g = synth.random_sparse(V=300, avg_deg=6, seed=13)
+    g.prefer_direct = True
+    compare(g)
+
+
+def test_self_dijkstra_loop_rule():
+    g = synth.random_sparse(V=200, avg_deg=4, seed=14)
+    compare(g, self_loop_rule=True)
+
+
+def test_integer_ties_replayed():
+    g = synth.integer_grid(rows=12, cols=12, seed=3)
+    st = compare(g)
+    assert st["replayed_sources"] > 0
+
+
+def test_integer_random_ties():
+    g = synth.random_sparse(V=300, avg_deg=5, seed=15, int_lat=True)
+    compare(g)
+
+
+def test_force_replay_matches():
+    g = synth.random_sparse(V=200, avg_deg=4, seed=16)
+    st = compare(g, force_replay=1)
+    assert st["replayed_sources"] == g.attached.size
+
+
+def test_multigraph_parallel_edges():
+    g = synth.random_sparse(V=150, avg_deg=4, seed=17)
+    # duplicate 40 edges with different latency/loss (parallel edges)
+    rng = np.random.default_rng(0)
+    pick = rng.choice(np.nonzero(g.src != g.dst)[0], 40, replace=False)
+    g.src = np.concatenate([g.src, g.dst[pick]])
+    g.dst = np.concatenate([g.dst, g.src[pick]])
+    g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.3, 1.7, 40)])
+    g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 40)])
+    compare(g)
+
+
+def test_complete_graph_direct_rule():
+    n = 40
+    iu, ju = np.triu_indices(n, 0)
+    rng = np.random.default_rng(2)
+    g = synth._finish("complete", n, iu, ju, rng.uniform(1, 50, len(iu)), rng.uniform(0, 0.05, len(iu)),
+                      np.arange(n))
+    og = oracle_for(g)
+    assert og.is_complete()
+    compare(g)
+
+
+def test_geometric_small():
+    g = synth.geometric_complete_ish(V=600, A=100)
+    compare(g)
+
+
+def test_sssp_full_rows_vs_oracle():
+    g = synth.random_sparse(V=500, avg_deg=4, seed=21)
+    og = oracle_for(g)
+    eng = E.Engine.from_synth(g)
+    srcs = np.array([0, 7, 99, 250, 499], np.int32)
+    dist, pred, hops, tie = eng.sssp(srcs)
+    for k, s in enumerate(srcs):
+        d, parent = og.dijkstra(int(s))
+        dd = np.where(d < 0, np.inf, d)
+        assert np.array_equal(dist[k].view(np.uint64), dd.view(np.uint64))
+        # predecessor vertex from igraph parent edge
+        pv = np.where(parent >= 0, np.where(og.src[np.maximum(parent, 0)] == np.arange(g.n),
+                                            og.dst[np.maximum(parent, 0)], og.src[np.maximum(parent, 0)]), -1)
+        notie = tie[k] == 0
+        assert np.array_equal(pred[k][notie], pv[notie])
+    eng.close()
