@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Headline benchmark: SSSP source-paths/s + attached-pair matrix build time
+(BASELINE.json "metric"), on BASELINE.json configs[1] -- the synthetic 10k-vertex
+geometric complete-ish graph with 1k attached hosts per MI355X.
+
+A step = one pass of the hot path over one batch of input: every source this rank owns
+(1000 unique attached vertices) -> shortest-latency routes to all V vertices, composed
+into the attached-pair latency / reliability / hop rows on the device; with N > 1 ranks
+the rows are exchanged by an RCCL all-gather so every rank holds the full matrix
+(SURVEY.md 8e).  Weak scaling: per-GPU work is fixed (1000 sources), the attached set
+is 1000*N vertices.
+
+python bench.py --gpus N --steps K --warmup W        (N>1 via torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+METRIC = "SSSP source-paths/sec + attached-pair matrix build time; % HBM peak, 1/2/4/8 GPU"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_workload(config, world, scale):
+    from shadow_amd import synth
+    if config == "C2":
+        g = synth.geometric_complete_ish(V=int(10_000 * scale), A=int(1_000 * scale) * world)
+        per = int(1_000 * scale)
+        desc = f"C2 synthetic geometric complete-ish graph, V={g.n}, {per} attached sources per GPU"
+    elif config == "C4":
+        g = synth.barabasi_albert(V=int(100_000 * scale), A=int(10_000 * scale))
+        per = (len(g.attached) + world - 1) // world
+        desc = f"C4 synthetic Barabasi-Albert m=3, V={g.n}, A={len(g.attached)} sharded over GPUs"
+    elif config == "C3":
+        g = synth.knn_geographic(V=int(7_000 * scale))
+        per = (len(g.attached) + world - 1) // world
+        desc = f"C3 Tor stand-in geographic 16-NN, V={g.n}, A={len(g.attached)} sharded over GPUs"
+    elif config == "C5":
+        g = synth.chung_lu(V=int(1_000_000 * scale), A=int(50_000 * scale))
+        per = (len(g.attached) + world - 1) // world
+        desc = f"C5 synthetic Chung-Lu sparse AS graph, V={g.n}, A={len(g.attached)} sharded over GPUs"
+    else:
+        raise SystemExit(f"unknown config {config}")
+    return g, per, desc
+
+
+def algorithmic_bytes_per_source(V, n_arcs, A):
+    """B_src = 4(V+1) + 12*E_arc + 12*V + 20*A"""
+    return 4 * (V + 1) + 12 * n_arcs + 12 * V + 20 * A
+
+
+def cpu_baseline(g, n_sources, budget_s=20.0):
+    """The oracle (heap-exact C restatement of the reference path, 1 thread: the reference
+    serialises every Dijkstra under graphLock, topology.c:1747-1781) on a bounded sample."""
+    from oracle import oracle as O
+    og = O.OracleGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss, directed=g.directed)
+    flags = og.flags(prefer_direct=g.prefer_direct)
+    done = 0
+    t0 = time.perf_counter()
+    while done < n_sources and time.perf_counter() - t0 < budget_s:
+        og.pair_rows(flags, g.attached, done, done + 1, nthreads=1)
+        done += 1
+    dt = time.perf_counter() - t0
+    og.close()
+    return {"value": done / dt, "unit": "source-paths/s", "cores": 1, "kind": "port",
+            "sample": f"{done} sources x {len(g.attached)} attached targets of the same graph "
+                      f"({dt:.1f} s, oracle/topo_oracle.c, 1 thread)"}
+
+
+def load_traffic(workload_key):
+    p = os.path.join(ROOT, "profiles", "relax_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(workload_key)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sources", type=int, default=12)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{local}")
+
+    from shadow_amd import engine as E
+    t = time.perf_counter()
+    g, per, desc = build_workload(args.config, world, args.scale)
+    A = len(g.attached)
+    r0, r1 = rank * per, min(A, (rank + 1) * per)
+    log(f"[rank {rank}] workload {desc}: E={g.m} built in {time.perf_counter() - t:.1f}s")
+    t = time.perf_counter()
+    eng = E.Engine.from_synth(g, device=local)
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_TIMING, 1)
+    log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
+        f"complete={eng.complete}")
+    rows = r1 - r0
+    lat = torch.empty((rows, A), dtype=torch.float64, device=dev)
+    rel = torch.empty((rows, A), dtype=torch.float64, device=dev)
+    hops = torch.empty((rows, A), dtype=torch.int32, device=dev)
+    if world > 1:
+        full_lat = torch.empty((per * world, A), dtype=torch.float64, device=dev)
+        full_rel = torch.empty((per * world, A), dtype=torch.float64, device=dev)
+        full_hops = torch.empty((per * world, A), dtype=torch.int32, device=dev)
+
+    def step():
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        eng.compute_rows_device(r0, r1, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(full_lat, lat)
+            dist.all_gather_into_tensor(full_rel, rel)
+            dist.all_gather_into_tensor(full_hops, hops)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total_sources = A if world > 1 else rows  # every rank's rows per step
+    value = total_sources * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # roofline of the dominant kernel (k_relax), from live HIP events on its stream
+    B_src = algorithmic_bytes_per_source(g.n, st["n_arcs"], A)
+    relax_launches = max(1, st["relax_launches"])
+    bytes_per_launch = rows * args.steps * B_src / relax_launches
+    avg_launch_s = st["relax_ms"] / relax_launches / 1e3
+    achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
+    traffic = load_traffic(f"{args.config}@{args.scale}")
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "kernel": "k_relax", "avg_launch_ms": avg_launch_s * 1e3,
+                "launches_per_step": relax_launches / args.steps,
+                "algorithmic_bytes_per_source": B_src}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(g, args.cpu_sources)
+        except Exception as e:  # report, never fake
+            cpu = {"value": None, "error": str(e)}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "source-paths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak" if args.config == "C2" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md 8d generator, fixed seeds)",
+            "config": {"workload": desc, "n_vertices": g.n, "n_edges": g.m, "n_arcs": st["n_arcs"],
+                       "attached": A, "sources_per_gpu": rows, "matrix_build_ms": ms_per_step,
+                       "parallelism": f"sources sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "engine": {"rounds_per_step": st["rounds"] / args.steps, "replayed_sources": st["replayed_sources"],
+                       "relax_ms_per_step": st["relax_ms"] / args.steps,
+                       "compose_ms_per_step": st["compose_ms"] / args.steps},
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,7 +15,7 @@ LIB = os.path.join(OUT, "libshadowtopo_hip.so")
 ARCH = os.environ.get("SHADOWTOPO_ARCH", "gfx950")
 
 HIP_SOURCES = ["engine.hip"]
-C_SOURCES = []  # filled in by the host shim (topology_hip.c, graphml.c, ...)
+C_SOURCES = ["graphml.c", "topology_hip.c", "shadow_hooks.c"]  # C host shim
 
 
 def _hipcc():
@@ -54,9 +54,13 @@ def build(verbose=False, force=False):
               "-I", inc, "-I", CSRC, "-c", s, "-o", o], verbose)
         objs.append(o)
     hipcc = _hipcc()
+    for s in hip_srcs:
+        o = os.path.join(OUT, os.path.basename(s) + ".o")
+        _run([hipcc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=off",
+              "-I", inc, "-I", CSRC, "-c", s, "-o", o], verbose)
+        objs.append(o)
     tmp = LIB + ".tmp"
-    _run([hipcc, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-          "-I", inc, "-I", CSRC] + hip_srcs + objs + ["-o", tmp, "-pthread"], verbose)
+    _run([hipcc, "-shared", "-fPIC"] + objs + ["-o", tmp, "-pthread"], verbose)
     os.replace(tmp, LIB)
     return LIB
 

@@ -1,0 +1,1146 @@
+/*
+ * topology_hip.c -- Shadow's topology API (include/topology_hip.h) on top of the MI355X
+ * engine (include/shadowtopo.h).
+ *
+ * Kept from the reference (/root/reference/src/main/routing/topology.c), restated in C
+ * over flat arrays instead of igraph + glib:
+ *   - GraphML load + validation            :371-399, :565-1210 (graphml.c, check_*)
+ *   - host -> vertex attachment            :2094-2430 (find_attachment_vertex)
+ *   - detach                               :2432-2439
+ *   - getters / packet counter             :2053-2092
+ *   - min-latency upcall                   :1374-1385
+ *   - teardown logging                     :1266-1282, :1929-1967, path.c:62-75
+ * Replaced: the lazy per-source igraph Dijkstra and the two-level GHashTable path cache
+ * (:1284-1386, :1545-1927, :1969-2051).  On the first query (a worker thread, as in the
+ * reference) the engine computes the whole attached-pair matrix once, eagerly, on the
+ * GPU; after that every lookup is two array reads.  Pairs follow the canonical
+ * ordered-pair rule of SURVEY.md 8.0 (the value the reference stores for (s,t) when s's
+ * own computation runs first).
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <math.h>
+#include <netinet/in.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+#include <time.h>
+
+#include "graphml.h"
+#include "shadowtopo.h"
+#include "shim_log.h"
+#include "topology_hip.h"
+#include "topology_hip_ext.h"
+
+/* Shadow functions (strong in Shadow, weak stand-ins in shadow_hooks.c) */
+extern uint32_t address_toNetworkIP(Address* address);
+extern in_addr_t address_stringToIP(const char* ipString);
+extern char* address_toHostIPString(Address* address);
+extern char* address_toString(Address* address);
+extern double random_nextDouble(Random* random);
+extern void worker_updateMinTimeJump(double minPathLatency);
+
+#define TOPO_MAGIC 0x70B01060u
+
+/* ------------------------------------------------------------ IP -> vertex table */
+typedef struct {
+    uint32_t* keys;
+    int32_t* vals;
+    uint8_t* state; /* 0 empty, 1 used, 2 deleted */
+    size_t cap, used, live;
+} iptable;
+
+static size_t ip_slot(uint32_t ip, size_t cap) {
+    uint64_t h = (uint64_t)ip * 0x9E3779B97F4A7C15ULL;
+    return (size_t)(h >> 20) & (cap - 1);
+}
+
+static int ipt_grow(iptable* t) {
+    size_t ncap = t->cap ? t->cap * 2 : 256;
+    uint32_t* nk = calloc(ncap, sizeof(uint32_t));
+    int32_t* nv = calloc(ncap, sizeof(int32_t));
+    uint8_t* ns = calloc(ncap, 1);
+    if (!nk || !nv || !ns) {
+        free(nk);
+        free(nv);
+        free(ns);
+        return -1;
+    }
+    for (size_t i = 0; i < t->cap; i++) {
+        if (t->state[i] != 1) continue;
+        size_t j = ip_slot(t->keys[i], ncap);
+        while (ns[j]) j = (j + 1) & (ncap - 1);
+        nk[j] = t->keys[i];
+        nv[j] = t->vals[i];
+        ns[j] = 1;
+    }
+    free(t->keys);
+    free(t->vals);
+    free(t->state);
+    t->keys = nk;
+    t->vals = nv;
+    t->state = ns;
+    t->cap = ncap;
+    t->used = t->live;
+    return 0;
+}
+
+static int32_t ipt_get(const iptable* t, uint32_t ip) {
+    if (!t->cap) return -1;
+    size_t j = ip_slot(ip, t->cap);
+    while (t->state[j]) {
+        if (t->state[j] == 1 && t->keys[j] == ip) return t->vals[j];
+        j = (j + 1) & (t->cap - 1);
+    }
+    return -1;
+}
+
+static int ipt_put(iptable* t, uint32_t ip, int32_t v) { /* g_hash_table_replace */
+    if ((t->used + 1) * 2 > t->cap && ipt_grow(t)) return -1;
+    size_t j = ip_slot(ip, t->cap);
+    size_t tomb = (size_t)-1;
+    while (t->state[j]) {
+        if (t->state[j] == 1 && t->keys[j] == ip) {
+            t->vals[j] = v;
+            return 0;
+        }
+        if (t->state[j] == 2 && tomb == (size_t)-1) tomb = j;
+        j = (j + 1) & (t->cap - 1);
+    }
+    if (tomb != (size_t)-1) j = tomb;
+    else t->used++;
+    t->keys[j] = ip;
+    t->vals[j] = v;
+    t->state[j] = 1;
+    t->live++;
+    return 0;
+}
+
+static void ipt_del(iptable* t, uint32_t ip) {
+    if (!t->cap) return;
+    size_t j = ip_slot(ip, t->cap);
+    while (t->state[j]) {
+        if (t->state[j] == 1 && t->keys[j] == ip) {
+            t->state[j] = 2;
+            t->live--;
+            return;
+        }
+        j = (j + 1) & (t->cap - 1);
+    }
+}
+
+/* ------------------------------------------------------------ state */
+typedef struct matrix {
+    int32_t A;
+    double* lat;
+    double* rel;
+    uint32_t* hops;
+    uint8_t* kind;
+    _Atomic(uint64_t*)* cnt_rows; /* lazily allocated per row, A entries each */
+    struct matrix* next;          /* retired matrices (readers may still hold them) */
+} matrix;
+
+struct _Topology {
+    uint32_t magic;
+    gml_graph* gml;
+    int32_t V;
+    int64_t E;
+    int directed, complete, connected, clusters, prefer_direct;
+    double* elat;  /* edge latency (ms) */
+    double* eloss; /* edge packetloss */
+    double* vloss; /* vertex packetloss, NaN = absent */
+    const gml_attr *a_ip, *a_city, *a_country, *a_geo, *a_type, *a_bwdown, *a_bwup, *a_asn, *a_vloss;
+    pthread_rwlock_t ip_lock;
+    iptable ips;
+    int32_t* att_index; /* [V] attached index or -1 (verticesWithAttachedHosts) */
+    int32_t* attached;
+    int32_t n_att, cap_att;
+    pthread_mutex_t compute_lock;
+    _Atomic(matrix*) mat;
+    matrix* retired;
+    pthread_mutex_t cnt_lock;
+    shadowtopo_engine* eng;
+    int32_t device;
+    int self_rule;
+    double min_latency;
+    double compute_s;
+    int64_t compute_count;
+    int64_t self_count;
+};
+
+/* ------------------------------------------------------------ attribute helpers
+ * _topology_find{Vertex,Edge,Graph}Attribute{String,Double} (topology.c:284-369): a value
+ * counts only if the attribute exists (exact name) and is non-empty / not NaN. */
+static int vstr(const Topology* top, const gml_attr* a, int32_t v, const char** out) {
+    (void)top;
+    if (!a) return 0;
+    const char* s = gml_str(a, v);
+    if (!s || !s[0]) return 0;
+    if (out) *out = s;
+    return 1;
+}
+
+static int vnum(const gml_attr* a, int64_t i, double* out) {
+    if (!a || a->type == GML_STRING) return 0;
+    double x = gml_num(a, i);
+    if (isnan(x)) return 0;
+    if (out) *out = x;
+    return 1;
+}
+
+static const char* vid(const Topology* top, int32_t v) { return top->gml->node_ids[v]; }
+
+static const char* type_name(int t) {
+    return t == GML_NUMERIC ? "NUMERIC" : t == GML_STRING ? "STRING" : t == GML_BOOLEAN ? "BOOLEAN" : "UNKOWN";
+}
+
+/* _topology_checkAttributeType, topology.c:554-563 */
+static int check_type(const char* name, int parsed, int required) {
+    if (parsed == required) {
+        st_info("graph attribute '%s' with type '%s' is supported", name, type_name(parsed));
+        return 1;
+    }
+    st_warning("graph attribute '%s' with type '%s' is supported, but we found unsupported type '%s'", name,
+               type_name(required), type_name(parsed));
+    return 0;
+}
+
+/* case-insensitive prefix match of the reference's attribute keys (topology.c:193-282) */
+static int key_is(const char* name, const char* want, size_t len) { return strncasecmp(name, want, len) == 0; }
+
+/* _topology_checkGraphAttributes, topology.c:565-722 -- note the reference ASSIGNS the
+ * result of each type check (isSuccess = ...), so the last recognised attribute of each
+ * loop decides; restated literally. */
+static int check_attributes(Topology* top) {
+    const gml_graph* g = top->gml;
+    int ok = 1;
+    st_message("checking graph attributes...");
+    for (int i = 0; i < g->nattr; i++) {
+        const gml_attr* a = &g->attrs[i];
+        if (a->domain != GML_GRAPH) continue;
+        if (key_is(a->name, "preferdirectpaths", 17))
+            ok = check_type(a->name, a->type, GML_STRING);
+        else
+            st_warning("graph attribute '%s' is unsupported and will be ignored", a->name);
+    }
+    /* vertex attributes: the keys in order, then igraph's own "id" string attribute */
+    for (int i = 0; i <= g->nattr; i++) {
+        const char* name;
+        int type;
+        if (i < g->nattr) {
+            if (g->attrs[i].domain != GML_NODE) continue;
+            name = g->attrs[i].name;
+            type = g->attrs[i].type;
+        } else {
+            name = "id";
+            type = GML_STRING;
+        }
+        if (key_is(name, "id", 2) || key_is(name, "ip", 2) || key_is(name, "citycode", 8) ||
+            key_is(name, "countrycode", 11) || key_is(name, "type", 4))
+            ok = check_type(name, type, GML_STRING);
+        else if (key_is(name, "asn", 3) || key_is(name, "bandwidthdown", 13) || key_is(name, "bandwidthup", 11) ||
+                 key_is(name, "packetloss", 10))
+            ok = check_type(name, type, GML_NUMERIC);
+        else if (key_is(name, "geocode", 7)) {
+            ok = check_type(name, type, GML_STRING);
+            st_warning("vertex attribute '%s' has been renamed to 'countrycode' and is considered deprecated; "
+                       "please use 'countrycode' and/or 'citycode' instead", name);
+        } else
+            st_info("vertex attribute '%s' is unsupported and will be ignored", name);
+    }
+    if (g->n == 0) { /* igraph adds the "id" attribute only when there are vertices */
+        st_warning("the vertex attribute 'id' of type 'STRING' is required but not provided");
+        ok = 0;
+    }
+    if (!gml_find(g, GML_NODE, "bandwidthdown")) {
+        st_warning("the vertex attribute 'bandwidthdown' of type 'NUMERIC' is required but not provided");
+        ok = 0;
+    }
+    if (!gml_find(g, GML_NODE, "bandwidthup")) {
+        st_warning("the vertex attribute 'bandwidthup' of type 'NUMERIC' is required but not provided");
+        ok = 0;
+    }
+    for (int i = 0; i < g->nattr; i++) {
+        const gml_attr* a = &g->attrs[i];
+        if (a->domain != GML_EDGE) continue;
+        if (key_is(a->name, "latency", 7) || key_is(a->name, "jitter", 6) || key_is(a->name, "packetloss", 10))
+            ok = check_type(a->name, a->type, GML_NUMERIC);
+        else
+            st_info("edge attribute '%s' is unsupported and will be ignored", a->name);
+    }
+    if (!gml_find(g, GML_EDGE, "latency")) {
+        st_warning("the edge attribute 'latency' of type 'NUMERIC' is required but not provided");
+        ok = 0;
+    }
+    if (!gml_find(g, GML_EDGE, "packetloss")) {
+        st_warning("the edge attribute 'packetloss' of type 'NUMERIC' is required but not provided");
+        ok = 0;
+    }
+    if (ok)
+        st_message("successfully verified all graph, vertex, and edge attributes");
+    else
+        st_warning("we could not properly validate all graph, vertex, and edge attributes");
+    return ok;
+}
+
+/* igraph_is_connected / igraph_clusters (mode STRONG), topology.c:738-749 */
+static void connectivity(Topology* top) {
+    const int32_t V = top->V;
+    const int64_t E = top->E;
+    const gml_graph* g = top->gml;
+    if (V == 0) {
+        top->connected = 0;
+        top->clusters = 0;
+        return;
+    }
+    /* forward and reverse CSR */
+    int64_t* fp = calloc((size_t)V + 1, sizeof(int64_t));
+    int64_t* rp = calloc((size_t)V + 1, sizeof(int64_t));
+    int32_t* fa = malloc(sizeof(int32_t) * (size_t)(2 * E + 1));
+    int32_t* ra = malloc(sizeof(int32_t) * (size_t)(2 * E + 1));
+    for (int64_t e = 0; e < E; e++) {
+        fp[g->src[e] + 1]++;
+        rp[g->dst[e] + 1]++;
+        if (!top->directed) {
+            fp[g->dst[e] + 1]++;
+            rp[g->src[e] + 1]++;
+        }
+    }
+    for (int32_t v = 0; v < V; v++) {
+        fp[v + 1] += fp[v];
+        rp[v + 1] += rp[v];
+    }
+    int64_t* ff = malloc(sizeof(int64_t) * (size_t)V);
+    int64_t* rf = malloc(sizeof(int64_t) * (size_t)V);
+    memcpy(ff, fp, sizeof(int64_t) * (size_t)V);
+    memcpy(rf, rp, sizeof(int64_t) * (size_t)V);
+    for (int64_t e = 0; e < E; e++) {
+        fa[ff[g->src[e]]++] = g->dst[e];
+        ra[rf[g->dst[e]]++] = g->src[e];
+        if (!top->directed) {
+            fa[ff[g->dst[e]]++] = g->src[e];
+            ra[rf[g->src[e]]++] = g->dst[e];
+        }
+    }
+    /* Kosaraju: iterative DFS finish order on the forward graph, then reverse sweeps */
+    int32_t* order = malloc(sizeof(int32_t) * (size_t)V);
+    int32_t* stack = malloc(sizeof(int32_t) * (size_t)V);
+    int64_t* it = malloc(sizeof(int64_t) * (size_t)V);
+    uint8_t* seen = calloc((size_t)V, 1);
+    int32_t no = 0;
+    for (int32_t r = 0; r < V; r++) {
+        if (seen[r]) continue;
+        int32_t sp = 0;
+        stack[sp++] = r;
+        seen[r] = 1;
+        it[r] = fp[r];
+        while (sp) {
+            int32_t v = stack[sp - 1];
+            if (it[v] < fp[v + 1]) {
+                int32_t w = fa[it[v]++];
+                if (!seen[w]) {
+                    seen[w] = 1;
+                    it[w] = fp[w];
+                    stack[sp++] = w;
+                }
+            } else {
+                order[no++] = v;
+                sp--;
+            }
+        }
+    }
+    int32_t* comp = malloc(sizeof(int32_t) * (size_t)V);
+    for (int32_t v = 0; v < V; v++) comp[v] = -1;
+    int32_t nc = 0;
+    for (int32_t k = V - 1; k >= 0; k--) {
+        int32_t r = order[k];
+        if (comp[r] >= 0) continue;
+        int32_t sp = 0;
+        stack[sp++] = r;
+        comp[r] = nc;
+        while (sp) {
+            int32_t v = stack[--sp];
+            for (int64_t x = rp[v]; x < rp[v + 1]; x++) {
+                int32_t w = ra[x];
+                if (comp[w] < 0) {
+                    comp[w] = nc;
+                    stack[sp++] = w;
+                }
+            }
+        }
+        nc++;
+    }
+    top->clusters = nc;
+    top->connected = (nc == 1);
+    free(fp);
+    free(rp);
+    free(fa);
+    free(ra);
+    free(ff);
+    free(rf);
+    free(order);
+    free(stack);
+    free(it);
+    free(seen);
+    free(comp);
+}
+
+/* lowest-id self-loop per vertex (igraph_get_eid(v, v)) */
+static int32_t* loop_edges(const Topology* top) {
+    int32_t* le = malloc(sizeof(int32_t) * (size_t)top->V);
+    for (int32_t v = 0; v < top->V; v++) le[v] = -1;
+    for (int64_t e = top->E - 1; e >= 0; e--)
+        if (top->gml->src[e] == top->gml->dst[e]) le[top->gml->src[e]] = (int32_t)e;
+    return le;
+}
+
+/* _topology_isComplete, topology.c:450-552 */
+static int is_complete(const Topology* top) {
+    const int32_t V = top->V;
+    int64_t* deg = calloc((size_t)V, sizeof(int64_t));
+    for (int64_t e = 0; e < top->E; e++) {
+        deg[top->gml->src[e]]++; /* OUT-incident (directed: tail) */
+        if (!top->directed) deg[top->gml->dst[e]]++;
+    }
+    int32_t* le = loop_edges(top);
+    int complete = 1;
+    for (int32_t v = 0; v < V && complete; v++) {
+        int64_t ecount = deg[v];
+        if (!top->directed && le[v] >= 0) ecount -= 1;
+        if (ecount < V) {
+            st_info("Vert id=%ld has %ld incident edges to %ld total verts and thus this isn't a complete graph",
+                    (long)v, (long)ecount, (long)V);
+            complete = 0;
+        }
+    }
+    if (complete) st_info("Determined this graph is complete.");
+    free(deg);
+    free(le);
+    return complete;
+}
+
+/* _topology_checkGraphProperties, topology.c:724-809 */
+static int check_properties(Topology* top) {
+    st_message("checking graph properties...");
+    if (!check_attributes(top)) {
+        st_critical("topology validation failed because of problem with graph, vertex, or edge attributes");
+        return 0;
+    }
+    connectivity(top);
+    top->complete = is_complete(top);
+    int prefer = 0;
+    const gml_attr* pa = gml_find(top->gml, GML_GRAPH, "preferdirectpaths");
+    if (pa && pa->type == GML_STRING) {
+        const char* value = gml_str(pa, 0);
+        if (value && value[0]) {
+            int yes = !strncasecmp(value, "true", 4) || !strncasecmp(value, "yes", 3) || !strncasecmp(value, "1", 1);
+            if (yes) {
+                st_message("If a direct path between any pair of nodes exists, Shadow will prefer it over shortest "
+                           "path.");
+                prefer = 1;
+            } else {
+                st_message("Shadow will always use shortest path between a pair of nodes, even if a direct path "
+                           "exists (to override, set 'preferdirectpaths' to 'yes' or 'true' or '1' to enable)");
+            }
+        }
+    }
+    top->prefer_direct = prefer;
+    st_message("topology graph is %s, %s, and %s with %u %s. It does%s prefer direct paths.",
+               top->complete ? "complete" : "incomplete", top->directed ? "directed" : "undirected",
+               top->connected ? "strongly connected" : "disconnected", (unsigned)top->clusters,
+               top->clusters == 1 ? "cluster" : "clusters", top->prefer_direct ? "" : " not");
+    if (!top->connected || top->clusters > 1) {
+        st_critical("topology must be strongly connected with a single cluster; it is %sconnected with %i cluster%s",
+                    top->connected ? "" : "dis", top->clusters, top->clusters == 1 ? "" : "s");
+        return 0;
+    }
+    return 1;
+}
+
+/* _topology_checkGraphVerticesHelperHook, topology.c:811-978 */
+static int check_vertices(Topology* top) {
+    st_message("checking graph vertices...");
+    int all_ok = 1;
+    for (int32_t v = 0; v < top->V; v++) {
+        int ok = 1;
+        const char* id = vid(top, v);
+        if (!id || !id[0]) {
+            st_warning("required attribute 'id' on vertex %li is NULL", (long)v);
+            ok = 0;
+            id = "NULL";
+        }
+        double x;
+        if (!top->a_bwdown) {
+            st_warning("required attribute 'bandwidthdown' on vertex %li (id='%s') is missing", (long)v, id);
+            ok = 0;
+        } else if (!(vnum(top->a_bwdown, v, &x) && x > 0.0)) {
+            st_warning("required attribute 'bandwidthdown' on vertex %li (id='%s') is NAN or negative", (long)v, id);
+            ok = 0;
+        }
+        if (!top->a_bwup) {
+            st_warning("required attribute 'bandwidthup' on vertex %li (id='%s') is missing", (long)v, id);
+            ok = 0;
+        } else if (!(vnum(top->a_bwup, v, &x) && x > 0.0)) {
+            st_warning("required attribute 'bandwidthup' on vertex %li (id='%s') is NAN or negative", (long)v, id);
+            ok = 0;
+        }
+        if (top->a_asn && vnum(top->a_asn, v, &x) && !(x > 0.0)) {
+            st_warning("optional attribute 'asn' on vertex %li (id='%s') is non-positive", (long)v, id);
+            ok = 0;
+        }
+        if (top->a_vloss && vnum(top->a_vloss, v, &x) && !(x >= 0.0 && x <= 1.0)) {
+            st_warning("optional attribute 'packetloss' on vertex %li (id='%s') is out of range [0.0,1.0]", (long)v,
+                       id);
+            ok = 0;
+        }
+        if (!ok) all_ok = 0;
+    }
+    if (!all_ok) {
+        st_warning("we had a problem validating vertex attributes");
+        st_warning("unable to validate graph vertices");
+        return 0;
+    }
+    st_message("%u graph vertices ok", (unsigned)top->V);
+    return 1;
+}
+
+/* _topology_checkGraphEdgesHelperHook, topology.c:1041-1124 */
+static int check_edges(Topology* top) {
+    st_message("checking graph edges...");
+    const gml_attr* al = gml_find(top->gml, GML_EDGE, "latency");
+    const gml_attr* ap = gml_find(top->gml, GML_EDGE, "packetloss");
+    const gml_attr* aj = gml_find(top->gml, GML_EDGE, "jitter");
+    int all_ok = 1;
+    for (int64_t e = 0; e < top->E; e++) {
+        const char* from = vid(top, top->gml->src[e]);
+        const char* to = vid(top, top->gml->dst[e]);
+        double x;
+        if (al && vnum(al, e, &x)) {
+            if (!(x > 0.0)) {
+                st_warning("required attribute 'latency' on edge %li (from '%s' to '%s') is non-positive", (long)e,
+                           from, to);
+                all_ok = 0;
+            }
+        } else {
+            st_warning("required attribute 'latency' on edge %li (from '%s' to '%s') is missing or NAN", (long)e,
+                       from, to);
+            all_ok = 0;
+        }
+        if (ap && vnum(ap, e, &x)) {
+            if (!(x >= 0.0 && x <= 1.0)) {
+                st_warning("required attribute 'packetloss' on edge %li (from '%s' to '%s') is out of range [0.0,1.0]",
+                           (long)e, from, to);
+                all_ok = 0;
+            }
+        } else {
+            st_warning("required attribute 'packetloss' on edge %li (from '%s' to '%s') is missing or NAN", (long)e,
+                       from, to);
+            all_ok = 0;
+        }
+        if (aj && vnum(aj, e, &x) && !(x >= 0.0)) {
+            st_warning("optional attribute 'jitter' on edge %li (from '%s' to '%s') is negative", (long)e, from, to);
+            all_ok = 0;
+        }
+    }
+    if (!all_ok) {
+        st_warning("we had a problem validating edge attributes");
+        st_warning("unable to validate graph edges");
+        return 0;
+    }
+    st_message("%u graph edges ok", (unsigned)top->E);
+    return 1;
+}
+
+/* _topology_extractEdgeWeights (topology.c:1212-1246) + the per-vertex loss column */
+static int extract(Topology* top) {
+    const gml_attr* al = gml_find(top->gml, GML_EDGE, "latency");
+    const gml_attr* ap = gml_find(top->gml, GML_EDGE, "packetloss");
+    top->elat = malloc(sizeof(double) * (size_t)(top->E ? top->E : 1));
+    top->eloss = malloc(sizeof(double) * (size_t)(top->E ? top->E : 1));
+    top->vloss = malloc(sizeof(double) * (size_t)top->V);
+    if (!top->elat || !top->eloss || !top->vloss) return 0;
+    for (int64_t e = 0; e < top->E; e++) {
+        top->elat[e] = gml_num(al, e);
+        top->eloss[e] = gml_num(ap, e);
+    }
+    for (int32_t v = 0; v < top->V; v++) {
+        double x;
+        top->vloss[v] = vnum(top->a_vloss, v, &x) ? x : NAN;
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------ lifecycle */
+static void free_matrix(matrix* m) {
+    if (!m) return;
+    free(m->lat);
+    free(m->rel);
+    free(m->hops);
+    free(m->kind);
+    if (m->cnt_rows) {
+        for (int32_t i = 0; i < m->A; i++) free(atomic_load(&m->cnt_rows[i]));
+        free((void*)m->cnt_rows);
+    }
+    free(m);
+}
+
+static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix* m, int32_t i, int32_t j,
+                         uint64_t count, char* buf, size_t len) {
+    /* path_toString, path.c:62-75 */
+    size_t o = (size_t)i * m->A + j;
+    snprintf(buf, len,
+             "SourceIndex=%ld DestinationIndex=%ld Latency=%f Reliability=%f PacketCount=%lu isDirect=%s", (long)s,
+             (long)t, m->lat[o], m->rel[o], (unsigned long)count,
+             m->kind[o] == SHADOWTOPO_KIND_DIRECT ? "True" : "False");
+    (void)top;
+    return buf;
+}
+
+void topology_free(Topology* top) {
+    if (!top) return;
+    matrix* m = atomic_load(&top->mat);
+    if (m && m->cnt_rows && shadowtopo_log_enabled(ST_INFO)) {
+        /* _topology_logAllCachedPaths (topology.c:1929-1967): every pair a query touched */
+        char buf[512];
+        for (int32_t i = 0; i < m->A; i++) {
+            uint64_t* row = atomic_load(&m->cnt_rows[i]);
+            if (!row) continue;
+            for (int32_t j = 0; j < m->A; j++) {
+                if (!row[j]) continue;
+                int32_t s = top->attached[i], t = top->attached[j];
+                st_info("Found path %s%s%s in cache: %s", vid(top, s), top->directed ? "->" : "<->", vid(top, t),
+                        path_string(top, s, t, m, i, j, row[j] - 1, buf, sizeof buf));
+            }
+        }
+    }
+    st_message("path cache cleared, spent %f seconds computing %u shortest paths with dijkstra, "
+               "and %f seconds computing %u shortest self paths",
+               top->compute_s, (unsigned)top->compute_count, 0.0, (unsigned)top->self_count);
+    free_matrix(m);
+    for (matrix* r = top->retired; r;) {
+        matrix* n = r->next;
+        free_matrix(r);
+        r = n;
+    }
+    if (top->eng) shadowtopo_destroy(top->eng);
+    free(top->ips.keys);
+    free(top->ips.vals);
+    free(top->ips.state);
+    free(top->att_index);
+    free(top->attached);
+    free(top->elat);
+    free(top->eloss);
+    free(top->vloss);
+    gml_free(top->gml);
+    pthread_rwlock_destroy(&top->ip_lock);
+    pthread_mutex_destroy(&top->compute_lock);
+    pthread_mutex_destroy(&top->cnt_lock);
+    top->magic = 0;
+    free(top);
+}
+
+Topology* topology_new(const char* graphPath) {
+    if (!graphPath) return NULL;
+    Topology* top = calloc(1, sizeof(Topology));
+    if (!top) return NULL;
+    top->magic = TOPO_MAGIC;
+    pthread_rwlock_init(&top->ip_lock, NULL);
+    pthread_mutex_init(&top->compute_lock, NULL);
+    pthread_mutex_init(&top->cnt_lock, NULL);
+    const char* dev = getenv("SHADOWTOPO_DEVICE");
+    top->device = dev ? atoi(dev) : 0;
+    atomic_store(&top->mat, NULL);
+
+    char err[512] = {0};
+    st_message("reading graphml topology graph at '%s'...", graphPath);
+    if (gml_parse_file(graphPath, &top->gml, err, sizeof err) != 0) {
+        st_critical("reading graphml topology graph at '%s' failed: %s", graphPath, err);
+        topology_free(top);
+        st_critical("we failed to create the simulation topology because we were unable to validate the topology "
+                    "graphml file");
+        return NULL;
+    }
+    st_message("successfully read graphml topology graph at '%s'", graphPath);
+    top->V = top->gml->n;
+    top->E = top->gml->m;
+    top->directed = top->gml->directed;
+    top->a_ip = gml_find(top->gml, GML_NODE, "ip");
+    top->a_city = gml_find(top->gml, GML_NODE, "citycode");
+    top->a_country = gml_find(top->gml, GML_NODE, "countrycode");
+    top->a_geo = gml_find(top->gml, GML_NODE, "geocode");
+    top->a_type = gml_find(top->gml, GML_NODE, "type");
+    top->a_bwdown = gml_find(top->gml, GML_NODE, "bandwidthdown");
+    top->a_bwup = gml_find(top->gml, GML_NODE, "bandwidthup");
+    top->a_asn = gml_find(top->gml, GML_NODE, "asn");
+    top->a_vloss = gml_find(top->gml, GML_NODE, "packetloss");
+    int ok = check_properties(top) && check_vertices(top) && check_edges(top);
+    if (ok)
+        st_message("successfully parsed graphml and validated topology: graph is %s with %u %s, %u %s, and %u %s",
+                   top->connected ? "strongly connected" : "disconnected", (unsigned)top->clusters,
+                   top->clusters == 1 ? "cluster" : "clusters", (unsigned)top->V, top->V == 1 ? "vertex" : "vertices",
+                   (unsigned)top->E, top->E == 1 ? "edge" : "edges");
+    if (!ok || !extract(top)) {
+        topology_free(top);
+        st_critical("we failed to create the simulation topology because we were unable to validate the topology "
+                    "graphml file");
+        return NULL;
+    }
+    top->att_index = malloc(sizeof(int32_t) * (size_t)(top->V > 0 ? top->V : 1));
+    for (int32_t v = 0; v < top->V; v++) top->att_index[v] = -1;
+    return top;
+}
+
+/* ------------------------------------------------------------ attach */
+typedef struct {
+    int32_t* v;
+    int32_t n, cap;
+} ivec;
+
+static void iv_push(ivec* q, int32_t x) {
+    if (q->n == q->cap) {
+        q->cap = q->cap ? q->cap * 2 : 64;
+        q->v = realloc(q->v, sizeof(int32_t) * (size_t)q->cap);
+    }
+    q->v[q->n++] = x;
+}
+
+static int usable_ip(in_addr_t ip) { return ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK; }
+
+/* _topology_findAttachmentVertex + its hook, topology.c:2094-2369 */
+static int32_t find_attachment_vertex(Topology* top, Random* rnd, const char* ipHint, const char* cityHint,
+                                      const char* countryHint, const char* geoHint, const char* typeHint) {
+    enum { CITY_TYPE, CITY, COUNTRY_TYPE, COUNTRY, GEO_TYPE, GEO, TYPE, ALL, NQ };
+    ivec q[NQ];
+    uint32_t nips[NQ];
+    memset(q, 0, sizeof q);
+    memset(nips, 0, sizeof nips);
+    int requested_usable = 0, found_exact = 0;
+    in_addr_t requested = 0;
+    if (ipHint) {
+        in_addr_t ip = address_stringToIP(ipHint);
+        if (usable_ip(ip)) {
+            requested_usable = 1;
+            requested = ip;
+        }
+    }
+    for (int32_t v = 0; v < top->V; v++) {
+        const char *ipS = NULL, *cityS = NULL, *countryS = NULL, *geoS = NULL, *typeS = NULL;
+        int ipF = vstr(top, top->a_ip, v, &ipS);
+        int cityF = vstr(top, top->a_city, v, &cityS);
+        int countryF = vstr(top, top->a_country, v, &countryS);
+        int geoF = vstr(top, top->a_geo, v, &geoS);
+        int typeF = vstr(top, top->a_type, v, &typeS);
+        int cityM = cityF && cityHint && !strcasecmp(cityS, cityHint);
+        int countryM = countryF && countryHint && !strcasecmp(countryS, countryHint);
+        int geoM = geoF && geoHint && !strcasecmp(geoS, geoHint);
+        int typeM = typeF && typeHint && !strcasecmp(typeS, typeHint);
+        int vUsable = 0;
+        in_addr_t vip = INADDR_NONE;
+        if (ipF) {
+            in_addr_t ip = address_stringToIP(ipS);
+            if (usable_ip(ip)) {
+                vUsable = 1;
+                vip = ip;
+            }
+        }
+        if (requested_usable && vUsable && vip == requested) {
+            if (!found_exact) /* g_queue_clear of every queue; the IP counters are kept */
+                for (int k = 0; k < NQ; k++) q[k].n = 0;
+            found_exact = 1;
+            iv_push(&q[ALL], v);
+            nips[ALL]++;
+        }
+        if (found_exact) continue;
+        iv_push(&q[ALL], v);
+        if (vUsable) nips[ALL]++;
+        if (cityM && typeM) {
+            iv_push(&q[CITY_TYPE], v);
+            if (vUsable) nips[CITY_TYPE]++;
+        }
+        if (cityM) {
+            iv_push(&q[CITY], v);
+            if (vUsable) nips[CITY]++;
+        }
+        if (countryM && typeM) {
+            iv_push(&q[COUNTRY_TYPE], v);
+            if (vUsable) nips[COUNTRY_TYPE]++;
+        }
+        if (countryM) {
+            iv_push(&q[COUNTRY], v);
+            if (vUsable) nips[COUNTRY]++;
+        }
+        if (geoM && typeM) {
+            iv_push(&q[GEO_TYPE], v);
+            if (vUsable) nips[GEO_TYPE]++;
+        }
+        if (geoM) {
+            iv_push(&q[GEO], v);
+            if (vUsable) nips[GEO]++;
+        }
+        if (typeM) {
+            iv_push(&q[TYPE], v);
+            if (vUsable) nips[TYPE]++;
+        }
+    }
+    int pick = ALL;
+    int use_lpm = 0;
+    for (int k = CITY_TYPE; k <= TYPE; k++) {
+        if (q[k].n > 0) {
+            pick = k;
+            break;
+        }
+    }
+    if (pick != ALL)
+        use_lpm = requested_usable && nips[pick] > 0;
+    else
+        use_lpm = ipHint && nips[ALL] > 0;
+    int32_t chosen = -1;
+    ivec* c = &q[pick];
+    if (c->n > 0) {
+        if (use_lpm && !found_exact) {
+            /* _topology_getLongestPrefixMatch, topology.c:2219-2246 */
+            in_addr_t best_match = 0;
+            for (int32_t k = 0; k < c->n; k++) {
+                int32_t v = c->v[k];
+                const char* ipS = top->a_ip ? gml_str(top->a_ip, v) : "";
+                in_addr_t vip = address_stringToIP(ipS);
+                in_addr_t match = ~(vip ^ requested);
+                if (match > best_match || best_match == 0) {
+                    best_match = match;
+                    chosen = v;
+                }
+            }
+        } else {
+            double r = random_nextDouble(rnd);
+            int index_range = c->n - 1;
+            int chosen_index = (int)round((double)(index_range * r));
+            if (chosen_index >= 0 && chosen_index < c->n) chosen = c->v[chosen_index];
+        }
+    }
+    for (int k = 0; k < NQ; k++) free(q[k].v);
+    return chosen;
+}
+
+void topology_attach(Topology* top, Address* address, Random* randomSourcePool, char* ipHint, char* citycodeHint,
+                     char* countrycodeHint, char* geocodeHint, char* typeHint, uint64_t* bwDownOut,
+                     uint64_t* bwUpOut) {
+    if (!top || !address) return;
+    uint32_t node_ip = address_toNetworkIP(address);
+    int32_t v = find_attachment_vertex(top, randomSourcePool, ipHint, citycodeHint, countrycodeHint, geocodeHint,
+                                       typeHint);
+    if (v < 0) {
+        st_error("no attachment vertex for address '%s'", address_toHostIPString(address));
+        return;
+    }
+    pthread_rwlock_wrlock(&top->ip_lock);
+    ipt_put(&top->ips, node_ip, v);
+    if (top->att_index[v] < 0) {
+        if (top->n_att == top->cap_att) {
+            top->cap_att = top->cap_att ? top->cap_att * 2 : 256;
+            top->attached = realloc(top->attached, sizeof(int32_t) * (size_t)top->cap_att);
+        }
+        top->att_index[v] = top->n_att;
+        top->attached[top->n_att++] = v;
+    }
+    pthread_rwlock_unlock(&top->ip_lock);
+    double x;
+    if (bwUpOut) *bwUpOut = vnum(top->a_bwup, v, &x) ? (uint64_t)x : 0;
+    if (bwDownOut) *bwDownOut = vnum(top->a_bwdown, v, &x) ? (uint64_t)x : 0;
+    const char *ipS = NULL, *cityS = NULL, *countryS = NULL, *geoS = NULL, *typeS = NULL;
+    vstr(top, top->a_ip, v, &ipS);
+    vstr(top, top->a_city, v, &cityS);
+    vstr(top, top->a_country, v, &countryS);
+    vstr(top, top->a_geo, v, &geoS);
+    vstr(top, top->a_type, v, &typeS);
+#define NS(x) ((x) ? (x) : "(null)")
+    st_message("attached address '%s' to vertex %li ('%s') with attributes (ip=%s, citycode=%s, countrycode=%s, "
+               "geocode=%s, type=%s) using hints (ip=%s, citycode=%s, countrycode=%s, geocode=%s, type=%s)",
+               address_toHostIPString(address), (long)v, vid(top, v), NS(ipS), NS(cityS), NS(countryS), NS(geoS),
+               NS(typeS), NS(ipHint), NS(citycodeHint), NS(countrycodeHint), NS(geocodeHint), NS(typeHint));
+#undef NS
+}
+
+void topology_detach(Topology* top, Address* address) {
+    if (!top || !address) return;
+    uint32_t ip = address_toNetworkIP(address);
+    pthread_rwlock_wrlock(&top->ip_lock);
+    ipt_del(&top->ips, ip);
+    pthread_rwlock_unlock(&top->ip_lock);
+}
+
+/* ------------------------------------------------------------ eager computation */
+static int ensure_engine(Topology* top) {
+    if (top->eng) return 0;
+    uint32_t flags = 0;
+    if (top->directed) flags |= SHADOWTOPO_F_DIRECTED;
+    if (top->complete) flags |= SHADOWTOPO_F_COMPLETE;
+    if (top->prefer_direct) flags |= SHADOWTOPO_F_PREFER_DIRECT;
+    if (top->self_rule) flags |= SHADOWTOPO_F_SELF_DIJKSTRA_LOOP;
+    int rc = shadowtopo_create(top->V, top->E, top->gml->src, top->gml->dst, top->elat, top->eloss, top->vloss, flags,
+                               top->device, &top->eng);
+    if (rc != SHADOWTOPO_OK) {
+        st_critical("GPU topology engine unavailable (%d): %s", rc, shadowtopo_last_error());
+        top->eng = NULL;
+        return -1;
+    }
+    return 0;
+}
+
+static matrix* compute_matrix(Topology* top, int32_t A) {
+    if (ensure_engine(top)) return NULL;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    if (shadowtopo_set_attached(top->eng, top->attached, A) != SHADOWTOPO_OK) {
+        st_critical("shadowtopo_set_attached: %s", shadowtopo_last_error());
+        return NULL;
+    }
+    matrix* m = calloc(1, sizeof(matrix));
+    size_t n = (size_t)A * (size_t)A;
+    m->A = A;
+    m->lat = malloc(sizeof(double) * (n ? n : 1));
+    m->rel = malloc(sizeof(double) * (n ? n : 1));
+    m->hops = malloc(sizeof(uint32_t) * (n ? n : 1));
+    m->kind = malloc(n ? n : 1);
+    m->cnt_rows = calloc((size_t)(A ? A : 1), sizeof(*m->cnt_rows));
+    if (!m->lat || !m->rel || !m->hops || !m->kind || !m->cnt_rows) {
+        st_critical("out of host memory for the %d x %d attached-pair matrix", A, A);
+        free_matrix(m);
+        return NULL;
+    }
+    int rc = shadowtopo_compute_rows(top->eng, 0, A, m->lat, m->rel, m->hops, m->kind, SHADOWTOPO_MEM_HOST, NULL);
+    if (rc != SHADOWTOPO_OK) {
+        st_critical("attached-pair computation failed (%d): %s", rc, shadowtopo_last_error());
+        free_matrix(m);
+        return NULL;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    top->compute_count += top->complete ? 0 : A;
+    top->self_count += top->complete ? 0 : A;
+    /* _topology_storePathInCache's running minimum (topology.c:1374-1385) over every path
+     * the matrix holds */
+    double mn = 0;
+    for (size_t k = 0; k < n; k++)
+        if (m->kind[k] != SHADOWTOPO_KIND_NONE && (mn == 0 || m->lat[k] < mn)) mn = m->lat[k];
+    if (mn > 0 && (top->min_latency == 0 || mn < top->min_latency)) {
+        top->min_latency = mn;
+        worker_updateMinTimeJump(top->min_latency);
+    }
+    st_info("computed %d x %d attached-pair matrix on device %d in %f seconds", A, A, top->device,
+            top->compute_s);
+    return m;
+}
+
+static matrix* current_matrix(Topology* top, int32_t need) {
+    matrix* m = atomic_load_explicit(&top->mat, memory_order_acquire);
+    if (m && m->A > need) return m;
+    pthread_mutex_lock(&top->compute_lock);
+    m = atomic_load_explicit(&top->mat, memory_order_acquire);
+    if (!m || m->A <= need) {
+        pthread_rwlock_rdlock(&top->ip_lock);
+        int32_t A = top->n_att;
+        pthread_rwlock_unlock(&top->ip_lock);
+        matrix* nm = A > need ? compute_matrix(top, A) : NULL;
+        if (nm) {
+            if (m) {
+                m->next = top->retired;
+                top->retired = m;
+            }
+            atomic_store_explicit(&top->mat, nm, memory_order_release);
+            m = nm;
+        } else {
+            m = NULL;
+        }
+    }
+    pthread_mutex_unlock(&top->compute_lock);
+    return m;
+}
+
+static int32_t connected_vertex(Topology* top, Address* a) {
+    /* _topology_getConnectedVertexIndex, topology.c:1388-1405 */
+    uint32_t ip = address_toNetworkIP(a);
+    pthread_rwlock_rdlock(&top->ip_lock);
+    int32_t v = ipt_get(&top->ips, ip);
+    pthread_rwlock_unlock(&top->ip_lock);
+    if (v < 0) st_warning("address %s is not connected to the topology", address_toHostIPString(a));
+    return v;
+}
+
+/* _topology_getPathEntry, topology.c:1969-2051: returns the matrix and pair offset */
+static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off, int32_t* ri, int32_t* rj) {
+    int32_t vs = connected_vertex(top, src);
+    if (vs < 0) {
+        st_critical("invalid vertex %i, source address %s is not connected to topology", (int)vs,
+                    address_toString(src));
+        return NULL;
+    }
+    int32_t vd = connected_vertex(top, dst);
+    if (vd < 0) {
+        st_critical("invalid vertex %i, destination address %s is not connected to topology", (int)vd,
+                    address_toString(dst));
+        return NULL;
+    }
+    int32_t i = top->att_index[vs], j = top->att_index[vd];
+    matrix* m = current_matrix(top, i > j ? i : j);
+    if (m) {
+        size_t o = (size_t)i * (size_t)m->A + (size_t)j;
+        if (m->kind[o] != SHADOWTOPO_KIND_NONE) {
+            *off = o;
+            if (ri) *ri = i;
+            if (rj) *rj = j;
+            return m;
+        }
+    }
+    st_error("unable to find path between node %s at %s (vertex %i) and node %s at %s (vertex %i)",
+             address_toString(src), vid(top, vs), (int)vs, address_toString(dst), vid(top, vd), (int)vd);
+    return NULL;
+}
+
+double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress) {
+    size_t o;
+    matrix* m = path_entry(top, srcAddress, dstAddress, &o, NULL, NULL);
+    return m ? m->lat[o] : -1.0;
+}
+
+double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress) {
+    size_t o;
+    matrix* m = path_entry(top, srcAddress, dstAddress, &o, NULL, NULL);
+    return m ? m->rel[o] : -1.0;
+}
+
+int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress) {
+    return topology_getLatency(top, srcAddress, dstAddress) > -1 ? 1 : 0;
+}
+
+/* counters: one per cached Path, i.e. per unordered pair in undirected graphs (the
+ * reference stores one direction, topology.c:1312-1318); stored value = count + 1 so a
+ * touched pair is non-zero (the teardown log lists touched pairs) */
+static _Atomic uint64_t* counter_of(Topology* top, matrix* m, int32_t i, int32_t j) {
+    if (!top->directed && j < i) {
+        int32_t t = i;
+        i = j;
+        j = t;
+    }
+    uint64_t* row = atomic_load_explicit(&m->cnt_rows[i], memory_order_acquire);
+    if (!row) {
+        pthread_mutex_lock(&top->cnt_lock);
+        row = atomic_load_explicit(&m->cnt_rows[i], memory_order_acquire);
+        if (!row) {
+            row = calloc((size_t)m->A, sizeof(uint64_t));
+            atomic_store_explicit(&m->cnt_rows[i], row, memory_order_release);
+        }
+        pthread_mutex_unlock(&top->cnt_lock);
+    }
+    if (!row) return NULL;
+    return (_Atomic uint64_t*)&row[j];
+}
+
+void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Address* dstAddress) {
+    size_t o;
+    int32_t i, j;
+    matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, &j);
+    if (!m) {
+        st_error("unable to find path between node %s and node %s", address_toString(srcAddress),
+                 address_toString(dstAddress));
+        return;
+    }
+    _Atomic uint64_t* c = counter_of(top, m, i, j);
+    if (!c) return;
+    uint64_t expect = atomic_load_explicit(c, memory_order_relaxed);
+    if (expect == 0) {
+        /* first touch: 0 -> 2 (touched + one packet) */
+        if (atomic_compare_exchange_strong(c, &expect, 2)) return;
+    }
+    atomic_fetch_add_explicit(c, 1, memory_order_relaxed);
+}
+
+/* ------------------------------------------------------------ extensions */
+int topology_hip_set_device(Topology* top, int32_t device) {
+    if (!top || top->eng) return -1;
+    top->device = device;
+    return 0;
+}
+
+int topology_hip_set_self_rule(Topology* top, int32_t dijkstra_loop) {
+    if (!top || top->eng) return -1;
+    top->self_rule = dijkstra_loop ? 1 : 0;
+    return 0;
+}
+
+int topology_hip_prepare(Topology* top) {
+    if (!top) return -1;
+    if (top->n_att == 0) return 0;
+    return current_matrix(top, top->n_att - 1) ? 0 : -1;
+}
+
+int topology_hip_get_info(Topology* top, topology_hip_info* out) {
+    if (!top || !out) return -1;
+    memset(out, 0, sizeof *out);
+    out->n_vertices = top->V;
+    out->n_edges = top->E;
+    out->is_directed = top->directed;
+    out->is_complete = top->complete;
+    out->is_connected = top->connected;
+    out->cluster_count = top->clusters;
+    out->prefers_direct_paths = top->prefer_direct;
+    out->n_attached = top->n_att;
+    matrix* m = atomic_load(&top->mat);
+    out->computed_for = m ? m->A : 0;
+    out->device = top->device;
+    out->min_path_latency = top->min_latency;
+    out->compute_seconds = top->compute_s;
+    out->compute_count = top->compute_count;
+    return 0;
+}
+
+int32_t topology_hip_attached(Topology* top, int32_t* out, int32_t cap) {
+    if (!top) return -1;
+    int32_t n = top->n_att < cap ? top->n_att : cap;
+    if (out && n > 0) memcpy(out, top->attached, sizeof(int32_t) * (size_t)n);
+    return top->n_att;
+}
+
+int32_t topology_hip_vertex_of_ip(Topology* top, uint32_t ip) {
+    if (!top) return -1;
+    pthread_rwlock_rdlock(&top->ip_lock);
+    int32_t v = ipt_get(&top->ips, ip);
+    pthread_rwlock_unlock(&top->ip_lock);
+    return v;
+}
+
+int32_t topology_hip_vertex_of_id(Topology* top, const char* id) {
+    if (!top || !id) return -1;
+    for (int32_t v = 0; v < top->V; v++)
+        if (!strcmp(top->gml->node_ids[v], id)) return v;
+    return -1;
+}
+
+uint64_t topology_hip_packet_count(Topology* top, int32_t src_vertex, int32_t dst_vertex) {
+    if (!top || src_vertex < 0 || dst_vertex < 0 || src_vertex >= top->V || dst_vertex >= top->V) return 0;
+    int32_t i = top->att_index[src_vertex], j = top->att_index[dst_vertex];
+    matrix* m = atomic_load(&top->mat);
+    if (!m || i < 0 || j < 0 || i >= m->A || j >= m->A) return 0;
+    if (!top->directed && j < i) {
+        int32_t t = i;
+        i = j;
+        j = t;
+    }
+    uint64_t* row = atomic_load(&m->cnt_rows[i]);
+    if (!row || !row[j]) return 0;
+    return row[j] - 1;
+}
+
+int topology_hip_edges(Topology* top, const int32_t** src, const int32_t** dst, const double** latency,
+                       const double** packetloss, const double** vertex_packetloss) {
+    if (!top) return -1;
+    if (src) *src = top->gml->src;
+    if (dst) *dst = top->gml->dst;
+    if (latency) *latency = top->elat;
+    if (packetloss) *packetloss = top->eloss;
+    if (vertex_packetloss) *vertex_packetloss = top->vloss;
+    return 0;
+}

@@ -1,0 +1,169 @@
+"""CPU: pin the oracle (the checker) before trusting it.
+
+* against the reference's own data: the shipped topology (direct rule) and the
+  1-vertex test topologies of src/test/**/*.test.shadow.config.xml;
+* against independent shortest-path implementations (scipy, networkx) for distances;
+* igraph-specific semantics restated in topo_oracle.c: get_eid lowest id,
+  completeness count, incidence order, self-path rule;
+* regression pins (tests/golden/synthetic_*.npz).
+"""
+import json
+import lzma
+import os
+
+import networkx as nx
+import numpy as np
+import pytest
+import scipy.sparse as sp
+from scipy.sparse.csgraph import dijkstra as sp_dijkstra
+
+from oracle import oracle as O
+from oracle.graphml_ref import read_graphml
+from shadow_amd import synth
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def og_of(g):
+    return O.OracleGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss, directed=g.directed)
+
+
+def test_shipped_topology_direct_rule():
+    g = read_graphml(lzma.open(os.path.join(GOLD, "c1_topology.graphml.xml.xz"), "rt").read())
+    assert (g.n, len(g.src)) == (183, 16836)
+    og = O.from_refgraph(g)
+    assert og.is_complete()
+    gold = np.load(os.path.join(GOLD, "c1_direct.npz"))
+    att = np.arange(g.n, dtype=np.int32)
+    lat, rel, hops, kind, fails = og.pair_rows(og.flags(), att)
+    assert fails == 0
+    assert (kind == O.KIND_DIRECT).all() and (hops == 1).all()
+    assert np.array_equal(lat, gold["lat"])
+    assert np.array_equal(rel, gold["rel"])
+
+
+def test_reference_test_graphs():
+    cases = json.load(open(os.path.join(GOLD, "ref_test_graphs.json")))
+    seen = set()
+    for c in cases:
+        g = read_graphml(c["graphml"])
+        og = O.from_refgraph(g)
+        assert og.is_complete()  # one vertex + self-loop: 2 incident - 1 >= 1
+        lat, rel, hops, kind, _ = og.pair_rows(og.flags(), np.array([0], np.int32))
+        assert lat[0, 0] == c["self_latency"] == 50.0
+        assert rel[0, 0] == c["self_reliability"]
+        seen.add(c["self_reliability"])
+    # example config: 0.99 (resource/examples/shadow.config.xml:11-21); lossless / lossy tests
+    assert seen == {0.99, 1.0, 0.75}
+
+
+@pytest.mark.parametrize("seed,directed", [(1, False), (2, False), (3, True), (4, True)])
+def test_distances_vs_scipy(seed, directed):
+    g = synth.random_sparse(V=400, avg_deg=5, seed=seed, directed=directed)
+    og = og_of(g)
+    m = g.src != g.dst
+    a = sp.coo_matrix((g.latency[m], (g.src[m], g.dst[m])), shape=(g.n, g.n))
+    # parallel edges: keep the minimum latency (coo->csr would sum them)
+    best = {}
+    for s, t, w in zip(a.row, a.col, a.data):
+        k = (s, t) if directed else (min(s, t), max(s, t))
+        best[k] = min(best.get(k, np.inf), w)
+    r, c, w = zip(*[(k[0], k[1], v) for k, v in best.items()])
+    csr = sp.csr_matrix((w, (r, c)), shape=(g.n, g.n))
+    for s in (0, 17, 123):
+        d, _ = og.dijkstra(s)
+        ds = sp_dijkstra(csr, directed=directed, indices=s)
+        assert np.array_equal(np.where(d < 0, np.inf, d), ds)
+
+
+def test_distances_vs_networkx_and_paths_are_shortest():
+    g = synth.random_sparse(V=200, avg_deg=4, seed=8)
+    og = og_of(g)
+    G = nx.Graph()
+    for s, t, w in zip(g.src, g.dst, g.latency):
+        if s != t:
+            G.add_edge(int(s), int(t), weight=float(w))
+    d, parent = og.dijkstra(5)
+    nd = nx.single_source_dijkstra_path_length(G, 5)
+    for v, dv in nd.items():
+        assert abs(d[v] - dv) <= 1e-9 * max(1.0, dv)
+        # the oracle's path latency (left fold, topology.c:1473-1499) equals d(v) exactly
+        p = og.path(5, v, parent)
+        acc = 0.0
+        for a, b in zip(p[:-1], p[1:]):
+            acc += g.latency[og.get_eid(a, b)]
+        assert acc == d[v]
+
+
+def test_get_eid_lowest_and_undirected():
+    n = 5
+    src = np.array([0, 1, 2, 1, 3, 3], np.int32)
+    dst = np.array([1, 0, 2, 2, 4, 4], np.int32)
+    og = O.OracleGraph(n, src, dst, np.ones(6) * 2, np.zeros(6))
+    assert og.get_eid(0, 1) == 0 and og.get_eid(1, 0) == 0  # parallel: lowest id
+    assert og.get_eid(2, 2) == 2
+    assert og.get_eid(2, 1) == 3
+    assert og.get_eid(4, 3) == 4
+    assert og.get_eid(0, 4) == -1
+    ogd = O.OracleGraph(n, src, dst, np.ones(6) * 2, np.zeros(6), directed=True)
+    assert ogd.get_eid(1, 0) == 1 and ogd.get_eid(0, 1) == 0 and ogd.get_eid(2, 1) == -1
+
+
+def test_completeness_rule():
+    # complete simple graph with loops -> complete; remove one loop -> incomplete
+    n = 6
+    iu, ju = np.triu_indices(n, 0)
+    og = O.OracleGraph(n, iu.astype(np.int32), ju.astype(np.int32), np.ones(len(iu)), np.zeros(len(iu)))
+    assert og.is_complete()
+    keep = ~((iu == 3) & (ju == 3))
+    og2 = O.OracleGraph(n, iu[keep].astype(np.int32), ju[keep].astype(np.int32), np.ones(keep.sum()),
+                        np.zeros(keep.sum()))
+    assert not og2.is_complete()
+    # no self loops at all: every vertex has n-1 < n incident edges -> incomplete
+    iu1, ju1 = np.triu_indices(n, 1)
+    og3 = O.OracleGraph(n, iu1.astype(np.int32), ju1.astype(np.int32), np.ones(len(iu1)), np.zeros(len(iu1)))
+    assert not og3.is_complete()
+
+
+def test_self_path_rule_first_strict_min():
+    # vertex 0: edges (0,1) lat 5 loss .1, loop lat 5 loss .3, (0,2) lat 7
+    src = np.array([0, 0, 0, 1], np.int32)
+    dst = np.array([1, 0, 2, 2], np.int32)
+    lat = np.array([5.0, 5.0, 7.0, 1.0])
+    loss = np.array([0.1, 0.3, 0.0, 0.0])
+    og = O.OracleGraph(3, src, dst, lat, loss)
+    l, r = og.self_path(0)
+    # incidence order of vertex 0 (igraph_incident OUT, undirected): out part = edges with
+    # from==0 (only the loop, stored from=max=0), then in part by neighbour: loop, (0,1), (0,2)
+    assert l == 10.0
+    assert r == (1 - 0.3) ** 2
+
+
+def test_heap_pop_order_is_nondecreasing():
+    g = synth.random_sparse(V=300, avg_deg=4, seed=31, int_lat=True)
+    og = og_of(g)
+    d, parent, order = og.dijkstra(0, want_order=True)
+    assert np.all(np.diff(d[order]) >= 0)
+    assert len(order) == g.n
+
+
+def test_regression_pins():
+    for name in ("synthetic_sparse", "synthetic_ties", "synthetic_directed"):
+        z = np.load(os.path.join(GOLD, name + ".npz"))
+        og = O.OracleGraph(int(z["n"]), z["src"], z["dst"], z["latency"], z["packetloss"], z["vloss"],
+                           directed=bool(z["directed"]))
+        lat, rel, hops, kind, _ = og.pair_rows(og.flags(), z["attached"])
+        assert np.array_equal(lat, z["lat"]) and np.array_equal(rel, z["rel"])
+        assert np.array_equal(hops, z["hops"]) and np.array_equal(kind, z["kind"])
+
+
+def test_tie_detector_flags_integer_grid():
+    g = synth.integer_grid(rows=6, cols=6, seed=1)
+    og = og_of(g)
+    d, _ = og.dijkstra(0)
+    tie = og.tie_vertices(0, d)
+    assert tie.sum() > 0
+    g2 = synth.random_sparse(V=300, avg_deg=4, seed=2)
+    og2 = og_of(g2)
+    d2, _ = og2.dijkstra(0)
+    assert og2.tie_vertices(0, d2).sum() == 0
