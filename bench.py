@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sources", type=int, default=12)
+    ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
+    ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     args = ap.parse_args()
 
     import torch
@@ -126,6 +128,10 @@ def main():
     eng = E.Engine.from_synth(g, device=local)
     eng.set_attached(g.attached)
     eng.set_option(E.OPT_TIMING, 1)
+    if args.profile_counts:
+        eng.set_option(E.OPT_PROFILE, 1)
+    if args.batches:
+        eng.set_option(E.OPT_BATCHES_IN_FLIGHT, args.batches)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0
@@ -209,7 +215,8 @@ def main():
             "cpu_baseline": cpu,
             "engine": {"rounds_per_step": st["rounds"] / args.steps, "replayed_sources": st["replayed_sources"],
                        "relax_ms_per_step": st["relax_ms"] / args.steps,
-                       "compose_ms_per_step": st["compose_ms"] / args.steps},
+                       "compose_ms_per_step": st["compose_ms"] / args.steps, "dense": st["dense"],
+                       "visits_per_step": st["visits"] / args.steps, "changes_per_step": st["changes"] / args.steps},
         }
         print(json.dumps(out), flush=True)
     eng.close()

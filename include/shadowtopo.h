@@ -48,6 +48,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 /* let the engine decide F_COMPLETE with the reference's rule (_topology_isComplete,
  * topology.c:450-552) instead of trusting the caller's F_COMPLETE bit */
 #define SHADOWTOPO_F_AUTO_COMPLETE 0x10u
+/* relaxation layout: default picks the dense-tile form when arcs >= V^2/4 (and the
+ * V x V tables fit), the CSR form otherwise; these force one (testing / tuning) */
+#define SHADOWTOPO_F_FORCE_DENSE 0x20u
+#define SHADOWTOPO_F_FORCE_CSR 0x40u
 
 /* where compute_rows' output buffers live */
 #define SHADOWTOPO_MEM_HOST 0
@@ -64,6 +68,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_TIMING 2            /* 1 = record HIP events around every relax launch */
 #define SHADOWTOPO_OPT_MAX_ROUNDS 3        /* iteration guard (default 4*V+64) */
 #define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
+#define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count (vertex, batch) visits and changes (CSR relax) */
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;
@@ -82,6 +87,10 @@ typedef struct shadowtopo_stats {
     double wall_ms;          /* host wall time inside compute calls */
     int32_t device;
     int32_t multigraph;
+    int32_t dense;           /* 1 = dense-tile relaxation in use */
+    int32_t reserved;
+    int64_t visits;          /* OPT_PROFILE: active (vertex, batch) waves processed */
+    int64_t changes;         /* OPT_PROFILE: (vertex, batch) waves that changed */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

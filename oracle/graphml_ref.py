@@ -153,7 +153,9 @@ def read_graphml(text: str) -> RefGraph:
                 dv = default if default is not None else ""
                 g.eattr[name] = (kind, [d.get(kid, dv) for d in edata])
         if dom in ("graph", "all"):
-            dv = default if default is not None else ("" if kind != "numeric" else math.nan)
-            val = gdata.get(kid, dv)
-            g.gattr[name] = (kind, _parse_num(val, math.nan) if kind == "numeric" else val)
+            if kind == "numeric":
+                dv = _parse_num(default, math.nan)
+                g.gattr[name] = (kind, _parse_num(gdata[kid], dv) if kid in gdata else dv)
+            else:
+                g.gattr[name] = (kind, gdata.get(kid, default if default is not None else ""))
     return g

@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU tests + optional extra bench configs
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:-r01}
+shift
+timeout -k 10 600 python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu > gpurun_out/gputests_$TAG.log 2>&1
+rc=$?
+tail -40 gpurun_out/gputests_$TAG.log
+[ $rc -ne 0 ] && { echo "gpu tests failed rc=$rc"; exit 1; }
+for cfg in "$@"; do
+  timeout -k 10 400 python -u bench.py --config $cfg --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_${TAG}_$cfg.json 2> gpurun_out/bench_${TAG}_$cfg.err || { echo "bench $cfg failed"; tail -20 gpurun_out/bench_${TAG}_$cfg.err; exit 1; }
+  cat gpurun_out/bench_${TAG}_$cfg.json
+done

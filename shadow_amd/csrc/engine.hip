@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -87,16 +88,54 @@ struct GraphDev {
     const int32_t* loop_eid; // lowest-id self-loop per vertex, -1 if none
 };
 
-struct BatchDev {
-    double* D;       // [V][64] distance
-    uint32_t* H;     // [V][64] hops | TAINT
-    double* R;       // [V][64] reliability fold along the tree path
-    int32_t* P;      // [V][64] predecessor in-arc
-    uint8_t* act[2]; // [V] frontier flags, alternating rounds
-    int32_t srcv[KL];
-    int32_t row[KL];
-    unsigned long long replay_mask;
+// Per-batch state lives in contiguous pools (slot b at offset b * vk), addressed from the
+// kernel argument itself: no dependent load of a descriptor before the first useful load.
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) uint32_t guint;
+typedef __attribute__((address_space(1))) int32_t gint;
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+
+struct Pools {
+    double* D;          // [slot][Vp][64] distance
+    uint32_t* H;        // [slot][Vp][64] hops | TAINT
+    double* R;          // [slot][Vp][64] reliability fold along the tree path
+    int32_t* P;         // [slot][Vp][64] predecessor in-arc
+    uint8_t* act;       // [slot][2][Vp] frontier flags, alternating rounds
+    int32_t* srcv;      // [slot][64] source vertex per lane (-1 = unused lane)
+    int32_t* row;       // [slot][64] attached row per lane (-1 = none)
+    unsigned long long* mask;  // [slot] lanes whose rows need the heap-exact replay
+    int64_t vk;         // Vp * 64
+    int32_t Vp;
+    int32_t pad_;
 };
+
+struct BatchDev {
+    gdouble* D;
+    guint* H;
+    gdouble* R;
+    gint* P;
+    gbyte* act0;
+    gbyte* act1;
+    const int32_t* srcv;
+    const int32_t* row;
+    unsigned long long* mask;
+    __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
+};
+
+__device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
+    BatchDev B;
+    const size_t o = (size_t)b * (size_t)p.vk;
+    B.D = (gdouble*)(p.D + o);
+    B.H = (guint*)(p.H + o);
+    B.R = (gdouble*)(p.R + o);
+    B.P = (gint*)(p.P + o);
+    B.act0 = (gbyte*)(p.act + (size_t)b * 2 * p.Vp);
+    B.act1 = B.act0 + p.Vp;
+    B.srcv = p.srcv + (size_t)b * KL;
+    B.row = p.row + (size_t)b * KL;
+    B.mask = p.mask + b;
+    return B;
+}
 
 struct ReplayDev {
     double* dist;     // [slot][V]
@@ -109,11 +148,10 @@ struct ReplayDev {
     int32_t row[REPLAY_SLOTS];
 };
 
-// global-address-space view of a pointer loaded from memory (lets the compiler emit
-// global_load instead of flat_load for the per-batch state arrays)
-typedef __attribute__((address_space(1))) double gdouble;
+constexpr int CSR_PAD = 8;  // in_src / in_w carry 8 padding arcs (u = 0, w = +inf) so chunk loads never clamp
 
 __device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000000000000LL); }
+__device__ __forceinline__ double dmax() { return __longlong_as_double(0x7fefffffffffffffLL); }
 
 __device__ __forceinline__ int64_t find_arc(const GraphDev& g, int32_t v, int32_t u) {
     int64_t lo = g.in_ptr[v], end = g.in_ptr[v + 1], hi = end;
@@ -135,8 +173,8 @@ __device__ __forceinline__ int32_t get_eid(const GraphDev& g, int32_t from, int3
 }
 
 // ---------------------------------------------------------------- batch state init
-__global__ void k_init(BatchDev* __restrict__ batches, int32_t V) {
-    BatchDev& B = batches[blockIdx.y];
+__global__ void k_init(Pools pools, int32_t V) {
+    const BatchDev B = batch_view(pools, blockIdx.y);
     const size_t total = (size_t)V * KL;
     const double inf = dinf();
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -146,14 +184,14 @@ __global__ void k_init(BatchDev* __restrict__ batches, int32_t V) {
         B.P[i] = -1;
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
-        B.act[0][i] = 0;
-        B.act[1][i] = 0;
+        B.act0[i] = 0;
+        B.act1[i] = 0;
     }
 }
 
 // sources: d(s) = 0, R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445); activate out-neighbours
-__global__ void k_seed(GraphDev g, BatchDev* __restrict__ batches) {
-    BatchDev& B = batches[blockIdx.y];
+__global__ void k_seed(GraphDev g, Pools pools) {
+    const BatchDev B = batch_view(pools, blockIdx.y);
     const int j = blockIdx.x;
     const int32_t s = B.srcv[j];
     if (s < 0) return;
@@ -164,17 +202,41 @@ __global__ void k_seed(GraphDev g, BatchDev* __restrict__ batches) {
         B.R[idx] = g.vfac[s];
         B.P[idx] = -1;
     }
-    for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act[0][g.out_dst[x]] = 1;
+    for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act0[g.out_dst[x]] = 1;
 }
 
-__device__ __forceinline__ void relax_one(double du, double w, int32_t e, double& bc, double& bdu, int32_t& be,
-                                          bool& tie) {
+// Record the new best for (v, lane): hop count / reliability carried from the predecessor
+// (topology.c:1499 totalReliability *= edgeReliability), the taint bit from the
+// predecessor's path or a tie here.  cur* were prefetched at kernel entry.
+__device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32_t v, int32_t arc, int32_t u, double bc,
+                                              double bdu, bool tie, const double* __restrict__ in_r, double curD,
+                                              uint32_t curH, double curR, int32_t curP) {
+    const size_t idx = (size_t)v * KL + lane;
+    const size_t uidx = (size_t)u * KL + lane;
+    const uint32_t hu = B.H[uidx];
+    const double ru = B.R[uidx];
+    const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? TAINT : 0u);
+    const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
+    const double r = ru * in_r[arc];
+    if (bc != curD || h != curH || r != curR || arc != curP) {
+        B.D[idx] = bc;
+        B.H[idx] = h;
+        B.R[idx] = r;
+        B.P[idx] = arc;
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void relax_arc(double du, double w, int32_t e, int32_t u, double& bc, double& bdu,
+                                          int32_t& be, int32_t& bu, bool& tie) {
     const double c = du + w;  // igraph: altdist = mindist + weights[edge]
-    if (c <= bc && du < dinf()) {
+    if (c <= bc) {
         if (c < bc || du < bdu) {
             bc = c;
             bdu = du;
             be = e;
+            bu = u;
             tie = false;
         } else if (du == bdu) {
             tie = true;  // two predecessors at the same d(u): heap pop order decides
@@ -182,15 +244,19 @@ __device__ __forceinline__ void relax_one(double du, double w, int32_t e, double
     }
 }
 
-// One relaxation round over every active destination vertex of every batch in flight.
+// One relaxation round over every active destination vertex of every batch in flight
+// (CSR form, any density).  One wave = one destination v; the in-arc list is walked in
+// chunks of 8: one s_load_dwordx8 of tails, one s_load_dwordx16 of weights (the arrays
+// carry CSR_PAD padding arcs, so a chunk never clamps; arcs past the row get weight +inf)
+// and 8 row loads, all in flight before the first compare.
 // Grid: 1-D, remapped so that all blocks sharing an XCD (blockIdx % 8) work on the same
 // batch (its [V][64] state then stays in that XCD's L2).  Placement is a speed hint only.
 __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                const int64_t* __restrict__ out_ptr,
-                                               const int32_t* __restrict__ out_dst, BatchDev* __restrict__ batches,
+                                               const int32_t* __restrict__ out_dst, Pools pools,
                                                int32_t V, int32_t nb, int32_t nvb, int32_t parity,
-                                               int32_t* __restrict__ cnt) {
+                                               int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
     const int32_t L = blockIdx.x;
     const int32_t xcd = L & 7;
     const int32_t q = L >> 3;
@@ -200,19 +266,25 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
     const int32_t v = (q % nvb) * 4 + wave;
     if (v >= V) return;
     const int lane = threadIdx.x & 63;
-    BatchDev& B = batches[b];
-    uint8_t* act_cur = B.act[parity];
+    const BatchDev B = batch_view(pools, b);
+    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
+    gbyte* act_cur = B.act(parity);
     if (act_cur[v] == 0) return;
     if (lane == 0) act_cur[v] = 0;
 
     const int32_t sv = B.srcv[lane];
-    const gdouble* Dl = (const gdouble*)(B.D + lane);
-    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
-    double bc = dinf(), bdu = dinf();
-    int32_t be = -1;
+    const size_t idx = (size_t)v * KL + lane;
+    const double curD = B.D[idx];
+    const uint32_t curH = B.H[idx];
+    const double curR = B.R[idx];
+    const int32_t curP = B.P[idx];
+    const gdouble* Dl = B.D + lane;
+    // (unlike the dense kernel, the running best is not seeded with curD here: rows are
+    // short, and seeding would put curD's load latency in front of the first row loads)
+    double bc = dmax(), bdu = dinf();
+    int32_t be = -1, bu = -1;
     bool tie = false;
-    int32_t e = beg;
-    for (; e + 8 <= end; e += 8) {
+    for (int32_t e = beg; e < end; e += 8) {
         int32_t u[8];
         double w[8], du[8];
 #pragma unroll
@@ -221,34 +293,152 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
             w[k] = in_w[e + k];
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) du[k] = Dl[(size_t)u[k] * KL];
+        for (int k = 0; k < 8; ++k) {
+            if (e + k >= end) w[k] = dinf();
+            du[k] = Dl[(size_t)u[k] * KL];
+        }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) relax_one(du[k], w[k], e + k, bc, bdu, be, tie);
+        for (int k = 0; k < 8; ++k) relax_arc(du[k], w[k], e + k, u[k], bc, bdu, be, bu, tie);
     }
-    for (; e < end; ++e) relax_one(Dl[(size_t)in_src[e] * KL], in_w[e], e, bc, bdu, be, tie);
 
     bool ch = false;
-    if (be >= 0 && sv >= 0 && sv != v) {
-        const size_t idx = (size_t)v * KL + lane;
-        const int32_t u = in_src[be];
-        const size_t uidx = (size_t)u * KL + lane;
-        const uint32_t hu = B.H[uidx];
-        const double ru = B.R[uidx];
-        const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? TAINT : 0u);
-        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
-        const double r = ru * in_r[be];  // topology.c:1499 totalReliability *= edgeReliability
-        if (bc != B.D[idx] || h != B.H[idx] || r != B.R[idx] || be != B.P[idx]) {
-            B.D[idx] = bc;
-            B.H[idx] = h;
-            B.R[idx] = r;
-            B.P[idx] = be;
-            ch = true;
+    if (be >= 0 && sv >= 0 && sv != v) ch = finish_vertex(B, lane, v, be, bu, bc, bdu, tie, in_r, curD, curH, curR, curP);
+    if (__ballot(ch)) {
+        gbyte* act_nxt = B.act(parity ^ 1);
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7)) + 1], 1ull);
+    }
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7))], 1ull);
+}
+
+// Dense form for complete-ish graphs (arcs >= V^2/4): W[u][v] = merged latency of arc
+// u -> v (+inf if none), WI[u][v] = its in-arc index, rows padded to Vp = roundup(V, 8).
+// One wave owns DT = 8 consecutive destinations and streams every u: one 512-byte row
+// load of d(u) for the 64 sources feeds 8 candidates (8x less cache traffic than the CSR
+// walk), the 8 weights arrive as one 64-byte scalar load.  A batch's tiles are all
+// recomputed in a round iff any vertex of that batch changed in the previous round (in a
+// complete-ish graph every vertex is an in-neighbour of every other).
+constexpr int DT = 8;
+
+__device__ __forceinline__ void relax_u(double du, double w, int32_t u, double& bc, double& bdu, int32_t& bu,
+                                        uint32_t& tie, uint32_t bit) {
+    const double c = du + w;
+    if (c <= bc) {
+        if (c < bc || du < bdu) {
+            bc = c;
+            bdu = du;
+            bu = u;
+            tie &= ~bit;
+        } else if (du == bdu) {
+            tie |= bit;
         }
     }
-    if (__ballot(ch)) {
-        uint8_t* act_nxt = B.act[parity ^ 1];
-        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
-        if (lane == 0) atomicAdd(&cnt[b], 1);
+}
+
+__global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ W, const int32_t* __restrict__ WI,
+                                                     int32_t Vp, const double* __restrict__ in_r,
+                                                     Pools pools, int32_t V, int32_t nb,
+                                                     int32_t ntb, const int32_t* __restrict__ cnt_prev,
+                                                     int32_t* __restrict__ cnt) {
+    const int32_t L = blockIdx.x;
+    const int32_t xcd = L & 7;
+    const int32_t q = L >> 3;
+    const int32_t b = xcd + 8 * (q / ntb);
+    if (b >= nb) return;
+    if (cnt_prev[b] == 0) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v0 = ((q % ntb) * 4 + wave) * DT;
+    if (v0 >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    const int32_t sv = B.srcv[lane];
+    const gdouble* Dl = B.D + lane;
+    double bc[DT], bdu[DT];
+    int32_t bu[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        const double cd = B.D[(size_t)(v0 + t) * KL + lane];  // padding rows are +inf
+        // the current distance bounds the new minimum from above (distances only decrease
+        // and the stored predecessor still offers a candidate <= cd): seed the running best
+        // with it so that only candidates c <= cd take the slow path (bdu = +inf: an equal
+        // candidate is accepted as the first of its key)
+        bc[t] = cd < dinf() ? cd : dmax();
+        bdu[t] = dinf();
+        bu[t] = -1;
+    }
+    uint32_t tie = 0;
+    for (int32_t u = 0; u < V; u += 2) {
+        const double du[2] = {Dl[(size_t)u * KL], Dl[(size_t)(u + 1) * KL]};  // row V is padding (+inf)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const double* w = W + (size_t)(u + k) * Vp + v0;
+            double c[DT];
+            bool hit = false;
+#pragma unroll
+            for (int t = 0; t < DT; ++t) {
+                c[t] = du[k] + w[t];
+                hit |= c[t] <= bc[t];
+            }
+            if (hit) {  // rare once the running bests sit at the current distances
+#pragma unroll
+                for (int t = 0; t < DT; ++t) {
+                    if (c[t] <= bc[t]) {
+                        if (c[t] < bc[t] || du[k] < bdu[t]) {
+                            bc[t] = c[t];
+                            bdu[t] = du[k];
+                            bu[t] = u + k;
+                            tie &= ~(1u << t);
+                        } else if (du[k] == bdu[t]) {
+                            tie |= 1u << t;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        const int32_t v = v0 + t;
+        if (v >= V) break;
+        bool ch = false;
+        if (bu[t] >= 0 && sv >= 0 && sv != v) {
+            const size_t idx = (size_t)v * KL + lane;
+            const int32_t arc = WI[(size_t)bu[t] * Vp + v];
+            ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx], B.H[idx],
+                               B.R[idx], B.P[idx]);
+        }
+        any |= ch;
+    }
+    if (__ballot(any) && lane == 0) cnt[b] = 1;
+}
+
+// Dense round 0: every destination's only finite candidate is its source's direct arc
+// (d = 0 elsewhere is +inf), so the first round needs one weight per (v, source), not a
+// sweep over all u.
+__global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W, const int32_t* __restrict__ WI,
+                                                    int32_t Vp, const double* __restrict__ in_r,
+                                                    Pools pools, int32_t V) {
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int lane = threadIdx.x & 63;
+    const int32_t sv = B.srcv[lane];
+    if (sv < 0) return;
+    const int32_t v0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * DT;
+    const uint32_t hs = B.H[(size_t)sv * KL + lane];
+    const double rs = B.R[(size_t)sv * KL + lane];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        const int32_t v = v0 + t;
+        if (v >= V || v == sv) continue;
+        const double w = W[(size_t)sv * Vp + v];
+        if (!(w < dinf())) continue;
+        const size_t idx = (size_t)v * KL + lane;
+        const int32_t arc = WI[(size_t)sv * Vp + v];
+        B.D[idx] = 0.0 + w;
+        B.H[idx] = ((hs & HMASK) + 1u) | (hs & TAINT);
+        B.R[idx] = rs * in_r[arc];
+        B.P[idx] = arc;
     }
 }
 
@@ -256,9 +446,14 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
 // _topology_computeShortestPathToSelf (topology.c:1545-1653): first strict minimum of the
 // OUT-incident edges in igraph order, used twice; or (F_SELF_DIJKSTRA_LOOP) the [s] path
 // through the source's self-loop (topology.c:1456-1499).
-__global__ void k_self(GraphDev g, const int32_t* __restrict__ attached, int32_t A, double* self_lat,
-                       double* self_rel, uint32_t* self_hops, uint8_t* self_kind) {
-    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per attached vertex: each lane keeps the first strict minimum of its strided
+// slice of the incidence list (position order), then a wave reduction on (latency,
+// position) picks the first strict minimum overall -- the reference's sequential rule.
+__global__ __launch_bounds__(256) void k_self(GraphDev g, const int32_t* __restrict__ attached, int32_t A,
+                                              double* self_lat, double* self_rel, uint32_t* self_hops,
+                                              uint8_t* self_kind) {
+    const int32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (i >= A) return;
     const int32_t v = attached[i];
     double lat = -1.0, rel = -1.0;
@@ -274,24 +469,36 @@ __global__ void k_self(GraphDev g, const int32_t* __restrict__ attached, int32_t
             kind = SHADOWTOPO_KIND_DIJKSTRA;
         }
     } else if (g.inc_ptr[v + 1] > g.inc_ptr[v]) {
-        double minl = 0.0, rmin = 0.0;
-        for (int64_t x = g.inc_ptr[v]; x < g.inc_ptr[v + 1]; ++x) {
-            const int32_t e = g.inc_eid[x];
-            const double l = g.elat[e];
-            if (minl == 0 || l < minl) {
+        const int64_t beg = g.inc_ptr[v], end = g.inc_ptr[v + 1];
+        double minl = dinf();
+        int64_t pos = INT64_MAX;
+        for (int64_t x = beg + lane; x < end; x += 64) {
+            const double l = g.elat[g.inc_eid[x]];
+            if (l < minl) {
                 minl = l;
-                rmin = g.erel[e];
+                pos = x;
             }
         }
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ol = __shfl_xor(minl, off);
+            const int64_t op = __shfl_xor(pos, off);
+            if (ol < minl || (ol == minl && op < pos)) {
+                minl = ol;
+                pos = op;
+            }
+        }
+        const double rmin = g.erel[g.inc_eid[pos]];
         lat = 2.0 * minl;
         rel = rmin * rmin;
         hops = 2;
         kind = SHADOWTOPO_KIND_SELF;
     }
-    self_lat[i] = lat;
-    self_rel[i] = rel;
-    self_hops[i] = hops;
-    self_kind[i] = kind;
+    if (lane == 0) {
+        self_lat[i] = lat;
+        self_rel[i] = rel;
+        self_hops[i] = hops;
+        self_kind[i] = kind;
+    }
 }
 
 // ---------------------------------------------------------------- pair dispatch
@@ -359,7 +566,7 @@ __device__ void walk_tree(const GraphDev& g, const BatchDev& B, int lane, int32_
     o.rel = rel;
 }
 
-__global__ __launch_bounds__(256) void k_compose(GraphDev g, BatchDev* __restrict__ batches,
+__global__ __launch_bounds__(256) void k_compose(GraphDev g, Pools pools,
                                                  const int32_t* __restrict__ attached, int32_t A,
                                                  const double* __restrict__ self_lat,
                                                  const double* __restrict__ self_rel,
@@ -369,7 +576,7 @@ __global__ __launch_bounds__(256) void k_compose(GraphDev g, BatchDev* __restric
                                                  int32_t row_base) {
     __shared__ double sd[64 * 65];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    BatchDev& B = batches[blockIdx.y];
+    const BatchDev B = batch_view(pools, blockIdx.y);
     const int32_t t0 = blockIdx.x * 64;
     const int32_t s = B.srcv[lane];
     double vl[16], vr[16];
@@ -409,7 +616,7 @@ __global__ __launch_bounds__(256) void k_compose(GraphDev g, BatchDev* __restric
         vh[i] = o.hops;
         vk[i] = o.kind;
     }
-    if (taint_any) atomicOr(&B.replay_mask, 1ull << lane);
+    if (taint_any) atomicOr(B.mask, 1ull << lane);
 
     const int32_t nrow = 64;
     // lat
@@ -617,12 +824,12 @@ __global__ void k_compose_replay(GraphDev g, ReplayDev rp, const int32_t* __rest
 }
 
 // parity tooling: [V][64] -> per-source rows
-__global__ void k_extract(GraphDev g, BatchDev* __restrict__ batches, int32_t nsrc, double* dist, int32_t* pred,
+__global__ void k_extract(GraphDev g, Pools pools, int32_t nsrc, double* dist, int32_t* pred,
                           uint32_t* hops, uint8_t* tie) {
     const int32_t v = blockIdx.x * blockDim.x + threadIdx.x;
     const int32_t j = blockIdx.y;
     if (v >= g.V || j >= nsrc) return;
-    BatchDev& B = batches[0];
+    const BatchDev B = batch_view(pools, 0);
     const size_t idx = (size_t)v * KL + j;
     const size_t o = (size_t)j * g.V + v;
     dist[o] = B.D[idx];
@@ -642,6 +849,10 @@ struct DevBuf {
 
 struct shadowtopo_engine {
     int32_t V = 0;
+    int32_t Vp = 0;  // V rounded up to a multiple of 8 (dense tiles, padding row)
+    int32_t dense = 0;
+    const double* d_W = nullptr;    // dense mode: [Vp][Vp] arc latency, +inf if none
+    const int32_t* d_WI = nullptr;  // dense mode: [Vp][Vp] in-arc index, -1 if none
     int64_t E = 0;
     int64_t n_arcs = 0;
     uint32_t flags = 0;
@@ -664,8 +875,8 @@ struct shadowtopo_engine {
     bool self_ready = false;
     // batch pool
     int32_t nb_cap = 0;
-    std::vector<BatchDev> h_batches;
-    BatchDev* d_batches = nullptr;
+    Pools pools{};                       // device pools for nb_cap batch slots
+    std::vector<int32_t> h_srcv, h_row;  // host staging of the per-lane tables
     std::vector<void*> batch_allocs;
     int32_t* d_cnt = nullptr;
     int32_t* h_cnt = nullptr;  // pinned
@@ -681,6 +892,9 @@ struct shadowtopo_engine {
     int32_t opt_timing = 0;
     int64_t opt_max_rounds = 0;
     int32_t opt_force_replay = 0;
+    int32_t opt_profile = 0;
+    unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
+    unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     shadowtopo_stats st{};
 };
@@ -719,37 +933,37 @@ void counting_sort(const std::vector<int32_t>& key, int32_t nkeys, std::vector<i
 void free_batches(shadowtopo_engine* eng) {
     for (void* p : eng->batch_allocs) (void)hipFree(p);
     eng->batch_allocs.clear();
-    eng->d_batches = nullptr;
+    eng->pools = Pools{};
     eng->d_cnt = nullptr;
     if (eng->h_cnt) (void)hipHostFree(eng->h_cnt);
     eng->h_cnt = nullptr;
-    eng->h_batches.clear();
+    eng->h_srcv.clear();
+    eng->h_row.clear();
     eng->nb_cap = 0;
 }
 
 int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
     if (eng->nb_cap >= nb) return SHADOWTOPO_OK;
     free_batches(eng);
-    const size_t VK = (size_t)eng->V * KL;
-    eng->h_batches.assign(nb, BatchDev{});
-    for (int32_t b = 0; b < nb; ++b) {
-        BatchDev& B = eng->h_batches[b];
-        int rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.D, VK * sizeof(double)))) return rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.H, VK * sizeof(uint32_t)))) return rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.R, VK * sizeof(double)))) return rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.P, VK * sizeof(int32_t)))) return rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.act[0], (size_t)eng->V))) return rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&B.act[1], (size_t)eng->V))) return rc;
-        for (int j = 0; j < KL; ++j) {
-            B.srcv[j] = -1;
-            B.row[j] = -1;
-        }
-    }
+    const size_t VK = (size_t)eng->Vp * KL;
+    Pools& P = eng->pools;
+    P.vk = (int64_t)VK;
+    P.Vp = eng->Vp;
     int rc;
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_batches, sizeof(BatchDev) * nb))) return rc;
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * nb))) return rc;
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.D, VK * nb * sizeof(double))) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.H, VK * nb * sizeof(uint32_t))) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.R, VK * nb * sizeof(double))) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.P, VK * nb * sizeof(int32_t))) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.act, (size_t)eng->Vp * 2 * nb)) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.srcv, sizeof(int32_t) * KL * nb)) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.mask, sizeof(unsigned long long) * nb)))
+        return rc;
+    eng->h_srcv.assign((size_t)KL * nb, -1);
+    eng->h_row.assign((size_t)KL * nb, -1);
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
     HIP_TRY(hipHostMalloc((void**)&eng->h_cnt, sizeof(int32_t) * nb, hipHostMallocDefault));
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->prof_buf, sizeof(unsigned long long) * 16 * nb))) return rc;
     eng->nb_cap = nb;
     return SHADOWTOPO_OK;
 }
@@ -771,7 +985,7 @@ int ensure_replay(shadowtopo_engine* eng) {
 
 int32_t default_nb(const shadowtopo_engine* eng) {
     if (eng->opt_nb > 0) return eng->opt_nb;
-    const double per_batch = (double)eng->V * KL * 24.0 + 2.0 * eng->V;
+    const double per_batch = (double)eng->Vp * KL * 24.0 + 2.0 * eng->Vp;
     const double budget = 24.0e9;
     int32_t nb = (int32_t)std::max(1.0, std::min(16.0, std::floor(budget / per_batch)));
     return nb;
@@ -780,7 +994,7 @@ int32_t default_nb(const shadowtopo_engine* eng) {
 int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->self_ready) return SHADOWTOPO_OK;
     if (eng->A > 0) {
-        hipLaunchKernelGGL(k_self, dim3((eng->A + 255) / 256), dim3(256), 0, s, eng->g, eng->d_attached, eng->A,
+        hipLaunchKernelGGL(k_self, dim3((eng->A + 3) / 4), dim3(256), 0, s, eng->g, eng->d_attached, eng->A,
                            eng->d_self_lat, eng->d_self_rel, eng->d_self_hops, eng->d_self_kind);
         HIP_TRY(hipGetLastError());
     }
@@ -793,26 +1007,45 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = eng->V;
     const GraphDev& g = eng->g;
     {
-        const size_t total = (size_t)V * KL;
+        const size_t total = (size_t)eng->Vp * KL;
         int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
-        hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->d_batches, V);
-        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->d_batches);
+        hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp);
+        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools);
         HIP_TRY(hipGetLastError());
     }
     const int32_t nvb = (V + 3) / 4;
     const int64_t nblocks = (int64_t)8 * nvb * ((nbg + 7) / 8);
+    const int32_t ntb = (V + 4 * DT - 1) / (4 * DT);
+    const int64_t nblocks_dense = (int64_t)8 * ntb * ((nbg + 7) / 8);
     if (nblocks > 0x7fffffff) return fail(SHADOWTOPO_EINVAL, "grid too large");
     const int64_t max_rounds = eng->opt_max_rounds > 0 ? eng->opt_max_rounds : 4LL * V + 64;
+    eng->d_prof = eng->opt_profile ? eng->prof_buf : nullptr;
+    if (eng->d_prof) HIP_TRY(hipMemsetAsync(eng->d_prof, 0, sizeof(unsigned long long) * 16 * nbg, s));
+    if (eng->dense) {
+        hipLaunchKernelGGL(k_seed_dense, dim3(ntb, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp, g.in_r,
+                           eng->pools, V);
+        HIP_TRY(hipGetLastError());
+        // round 0 consumes "changed" flags of a virtual round -1: every batch changed
+        HIP_TRY(hipMemsetAsync(eng->d_cnt + eng->nb_cap, 0x01, sizeof(int32_t) * nbg, s));
+    }
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
-        HIP_TRY(hipMemsetAsync(eng->d_cnt, 0, sizeof(int32_t) * nbg, s));
+        int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
+        int32_t* cnt_prev = eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
+        HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
-        hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
-                           g.out_ptr, g.out_dst, eng->d_batches, V, nbg, nvb, (int32_t)(round & 1), eng->d_cnt);
+        if (eng->dense) {
+            hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W, eng->d_WI,
+                               eng->Vp, g.in_r, eng->pools, V, nbg, ntb, cnt_prev, cnt_cur);
+        } else {
+            hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
+                               g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
+                               eng->d_prof);
+        }
         HIP_TRY(hipGetLastError());
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev1, s));
-        HIP_TRY(hipMemcpyAsync(eng->h_cnt, eng->d_cnt, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(eng->h_cnt, cnt_cur, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         eng->st.relax_launches++;
         eng->st.rounds++;
@@ -824,6 +1057,14 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         int64_t changed = 0;
         for (int32_t b = 0; b < nbg; ++b) changed += eng->h_cnt[b];
         if (changed == 0) break;
+    }
+    if (eng->d_prof) {
+        std::vector<unsigned long long> h((size_t)16 * nbg);
+        HIP_TRY(hipMemcpy(h.data(), eng->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < h.size(); i += 2) {
+            eng->st.visits += (int64_t)h[i];
+            eng->st.changes += (int64_t)h[i + 1];
+        }
     }
     return SHADOWTOPO_OK;
 }
@@ -865,31 +1106,31 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             row_base = r0;
         }
         for (int32_t b = 0; b < nbg; ++b) {
-            BatchDev& B = eng->h_batches[b];
             for (int j = 0; j < KL; ++j) {
                 const int32_t row = r0 + b * KL + j;
-                B.srcv[j] = row < r1 ? eng->h_attached[row] : -1;
-                B.row[j] = row < r1 ? row : -1;
+                eng->h_srcv[(size_t)b * KL + j] = row < r1 ? eng->h_attached[row] : -1;
+                eng->h_row[(size_t)b * KL + j] = row < r1 ? row : -1;
             }
-            B.replay_mask = 0;
         }
-        HIP_TRY(hipMemcpyAsync(eng->d_batches, eng->h_batches.data(), sizeof(BatchDev) * nbg,
+        HIP_TRY(hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL * nbg,
                                hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(eng->pools.row, eng->h_row.data(), sizeof(int32_t) * KL * nbg,
+                               hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(eng->pools.mask, 0, sizeof(unsigned long long) * nbg, s));
         if (!complete) {
             if ((rc = run_rounds(eng, nbg, s))) return rc;
         }
         auto t0 = std::chrono::steady_clock::now();
         if (A > 0) {
-            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(256), 0, s, eng->g, eng->d_batches,
+            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(256), 0, s, eng->g, eng->pools,
                                eng->d_attached, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
                                eng->d_self_kind, dl, dr, dh, dk, row_base);
             HIP_TRY(hipGetLastError());
         }
         // collect tie-tainted sources
         std::vector<unsigned long long> masks(nbg);
-        for (int32_t b = 0; b < nbg; ++b)
-            HIP_TRY(hipMemcpyAsync(&masks[b], &eng->d_batches[b].replay_mask, sizeof(unsigned long long),
-                                   hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(masks.data(), eng->pools.mask, sizeof(unsigned long long) * nbg,
+                               hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         eng->st.compose_ms +=
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1062,6 +1303,12 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         i = j + 1;
     }
     for (int32_t v = 0; v < V; ++v) in_ptr[(size_t)v + 1] += in_ptr[v];
+    for (int k = 0; k < CSR_PAD; ++k) {  // padding arcs for the unclamped chunk loads
+        in_src.push_back(0);
+        in_w.push_back(std::numeric_limits<double>::infinity());
+        in_r.push_back(0.0);
+        in_eid.push_back(-1);
+    }
     std::vector<int64_t> out_ptr;
     std::vector<int32_t> out_dst;
     if (directed) {
@@ -1122,7 +1369,18 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     }
     eng->flags = flags;
     eng->multigraph = multigraph;
-    eng->n_arcs = (int64_t)in_src.size();
+    eng->n_arcs = (int64_t)in_src.size() - CSR_PAD;
+    eng->Vp = (V + 7) / 8 * 8;
+    {
+        const double VV = (double)V * (double)V;
+        const bool fits = (double)eng->Vp * eng->Vp * 12.0 <= 24.0e9;
+        if (flags & SHADOWTOPO_F_FORCE_DENSE)
+            eng->dense = fits ? 1 : 0;
+        else if (flags & SHADOWTOPO_F_FORCE_CSR)
+            eng->dense = 0;
+        else
+            eng->dense = (!(flags & SHADOWTOPO_F_COMPLETE) && fits && (double)eng->n_arcs >= 0.25 * VV) ? 1 : 0;
+    }
 
     GraphDev& g = eng->g;
     g.V = V;
@@ -1137,6 +1395,20 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         (rc = upload(eng, vfac, &g.vfac)) || (rc = upload(eng, loop_eid, &g.loop_eid))) {
         shadowtopo_destroy(eng);
         return rc;
+    }
+    if (eng->dense) {
+        const size_t Vp = (size_t)eng->Vp;
+        std::vector<double> W(Vp * Vp, std::numeric_limits<double>::infinity());
+        std::vector<int32_t> WI(Vp * Vp, -1);
+        for (int32_t v = 0; v < V; ++v)
+            for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) {
+                W[(size_t)in_src[x] * Vp + v] = in_w[x];
+                WI[(size_t)in_src[x] * Vp + v] = (int32_t)x;
+            }
+        if ((rc = upload(eng, W, &eng->d_W)) || (rc = upload(eng, WI, &eng->d_WI))) {
+            shadowtopo_destroy(eng);
+            return rc;
+        }
     }
     if (directed) {
         if ((rc = upload(eng, out_ptr, &g.out_ptr)) || (rc = upload(eng, out_dst, &g.out_dst))) {
@@ -1161,6 +1433,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->st.n_arcs = eng->n_arcs;
     eng->st.device = device;
     eng->st.multigraph = multigraph;
+    eng->st.dense = eng->dense;
     *out = eng;
     return SHADOWTOPO_OK;
 }
@@ -1230,6 +1503,9 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_FORCE_REPLAY:
             eng->opt_force_replay = value ? 1 : 0;
             return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_PROFILE:
+            eng->opt_profile = value ? 1 : 0;
+            return SHADOWTOPO_OK;
         default:
             return fail(SHADOWTOPO_EINVAL, "unknown option %d", key);
     }
@@ -1271,18 +1547,17 @@ int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_so
     HIP_TRY(hipMalloc((void**)&d_tie, KL * V));
     for (int32_t i0 = 0; i0 < n_sources && rc == 0; i0 += KL) {
         const int32_t n = std::min(KL, n_sources - i0);
-        BatchDev& B = eng->h_batches[0];
         for (int j = 0; j < KL; ++j) {
-            B.srcv[j] = j < n ? sources[i0 + j] : -1;
-            B.row[j] = -1;
+            eng->h_srcv[j] = j < n ? sources[i0 + j] : -1;
+            eng->h_row[j] = -1;
         }
-        B.replay_mask = 0;
-        if (hipMemcpyAsync(eng->d_batches, &B, sizeof(BatchDev), hipMemcpyHostToDevice, s) != hipSuccess) {
+        if (hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL, hipMemcpyHostToDevice, s) !=
+            hipSuccess) {
             rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
             break;
         }
         if ((rc = run_rounds(eng, 1, s))) break;
-        hipLaunchKernelGGL(k_extract, dim3((eng->V + 255) / 256, n), dim3(256), 0, s, eng->g, eng->d_batches, n,
+        hipLaunchKernelGGL(k_extract, dim3((eng->V + 255) / 256, n), dim3(256), 0, s, eng->g, eng->pools, n,
                            d_dist, d_pred, d_hops, d_tie);
         const size_t cnt = (size_t)n * V;
         const size_t o = (size_t)i0 * V;
@@ -1317,6 +1592,7 @@ void shadowtopo_reset_stats(shadowtopo_engine* eng) {
     eng->st.n_attached = keep.n_attached;
     eng->st.device = keep.device;
     eng->st.multigraph = keep.multigraph;
+    eng->st.dense = keep.dense;
 }
 
 int shadowtopo_is_complete(const shadowtopo_engine* eng) {

@@ -434,7 +434,13 @@ static int check_properties(Topology* top) {
     top->complete = is_complete(top);
     int prefer = 0;
     const gml_attr* pa = gml_find(top->gml, GML_GRAPH, "preferdirectpaths");
-    if (pa && pa->type == GML_STRING) {
+    if (pa && pa->type != GML_STRING) {
+        /* the reference reaches igraph_cattribute_GAS on a non-string attribute here
+         * (topology.c:292-293), which igraph's default error handler aborts on */
+        st_critical("graph attribute 'preferdirectpaths' must be a string");
+        return 0;
+    }
+    if (pa) {
         const char* value = gml_str(pa, 0);
         if (value && value[0]) {
             int yes = !strncasecmp(value, "true", 4) || !strncasecmp(value, "yes", 3) || !strncasecmp(value, "1", 1);

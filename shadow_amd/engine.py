@@ -19,6 +19,8 @@ F_COMPLETE = 0x2
 F_PREFER_DIRECT = 0x4
 F_SELF_DIJKSTRA_LOOP = 0x8
 F_AUTO_COMPLETE = 0x10
+F_FORCE_DENSE = 0x20
+F_FORCE_CSR = 0x40
 
 MEM_HOST = 0
 MEM_DEVICE = 1
@@ -29,6 +31,7 @@ OPT_BATCHES_IN_FLIGHT = 1
 OPT_TIMING = 2
 OPT_MAX_ROUNDS = 3
 OPT_FORCE_REPLAY = 4
+OPT_PROFILE = 5
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (
@@ -49,7 +52,8 @@ class Stats(ctypes.Structure):
         ("rounds", ctypes.c_int64), ("relax_launches", ctypes.c_int64), ("replayed_sources", ctypes.c_int64),
         ("tainted_pairs", ctypes.c_int64), ("relax_ms", ctypes.c_double), ("compose_ms", ctypes.c_double),
         ("replay_ms", ctypes.c_double), ("wall_ms", ctypes.c_double), ("device", ctypes.c_int32),
-        ("multigraph", ctypes.c_int32),
+        ("multigraph", ctypes.c_int32), ("dense", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("visits", ctypes.c_int64), ("changes", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -107,7 +111,7 @@ class Engine:
     """Device-resident topology graph + attached-pair computation."""
 
     def __init__(self, n, src, dst, latency, packetloss, vertex_packetloss=None, directed=False,
-                 prefer_direct=False, complete=None, self_dijkstra_loop=False, device=0):
+                 prefer_direct=False, complete=None, self_dijkstra_loop=False, device=0, layout="auto"):
         L = lib()
         self._keep = []
         src = np.ascontiguousarray(src, np.int32)
@@ -122,6 +126,10 @@ class Engine:
             flags |= F_PREFER_DIRECT
         if self_dijkstra_loop:
             flags |= F_SELF_DIJKSTRA_LOOP
+        if layout == "dense":
+            flags |= F_FORCE_DENSE
+        elif layout == "csr":
+            flags |= F_FORCE_CSR
         if complete is None:
             flags |= F_AUTO_COMPLETE
         elif complete:

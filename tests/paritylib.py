@@ -18,8 +18,8 @@ def oracle_matrix(g, self_loop_rule=False, nthreads=4):
     return lat, rel, hops, kind, og
 
 
-def engine_matrix(g, self_loop_rule=False, **opts):
-    eng = E.Engine.from_synth(g, self_dijkstra_loop=self_loop_rule)
+def engine_matrix(g, self_loop_rule=False, layout="auto", **opts):
+    eng = E.Engine.from_synth(g, self_dijkstra_loop=self_loop_rule, layout=layout)
     for k, v in opts.items():
         eng.set_option(getattr(E, "OPT_" + k.upper()), v)
     eng.set_attached(g.attached)
@@ -41,9 +41,9 @@ def assert_bitexact(name, got, want):
                              f"want {want[i, j]!r}")
 
 
-def compare(g, self_loop_rule=False, rel_tol=0.0, **opts):
+def compare(g, self_loop_rule=False, rel_tol=0.0, layout="auto", **opts):
     lat_o, rel_o, hops_o, kind_o, _ = oracle_matrix(g, self_loop_rule)
-    lat_e, rel_e, hops_e, kind_e, st = engine_matrix(g, self_loop_rule, **opts)
+    lat_e, rel_e, hops_e, kind_e, st = engine_matrix(g, self_loop_rule, layout=layout, **opts)
     assert_bitexact("kind", kind_e, kind_o)
     assert_bitexact("latency", lat_e, lat_o)
     assert_bitexact("hops", hops_e, hops_o)

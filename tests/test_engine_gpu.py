@@ -121,3 +121,49 @@ def test_sssp_full_rows_vs_oracle():
         notie = tie[k] == 0
         assert np.array_equal(pred[k][notie], pv[notie])
     eng.close()
+
+
+# ---- dense-tile relaxation (k_relax_dense): forced on graphs of every shape
+@pytest.mark.parametrize("seed", [1, 2])
+def test_dense_layout_sparse_graph(seed):
+    g = synth.random_sparse(V=301, avg_deg=5, seed=seed)  # odd V: padding row / column
+    st = compare(g, layout="dense")
+    assert st["dense"] == 1
+
+
+def test_dense_layout_directed():
+    g = synth.random_sparse(V=203, avg_deg=4, seed=5, directed=True)
+    assert compare(g, layout="dense")["dense"] == 1
+
+
+def test_dense_layout_vertex_loss_and_prefer_direct():
+    rng = np.random.default_rng(4)
+    g = synth.random_sparse(V=150, avg_deg=8, seed=6, vloss=rng.uniform(0, 0.1, 150))
+    g.prefer_direct = True
+    assert compare(g, layout="dense")["dense"] == 1
+
+
+def test_dense_layout_ties_and_multigraph():
+    g = synth.integer_grid(rows=9, cols=11, seed=2)
+    st = compare(g, layout="dense")
+    assert st["dense"] == 1 and st["replayed_sources"] > 0
+    g = synth.random_sparse(V=100, avg_deg=4, seed=17)
+    rng = np.random.default_rng(1)
+    pick = rng.choice(np.nonzero(g.src != g.dst)[0], 30, replace=False)
+    g.src = np.concatenate([g.src, g.dst[pick]])
+    g.dst = np.concatenate([g.dst, g.src[pick]])
+    g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.3, 1.7, 30)])
+    g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 30)])
+    compare(g, layout="dense")
+
+
+def test_geometric_auto_dense():
+    g = synth.geometric_complete_ish(V=700, A=130)
+    st = compare(g)
+    assert st["dense"] == 1  # complete-ish: auto layout picks dense
+
+
+def test_csr_forced_on_dense_graph():
+    g = synth.geometric_complete_ish(V=300, A=70)
+    st = compare(g, layout="csr")
+    assert st["dense"] == 0

@@ -1,0 +1,148 @@
+"""GPU: the drop-in topology API (topology_hip.h) end to end -- GraphML -> validation ->
+attach -> per-packet getters -- against the oracle and the reference's own fixtures."""
+import json
+import lzma
+import os
+
+import numpy as np
+import pytest
+
+from paritylib import oracle_matrix
+from shadow_amd import synth
+from shadow_amd import topology as T
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def quiet():
+    T.set_log_level(1)
+
+
+def write(tmp_path, name, text):
+    p = tmp_path / name
+    p.write_text(text)
+    return str(p)
+
+
+def with_vertex_ips(g):
+    ips = [f"10.{(v >> 16) & 255}.{(v >> 8) & 255}.{(v & 255)}" if (v & 255) else f"10.{200 + ((v >> 16) & 7)}.{(v >> 8) & 255}.1"
+           for v in range(g.n)]
+    return {"ip": ("d1", "string", ips)}, ips
+
+
+def attach_all(top, ips, vertices, base=0):
+    """one host per vertex, pinned by an exact IP hint; host IPs in 11.x"""
+    r = T.Random(7)
+    hosts = []
+    for k, v in enumerate(vertices, start=base):
+        a = T.Address(f"11.{(k >> 16) & 255}.{(k >> 8) & 255}.{k & 255}")
+        top.attach(a, r, ipHint=ips[v])
+        assert top.vertex_of_ip(a.ip) == v
+        hosts.append(a)
+    return hosts
+
+
+def check_against_oracle(tmp_path, g, n_hosts=None):
+    va, ips = with_vertex_ips(g)
+    text = synth.to_graphml(g, extra_vattr=va, prefer_direct=("true" if g.prefer_direct else None))
+    top = T.Topology.new(write(tmp_path, "g.xml", text))
+    assert top is not None
+    hosts = attach_all(top, ips, g.attached)
+    lat_o, rel_o, hops_o, kind_o, _ = oracle_matrix(g)
+    for i, a in enumerate(hosts):
+        for j, b in enumerate(hosts):
+            lat = top.getLatency(a, b)
+            assert lat == lat_o[i, j], (i, j, lat, lat_o[i, j])
+            assert top.getReliability(a, b) == rel_o[i, j]
+            assert top.isRoutable(a, b)
+    inf = top.info()
+    assert inf["computed_for"] == len(hosts)
+    valid = kind_o > 0
+    assert T.last_min_time_jump() == lat_o[valid].min() == inf["min_path_latency"]
+    return top, hosts
+
+
+def test_sparse_graph_all_pairs(tmp_path):
+    g = synth.random_sparse(V=180, avg_deg=4, seed=41, A=60)
+    top, _ = check_against_oracle(tmp_path, g)
+    top.free()
+
+
+def test_prefer_direct_graph(tmp_path):
+    g = synth.random_sparse(V=120, avg_deg=6, seed=42, A=50)
+    g.prefer_direct = True
+    top, _ = check_against_oracle(tmp_path, g)
+    assert top.info()["prefers_direct_paths"] == 1
+    top.free()
+
+
+def test_vertex_loss_graph(tmp_path):
+    rng = np.random.default_rng(1)
+    g = synth.random_sparse(V=120, avg_deg=4, seed=43, A=40, vloss=rng.uniform(0, 0.05, 120))
+    top, _ = check_against_oracle(tmp_path, g)
+    top.free()
+
+
+def test_packet_counters_one_per_unordered_pair(tmp_path):
+    g = synth.random_sparse(V=60, avg_deg=4, seed=44, A=10)
+    top, hosts = check_against_oracle(tmp_path, g)
+    a, b, c = hosts[0], hosts[1], hosts[2]
+    for _ in range(3):
+        top.incrementPathPacketCounter(a, b)
+    top.incrementPathPacketCounter(b, a)
+    top.incrementPathPacketCounter(c, c)
+    va, vb, vc = (top.vertex_of_ip(h.ip) for h in (a, b, c))
+    assert top.packet_count(va, vb) == 4 == top.packet_count(vb, va)
+    assert top.packet_count(vc, vc) == 1
+    assert top.packet_count(va, vc) == 0
+    top.free()
+
+
+def test_shipped_topology_complete_direct_rule(tmp_path):
+    text = lzma.open(os.path.join(GOLD, "c1_topology.graphml.xml.xz"), "rt").read()
+    top = T.Topology.new(write(tmp_path, "c1.xml", text))
+    gold = np.load(os.path.join(GOLD, "c1_direct.npz"))
+    r = T.Random(99)
+    hosts = [T.Address(f"11.0.{k // 200}.{k % 200 + 1}") for k in range(400)]
+    for h in hosts:
+        top.attach(h, r, countrycodeHint=None)
+    verts = [top.vertex_of_ip(h.ip) for h in hosts]
+    for i in range(0, 400, 7):
+        for j in range(0, 400, 5):
+            a, b = hosts[i], hosts[j]
+            assert top.getLatency(a, b) == gold["lat"][verts[i], verts[j]]
+            assert top.getReliability(a, b) == gold["rel"][verts[i], verts[j]]
+    assert top.info()["is_complete"] == 1
+    top.free()
+
+
+def test_reference_test_topologies(tmp_path):
+    """the 1-vertex graphs of resource/examples/shadow.config.xml and src/test/**: two
+    hosts on the one vertex (the tgen client/server example)"""
+    for k, case in enumerate(json.load(open(os.path.join(GOLD, "ref_test_graphs.json")))):
+        top = T.Topology.new(write(tmp_path, f"t{k}.xml", case["graphml"]))
+        assert top is not None
+        r = T.Random(1)
+        server, client = T.Address("11.0.0.1", "server"), T.Address("11.0.0.2", "client")
+        top.attach(server, r)
+        top.attach(client, r)
+        assert top.getLatency(client, server) == case["self_latency"] == 50.0
+        assert top.getReliability(client, server) == case["self_reliability"]
+        assert top.getLatency(server, server) == 50.0
+        top.free()
+
+
+def test_late_attach_recomputes(tmp_path):
+    g = synth.random_sparse(V=80, avg_deg=4, seed=45, A=20)
+    va, ips = with_vertex_ips(g)
+    top = T.Topology.new(write(tmp_path, "l.xml", synth.to_graphml(g, extra_vattr=va)))
+    hosts = attach_all(top, ips, g.attached[:10])
+    l01 = top.getLatency(hosts[0], hosts[1])
+    assert top.info()["computed_for"] == 10
+    more = attach_all(top, ips, g.attached[10:12], base=100)
+    assert top.getLatency(hosts[0], more[1]) > 0
+    assert top.info()["computed_for"] == 12
+    assert top.getLatency(hosts[0], hosts[1]) == l01
+    top.free()

@@ -1,0 +1,270 @@
+"""CPU tests of the C host shim (libshadowtopo_hip.so, topology_hip.h): the library loads
+and exports every declared symbol, GraphML ingest matches the independent reader,
+validation accepts/rejects like topology.c, attachment matches the restated reference
+algorithm.  No GPU: path queries must fail loudly (-1), never fall back to the CPU."""
+import lzma
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import attach_ref
+from oracle.graphml_ref import read_graphml
+from shadow_amd import engine as E
+from shadow_amd import synth
+from shadow_amd import topology as T
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def quiet():
+    T.set_log_level(1)
+
+
+def declared_functions():
+    names = set()
+    for h in os.listdir(INCLUDE):
+        txt = open(os.path.join(INCLUDE, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\([^;{]*\)\s*;", txt, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = E.lib()
+    names = declared_functions()
+    assert set(E.ENGINE_SYMBOLS) <= names
+    assert set(T.TOPOLOGY_SYMBOLS) <= names
+    assert set(T.EXT_SYMBOLS) <= names
+    for n in sorted(names):
+        assert hasattr(L, n), f"libshadowtopo_hip.so does not export {n}"
+
+
+def write(tmp_path, name, text):
+    p = tmp_path / name
+    p.write_text(text)
+    return str(p)
+
+
+def test_shipped_topology_loads(tmp_path):
+    text = lzma.open(os.path.join(GOLD, "c1_topology.graphml.xml.xz"), "rt").read()
+    top = T.Topology.new(write(tmp_path, "c1.graphml.xml", text))
+    assert top is not None
+    inf = top.info()
+    assert (inf["n_vertices"], inf["n_edges"]) == (183, 16836)
+    assert inf["is_complete"] == 1 and inf["is_connected"] == 1 and inf["cluster_count"] == 1
+    assert inf["is_directed"] == 0 and inf["prefers_direct_paths"] == 0
+    ref = read_graphml(text)
+    src, dst, lat, loss, vl = top.edges()
+    assert np.array_equal(src, ref.src) and np.array_equal(dst, ref.dst)
+    assert np.array_equal(lat, ref.enum("latency")) and np.array_equal(loss, ref.enum("packetloss"))
+    assert np.array_equal(vl, ref.vnum("packetloss"))
+    assert top.vertex_of_id(ref.ids[17]) == 17
+    top.free()
+
+
+@pytest.mark.parametrize("gen", ["sparse", "directed", "vloss", "geo"])
+def test_graphml_ingest_matches_reference_reader(tmp_path, gen):
+    if gen == "sparse":
+        g = synth.random_sparse(V=300, seed=1)
+    elif gen == "directed":
+        g = synth.random_sparse(V=200, seed=2, directed=True)
+    elif gen == "vloss":
+        vl = np.where(np.arange(150) % 3 == 0, np.nan, np.linspace(0, 0.2, 150))
+        g = synth.random_sparse(V=150, seed=3, vloss=vl)
+    else:
+        g = synth.geometric_complete_ish(V=120, A=10)
+    text = synth.to_graphml(g)
+    top = T.Topology.new(write(tmp_path, "g.xml", text))
+    assert top is not None
+    ref = read_graphml(text)
+    src, dst, lat, loss, vl = top.edges()
+    assert np.array_equal(src, ref.src) and np.array_equal(dst, ref.dst)
+    assert np.array_equal(lat, ref.enum("latency")) and np.array_equal(lat, g.latency)
+    assert np.array_equal(loss, g.packetloss)
+    assert np.array_equal(vl.view(np.uint64), ref.vnum("packetloss").view(np.uint64))
+    assert top.info()["is_directed"] == int(g.directed)
+    top.free()
+
+
+def test_example_config_graph_and_quirks(tmp_path):
+    # CDATA, entities, comments, node declared after use, for="all" key with default
+    text = """<?xml version="1.0"?>
+<!-- comment <node id="x"/> -->
+<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+ <key attr.name="latency" attr.type="double" for="edge" id="l"><default>7.5</default></key>
+ <key attr.name="packetloss" attr.type="double" for="all" id="p"/>
+ <key attr.name="bandwidthdown" attr.type="int" for="node" id="bd"/>
+ <key attr.name="bandwidthup" attr.type="int" for="node" id="bu"/>
+ <key attr.name="type" attr.type="string" for="node" id="t"/>
+ <graph edgedefault="undirected">
+  <edge source="b&amp;c" target="a"><data key="p">0.5</data></edge>
+  <node id="a"><data key="bd">10</data><data key="bu">20</data><data key="t"><![CDATA[re<lay]]></data>
+   <data key="p">0.25</data></node>
+  <node id="b&amp;c"><data key="bd">1</data><data key="bu">2</data></node>
+  <edge source="a" target="a"><data key="l">3.0</data><data key="p">0.0</data></edge>
+  <edge source="b&amp;c" target="b&amp;c"><data key="p">0.1</data></edge>
+ </graph>
+</graphml>"""
+    ref = read_graphml(text)
+    assert ref.ids == ["b&c", "a"]
+    top = T.Topology.new(write(tmp_path, "q.xml", text))
+    assert top is not None
+    src, dst, lat, loss, vl = top.edges()
+    assert list(src) == [0, 1, 0] and list(dst) == [1, 1, 0]
+    assert list(lat) == [7.5, 3.0, 7.5]
+    assert list(loss) == [0.5, 0.0, 0.1]
+    assert np.isnan(vl[0]) and vl[1] == 0.25
+    assert top.vertex_of_id("b&c") == 0
+    inf = top.info()
+    assert inf["is_complete"] == 1  # 2 vertices: each has one non-loop + loop twice - 1 = 2
+    top.free()
+
+
+BASE = """<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+ <key attr.name="latency" attr.type="{lt}" for="edge" id="l"/>
+ <key attr.name="packetloss" attr.type="double" for="edge" id="p"/>
+ <key attr.name="bandwidthdown" attr.type="int" for="node" id="bd"/>
+ <key attr.name="bandwidthup" attr.type="int" for="node" id="bu"/>
+ <key attr.name="packetloss" attr.type="double" for="node" id="vp"/>
+ {gkey}
+ <graph edgedefault="{ed}">{gdata}
+  <node id="a"><data key="bd">10</data><data key="bu">{bu}</data><data key="vp">{vp}</data></node>
+  <node id="b"><data key="bd">10</data><data key="bu">10</data></node>
+  <node id="c"><data key="bd">10</data><data key="bu">10</data></node>
+  <edge source="a" target="b"><data key="l">{lat}</data><data key="p">{loss}</data></edge>
+  <edge source="b" target="c"><data key="l">5</data><data key="p">0.0</data></edge>
+  {extra}
+ </graph>
+</graphml>"""
+
+
+def mk(**kw):
+    d = dict(lt="double", ed="undirected", bu="10", vp="0.0", lat="3.0", loss="0.1", extra="", gkey="", gdata="")
+    d.update(kw)
+    return BASE.format(**d)
+
+
+@pytest.mark.parametrize("kw,ok", [
+    ({}, True),
+    ({"lat": "0"}, False),              # latency must be > 0 (topology.c:1070)
+    ({"lat": "-2"}, False),
+    ({"loss": "1.5"}, False),           # packetloss in [0,1] (topology.c:1090)
+    ({"bu": "0"}, False),               # bandwidthup > 0 (topology.c:866-874)
+    ({"vp": "2"}, False),               # vertex packetloss in [0,1] (topology.c:957-969)
+    ({"lt": "string"}, False),          # latency must be NUMERIC (topology.c:680-681)
+    ({"extra": '<node id="d"><data key="bd">1</data><data key="bu">1</data></node>'}, False),  # disconnected
+    ({"ed": "directed"}, False),        # a->b->c not strongly connected
+    ({"ed": "directed", "extra": '<edge source="c" target="a"><data key="l">1</data><data key="p">0</data></edge>'},
+     True),
+])
+def test_validation(tmp_path, kw, ok):
+    top = T.Topology.new(write(tmp_path, "v.xml", mk(**kw)))
+    assert (top is not None) == ok
+    if top:
+        top.free()
+
+
+@pytest.mark.parametrize("val,want", [("true", 1), ("Yes", 1), ("1", 1), ("false", 0), ("no", 0)])
+def test_preferdirectpaths(tmp_path, val, want):
+    top = T.Topology.new(write(tmp_path, "pd.xml", mk(
+        gkey='<key attr.name="preferdirectpaths" attr.type="string" for="graph" id="g"/>',
+        gdata=f'<data key="g">{val}</data>')))
+    assert top is not None and top.info()["prefers_direct_paths"] == want
+    top.free()
+
+
+def test_preferdirectpaths_boolean_type_rejected(tmp_path):
+    top = T.Topology.new(write(tmp_path, "pdb.xml", mk(
+        gkey='<key attr.name="preferdirectpaths" attr.type="boolean" for="graph" id="g"/>',
+        gdata='<data key="g">true</data>')))
+    assert top is None  # the reference requires a STRING (topology.c:601-603)
+
+
+def attach_graph(n=40, seed=3):
+    rng = np.random.default_rng(seed)
+    g = synth.random_sparse(V=n, seed=seed)
+    countries = ["US", "DE", "FR", "BR"]
+    types = ["relay", "client", "server"]
+    cities = ["a", "b", "c", "d", "e", "f"]
+    ips = [f"10.{rng.integers(0, 4)}.{rng.integers(0, 255)}.{rng.integers(1, 255)}" if rng.random() < 0.6
+           else ("0.0.0.0" if rng.random() < 0.5 else None) for _ in range(n)]
+    va = {
+        "ip": ("d1", "string", ips),
+        "countrycode": ("d2", "string", [countries[rng.integers(0, 4)] for _ in range(n)]),
+        "citycode": ("d5", "string", [cities[rng.integers(0, 6)] if rng.random() < 0.5 else None for _ in range(n)]),
+        "type": ("d6", "string", [types[rng.integers(0, 3)] for _ in range(n)]),
+        "geocode": ("d8", "string", [countries[rng.integers(0, 4)] if rng.random() < 0.3 else None for _ in range(n)]),
+    }
+    vattr = {k: [(x or "") for x in v[2]] for k, v in va.items()}
+    return g, synth.to_graphml(g, extra_vattr=va), vattr
+
+
+def test_attach_matches_reference_algorithm(tmp_path):
+    g, text, vattr = attach_graph()
+    top = T.Topology.new(write(tmp_path, "att.xml", text))
+    assert top is not None
+    ref_rng = attach_ref.RandR(12345)
+    rnd = T.Random(12345)
+    rng = np.random.default_rng(0)
+    hints = []
+    for k in range(200):
+        ip = [None, "10.1.2.3", "10.0.0.1", "192.168.1.1", "0.0.0.0", "127.0.0.1", "garbage"][rng.integers(0, 7)]
+        if rng.random() < 0.2:
+            cand = [x for x in vattr["ip"] if x and x != "0.0.0.0"]
+            ip = cand[rng.integers(0, len(cand))]
+        h = dict(ipHint=ip,
+                 citycodeHint=[None, "a", "B", "zz"][rng.integers(0, 4)],
+                 countrycodeHint=[None, "us", "DE", "XX"][rng.integers(0, 4)],
+                 geocodeHint=[None, "FR", "br"][rng.integers(0, 3)],
+                 typeHint=[None, "relay", "CLIENT", "nope"][rng.integers(0, 4)])
+        hints.append(h)
+        addr = T.Address(f"11.0.{k // 250}.{k % 250 + 1}")
+        down, up = top.attach(addr, rnd, **h)
+        want = attach_ref.find_attachment_vertex(vattr, g.n, ref_rng, **h)
+        got = top.vertex_of_ip(addr.ip)
+        assert got == want, (k, h)
+        assert (down, up) == (10240, 10240)
+    att = top.attached()
+    assert len(set(att.tolist())) == len(att)
+    top.free()
+
+
+def test_detach_keeps_attached_vertex(tmp_path):
+    g, text, vattr = attach_graph(n=20, seed=5)
+    top = T.Topology.new(write(tmp_path, "d.xml", text))
+    a = T.Address("11.1.1.1")
+    top.attach(a, T.Random(1))
+    v = top.vertex_of_ip("11.1.1.1")
+    assert v >= 0
+    top.detach(a)
+    assert top.vertex_of_ip("11.1.1.1") == -1
+    assert v in top.attached().tolist()  # verticesWithAttachedHosts never shrinks (topology.c:2432-2439)
+    top.free()
+
+
+@pytest.mark.skipif(E.device_count() > 0, reason="CPU-only behaviour")
+def test_queries_fail_loudly_without_gpu(tmp_path):
+    g, text, _ = attach_graph(n=20, seed=6)
+    top = T.Topology.new(write(tmp_path, "n.xml", text))
+    a, b = T.Address("11.1.1.1"), T.Address("11.1.1.2")
+    r = T.Random(2)
+    top.attach(a, r)
+    top.attach(b, r)
+    assert top.getLatency(a, b) == -1.0
+    assert top.getReliability(a, b) == -1.0
+    assert not top.isRoutable(a, b)
+    top.free()
+
+
+def test_unattached_address_is_unroutable(tmp_path):
+    g, text, _ = attach_graph(n=20, seed=7)
+    top = T.Topology.new(write(tmp_path, "u.xml", text))
+    a, b = T.Address("11.1.1.1"), T.Address("11.1.1.9")
+    top.attach(a, T.Random(3))
+    assert top.getLatency(a, b) == -1.0  # topology.c:1979-1984 -> -1 (topology.c:2073)
+    top.free()
