@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--cpu-sources", type=int, default=12)
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
+    ap.add_argument("--dense-variant", type=int, default=0, help="0 = per-wave row streams (default), 1 = LDS-staged")
     args = ap.parse_args()
 
     import torch
@@ -132,6 +133,7 @@ def main():
         eng.set_option(E.OPT_PROFILE, 1)
     if args.batches:
         eng.set_option(E.OPT_BATCHES_IN_FLIGHT, args.batches)
+    eng.set_option(E.OPT_DENSE_VARIANT, args.dense_variant)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0

@@ -69,6 +69,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_MAX_ROUNDS 3        /* iteration guard (default 4*V+64) */
 #define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
 #define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count (vertex, batch) visits and changes (CSR relax) */
+#define SHADOWTOPO_OPT_DENSE_VARIANT 6     /* dense relax kernel: 0 = per-wave row streams (default), 1 = LDS-staged rows */
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;

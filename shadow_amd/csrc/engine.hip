@@ -312,6 +312,20 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
     if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7))], 1ull);
 }
 
+// Lexicographic (candidate, d(u)) minimum with heap-order tie detection, branch-free so the
+// compiler keeps the per-destination state in scalars (a branchy form made it copy whole
+// <8 x double> vectors around the control flow).
+__device__ __forceinline__ void lex_update(double c, double du, int32_t u, double& bc, double& bdu, int32_t& bu,
+                                           uint32_t& tie, uint32_t bit) {
+    const bool same_c = c == bc;
+    const bool take = (c < bc) | (same_c & (du < bdu));
+    const bool eq = same_c & (du == bdu);
+    bc = take ? c : bc;
+    bdu = take ? du : bdu;
+    bu = take ? u : bu;
+    tie = take ? (tie & ~bit) : (eq ? (tie | bit) : tie);
+}
+
 // Dense form for complete-ish graphs (arcs >= V^2/4): W[u][v] = merged latency of arc
 // u -> v (+inf if none), WI[u][v] = its in-arc index, rows padded to Vp = roundup(V, 8).
 // One wave owns DT = 8 consecutive destinations and streams every u: one 512-byte row
@@ -368,32 +382,29 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
         bu[t] = -1;
     }
     uint32_t tie = 0;
-    for (int32_t u = 0; u < V; u += 2) {
-        const double du[2] = {Dl[(size_t)u * KL], Dl[(size_t)(u + 1) * KL]};  // row V is padding (+inf)
+    // DR rows per iteration: their DR row loads and DR 64-byte weight loads are all in
+    // flight before the first compare (rows V.. are +inf padding; Vp is a multiple of 64)
+    constexpr int DR = 4;
+    for (int32_t u = 0; u < V; u += DR) {
+        double du[DR], w[DR][DT];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const double* w = W + (size_t)(u + k) * Vp + v0;
+        for (int r = 0; r < DR; ++r) {
+            du[r] = Dl[(size_t)(u + r) * KL];
+#pragma unroll
+            for (int t = 0; t < DT; ++t) w[r][t] = W[(size_t)(u + r) * Vp + v0 + t];
+        }
+#pragma unroll
+        for (int r = 0; r < DR; ++r) {
             double c[DT];
             bool hit = false;
 #pragma unroll
             for (int t = 0; t < DT; ++t) {
-                c[t] = du[k] + w[t];
+                c[t] = du[r] + w[r][t];
                 hit |= c[t] <= bc[t];
             }
             if (hit) {  // rare once the running bests sit at the current distances
 #pragma unroll
-                for (int t = 0; t < DT; ++t) {
-                    if (c[t] <= bc[t]) {
-                        if (c[t] < bc[t] || du[k] < bdu[t]) {
-                            bc[t] = c[t];
-                            bdu[t] = du[k];
-                            bu[t] = u + k;
-                            tie &= ~(1u << t);
-                        } else if (du[k] == bdu[t]) {
-                            tie |= 1u << t;
-                        }
-                    }
-                }
+                for (int t = 0; t < DT; ++t) lex_update(c[t], du[r], u + r, bc[t], bdu[t], bu[t], tie, 1u << t);
             }
         }
     }
@@ -410,6 +421,109 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
                                B.R[idx], B.P[idx]);
         }
         any |= ch;
+    }
+    if (__ballot(any) && lane == 0) cnt[b] = 1;
+}
+
+// LDS-staged variant: a 512-thread block owns 64 destinations (8 waves x DT); every
+// 32-row chunk of d(u) (16 KB) is loaded from global memory once per block, double-buffered
+// in LDS, and read by all 8 waves (conflict-free ds_read_b64, lane = source) -- 8x less
+// L2/MALL traffic than one row stream per wave.  Weights stay on the scalar path.
+constexpr int LDS_ROWS = 32;
+
+__global__ __launch_bounds__(512) void k_relax_dense_lds(const double* __restrict__ W, const int32_t* __restrict__ WI,
+                                                         int32_t Vp, const double* __restrict__ in_r, Pools pools,
+                                                         int32_t V, int32_t nb, int32_t ntb64,
+                                                         const int32_t* __restrict__ cnt_prev,
+                                                         int32_t* __restrict__ cnt) {
+    __shared__ __attribute__((aligned(16))) double sD[2][LDS_ROWS * KL];
+    const int32_t L = blockIdx.x;
+    const int32_t xcd = L & 7;
+    const int32_t q = L >> 3;
+    const int32_t b = xcd + 8 * (q / ntb64);
+    if (b >= nb) return;  // block-uniform exits only: the loop below has barriers
+    if (cnt_prev[b] == 0) return;
+    const int32_t vb = (q % ntb64) * 64;
+    if (vb >= V) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int32_t v0 = vb + wave * DT;
+    const BatchDev B = batch_view(pools, b);
+    const int32_t sv = B.srcv[lane];
+    double bc[DT], bdu[DT];
+    int32_t bu[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        // seeded with the current distance (see k_relax_dense); padding rows are +inf
+        const double cd = B.D[(size_t)(v0 + t) * KL + lane];
+        bc[t] = cd < dinf() ? cd : dmax();
+        bdu[t] = dinf();
+        bu[t] = -1;
+    }
+    uint32_t tie = 0;
+    // chunk fill: thread -> (row fr, 4 consecutive lanes fc..fc+3)
+    const int fr = threadIdx.x >> 4;
+    const int fc = (threadIdx.x & 15) * 4;
+    typedef double dbl2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(1))) const dbl2 gd2;
+    const int32_t nchunks = (V + LDS_ROWS - 1) / LDS_ROWS;
+    dbl2 p0, p1;
+    {
+        const gd2* src = (const gd2*)(B.D + (size_t)fr * KL + fc);
+        p0 = src[0];
+        p1 = src[1];
+        dbl2* dst = (dbl2*)&sD[0][fr * KL + fc];
+        dst[0] = p0;
+        dst[1] = p1;
+    }
+    __syncthreads();
+    for (int32_t k = 0; k < nchunks; ++k) {
+        const int cur = k & 1;
+        const bool more = k + 1 < nchunks;
+        if (more) {  // prefetch the next chunk into registers (rows past V are +inf padding)
+            const gd2* src = (const gd2*)(B.D + (size_t)((k + 1) * LDS_ROWS + fr) * KL + fc);
+            p0 = src[0];
+            p1 = src[1];
+        }
+        const double* rows = sD[cur];
+#pragma unroll 2
+        for (int r = 0; r < LDS_ROWS; ++r) {
+            const int32_t u = k * LDS_ROWS + r;
+            const double du = rows[r * KL + lane];
+            const double* w = W + (size_t)u * Vp + v0;
+            double c[DT];
+            bool hit = false;
+#pragma unroll
+            for (int t = 0; t < DT; ++t) {
+                c[t] = du + w[t];
+                hit |= c[t] <= bc[t];
+            }
+            if (hit) {
+#pragma unroll
+                for (int t = 0; t < DT; ++t) lex_update(c[t], du, u, bc[t], bdu[t], bu[t], tie, 1u << t);
+            }
+        }
+        if (more) {
+            dbl2* dst = (dbl2*)&sD[cur ^ 1][fr * KL + fc];
+            dst[0] = p0;
+            dst[1] = p1;
+        }
+        __syncthreads();
+    }
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        const int32_t v = v0 + t;
+        if (v >= V) break;
+        bool ch = false;
+        if (bu[t] >= 0 && sv >= 0 && sv != v) {
+            const size_t idx = (size_t)v * KL + lane;
+            const int32_t arc = WI[(size_t)bu[t] * Vp + v];
+            ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx], B.H[idx],
+                               B.R[idx], B.P[idx]);
+        }
+        any |= ch;
+        __builtin_amdgcn_sched_barrier(0);  // keep the 8 epilogues from being hoisted together (VGPRs)
     }
     if (__ballot(any) && lane == 0) cnt[b] = 1;
 }
@@ -893,6 +1007,7 @@ struct shadowtopo_engine {
     int64_t opt_max_rounds = 0;
     int32_t opt_force_replay = 0;
     int32_t opt_profile = 0;
+    int32_t opt_dense_variant = 0;  // 0 = one row stream per wave (default), 1 = LDS-staged rows
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1017,6 +1132,8 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int64_t nblocks = (int64_t)8 * nvb * ((nbg + 7) / 8);
     const int32_t ntb = (V + 4 * DT - 1) / (4 * DT);
     const int64_t nblocks_dense = (int64_t)8 * ntb * ((nbg + 7) / 8);
+    const int32_t ntb64 = (V + 63) / 64;
+    const int64_t nblocks_lds = (int64_t)8 * ntb64 * ((nbg + 7) / 8);
     if (nblocks > 0x7fffffff) return fail(SHADOWTOPO_EINVAL, "grid too large");
     const int64_t max_rounds = eng->opt_max_rounds > 0 ? eng->opt_max_rounds : 4LL * V + 64;
     eng->d_prof = eng->opt_profile ? eng->prof_buf : nullptr;
@@ -1036,8 +1153,12 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
         if (eng->dense) {
-            hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W, eng->d_WI,
-                               eng->Vp, g.in_r, eng->pools, V, nbg, ntb, cnt_prev, cnt_cur);
+            if (eng->opt_dense_variant == 0)
+                hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W,
+                                   eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb, cnt_prev, cnt_cur);
+            else
+                hipLaunchKernelGGL(k_relax_dense_lds, dim3((uint32_t)nblocks_lds), dim3(512), 0, s, eng->d_W,
+                                   eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb64, cnt_prev, cnt_cur);
         } else {
             hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
                                g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
@@ -1370,7 +1491,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->flags = flags;
     eng->multigraph = multigraph;
     eng->n_arcs = (int64_t)in_src.size() - CSR_PAD;
-    eng->Vp = (V + 7) / 8 * 8;
+    eng->Vp = (V + 63) / 64 * 64;  // dense tiles of 64 destinations, 32-row LDS chunks
     {
         const double VV = (double)V * (double)V;
         const bool fits = (double)eng->Vp * eng->Vp * 12.0 <= 24.0e9;
@@ -1505,6 +1626,9 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_PROFILE:
             eng->opt_profile = value ? 1 : 0;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DENSE_VARIANT:
+            eng->opt_dense_variant = (int32_t)value;
             return SHADOWTOPO_OK;
         default:
             return fail(SHADOWTOPO_EINVAL, "unknown option %d", key);

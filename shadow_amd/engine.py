@@ -32,6 +32,7 @@ OPT_TIMING = 2
 OPT_MAX_ROUNDS = 3
 OPT_FORCE_REPLAY = 4
 OPT_PROFILE = 5
+OPT_DENSE_VARIANT = 6
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (

@@ -167,3 +167,9 @@ def test_csr_forced_on_dense_graph():
     g = synth.geometric_complete_ish(V=300, A=70)
     st = compare(g, layout="csr")
     assert st["dense"] == 0
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_dense_variants_agree(variant):
+    g = synth.random_sparse(V=333, avg_deg=6, seed=23)
+    assert compare(g, layout="dense", dense_variant=variant)["dense"] == 1
