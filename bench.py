@@ -84,8 +84,8 @@ def load_traffic(workload_key):
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p))
-        return d.get(workload_key)
+        d = json.load(open(p)).get(workload_key)
+        return d["bytes_per_launch"] if d else None
     except Exception:
         return None
 
@@ -120,11 +120,12 @@ def main():
     dev = torch.device(f"cuda:{local}")
 
     from shadow_amd import engine as E
+    from shadow_amd import shard
     t = time.perf_counter()
-    g, per, desc = build_workload(args.config, world, args.scale)
+    g, _per, desc = build_workload(args.config, world, args.scale)
     A = len(g.attached)
-    r0, r1 = rank * per, min(A, (rank + 1) * per)
-    log(f"[rank {rank}] workload {desc}: E={g.m} built in {time.perf_counter() - t:.1f}s")
+    r0, r1, per = shard.shard_rows(A, world, rank)
+    log(f"[rank {rank}] workload {desc}: E={g.m} built in {time.perf_counter() - t:.1f}s; rows [{r0},{r1})")
     t = time.perf_counter()
     eng = E.Engine.from_synth(g, device=local)
     eng.set_attached(g.attached)
@@ -137,9 +138,10 @@ def main():
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0
-    lat = torch.empty((rows, A), dtype=torch.float64, device=dev)
-    rel = torch.empty((rows, A), dtype=torch.float64, device=dev)
-    hops = torch.empty((rows, A), dtype=torch.int32, device=dev)
+    # every rank contributes `per` rows to the all-gather (last rank's tail is padding)
+    lat = torch.zeros((per, A), dtype=torch.float64, device=dev)
+    rel = torch.zeros((per, A), dtype=torch.float64, device=dev)
+    hops = torch.zeros((per, A), dtype=torch.int32, device=dev)
     if world > 1:
         full_lat = torch.empty((per * world, A), dtype=torch.float64, device=dev)
         full_rel = torch.empty((per * world, A), dtype=torch.float64, device=dev)
@@ -147,8 +149,9 @@ def main():
 
     def step():
         stream = torch.cuda.current_stream(dev).cuda_stream
-        eng.compute_rows_device(r0, r1, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
-        if world > 1:
+        if rows > 0:
+            eng.compute_rows_device(r0, r1, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
+        if world > 1:  # RCCL all-gather over xGMI: every rank ends with the full matrix
             dist.all_gather_into_tensor(full_lat, lat)
             dist.all_gather_into_tensor(full_rel, rel)
             dist.all_gather_into_tensor(full_hops, hops)
@@ -176,18 +179,29 @@ def main():
     value = total_sources * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel (k_relax), from live HIP events on its stream
+    # roofline of the dominant kernel, from live HIP events on its stream: the dense full
+    # sweep (k_relax_dense) on complete-ish graphs, the CSR relax (k_relax) otherwise.  One
+    # launch relaxes every source of the batch group in flight, so its algorithmic bytes are
+    # SURVEY.md 8d's B_src times the sources it covers.
     B_src = algorithmic_bytes_per_source(g.n, st["n_arcs"], A)
-    relax_launches = max(1, st["relax_launches"])
-    bytes_per_launch = rows * args.steps * B_src / relax_launches
-    avg_launch_s = st["relax_ms"] / relax_launches / 1e3
+    if st["dense"]:
+        kname, launches, kms = "k_relax_dense", max(1, st["full_sweeps"]), st["full_ms"]
+    else:
+        kname, launches, kms = "k_relax", max(1, st["relax_launches"]), st["relax_ms"]
+    bytes_per_launch = rows * args.steps * B_src / launches
+    avg_launch_s = kms / launches / 1e3
     achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
-    traffic = load_traffic(f"{args.config}@{args.scale}")
+    traffic = load_traffic(f"{args.config}@{args.scale}@{world}")
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "kernel": "k_relax", "avg_launch_ms": avg_launch_s * 1e3,
-                "launches_per_step": relax_launches / args.steps,
-                "algorithmic_bytes_per_source": B_src}
+                "kernel": kname, "avg_launch_ms": avg_launch_s * 1e3,
+                "launches_per_step": launches / args.steps,
+                "algorithmic_bytes_per_source": B_src, "algorithmic_bytes_per_launch": bytes_per_launch,
+                "measured_hbm_gbs": (traffic / avg_launch_s / 1e9) if (traffic and avg_launch_s > 0) else None}
+    if st["dense"] and st["delta_sweeps"]:
+        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta",
+                                    "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
+                                    "launches_per_step": st["delta_sweeps"] / args.steps}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -218,7 +232,9 @@ def main():
             "engine": {"rounds_per_step": st["rounds"] / args.steps, "replayed_sources": st["replayed_sources"],
                        "relax_ms_per_step": st["relax_ms"] / args.steps,
                        "compose_ms_per_step": st["compose_ms"] / args.steps, "dense": st["dense"],
-                       "visits_per_step": st["visits"] / args.steps, "changes_per_step": st["changes"] / args.steps},
+                       "visits_per_step": st["visits"] / args.steps, "changes_per_step": st["changes"] / args.steps,
+                       "full_sweeps_per_step": st["full_sweeps"] / args.steps,
+                       "delta_sweeps_per_step": st["delta_sweeps"] / args.steps},
         }
         print(json.dumps(out), flush=True)
     eng.close()

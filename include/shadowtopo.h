@@ -70,6 +70,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
 #define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count (vertex, batch) visits and changes (CSR relax) */
 #define SHADOWTOPO_OPT_DENSE_VARIANT 6     /* dense relax kernel: 0 = per-wave row streams (default), 1 = LDS-staged rows */
+#define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
+                                              (vertex, source) pairs gets a change-mask delta round instead of a full
+                                              sweep (default 125; 0 = always full sweeps) */
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;
@@ -92,6 +95,10 @@ typedef struct shadowtopo_stats {
     int32_t reserved;
     int64_t visits;          /* OPT_PROFILE: active (vertex, batch) waves processed */
     int64_t changes;         /* OPT_PROFILE: (vertex, batch) waves that changed */
+    int64_t full_sweeps;     /* dense: full-sweep relax launches */
+    int64_t delta_sweeps;    /* dense: change-mask (delta) relax launches */
+    double full_ms;          /* OPT_TIMING: HIP-event time of the dense full sweeps (k_relax_dense) */
+    double delta_ms;         /* OPT_TIMING: HIP-event time of the delta rounds (k_relax_dense_delta) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -43,7 +43,8 @@ namespace {
 
 constexpr int KL = 64;                    // sources per batch = wave width
 constexpr uint32_t TAINT = 0x80000000u;   // H bit: tree path crosses a heap-order tie
-constexpr uint32_t HMASK = 0x7fffffffu;
+constexpr uint32_t LTIE = 0x40000000u;    // H bit: the tie is at this vertex (its own predecessor choice)
+constexpr uint32_t HMASK = 0x3fffffffu;
 constexpr int REPLAY_SLOTS = 64;
 
 thread_local std::string g_err;
@@ -104,6 +105,8 @@ struct Pools {
     int32_t* srcv;      // [slot][64] source vertex per lane (-1 = unused lane)
     int32_t* row;       // [slot][64] attached row per lane (-1 = none)
     unsigned long long* mask;  // [slot] lanes whose rows need the heap-exact replay
+    double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
+    unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -119,7 +122,11 @@ struct BatchDev {
     const int32_t* srcv;
     const int32_t* row;
     unsigned long long* mask;
+    gdouble* BDU;
+    unsigned long long* chm0;
+    unsigned long long* chm1;
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
+    __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
 
 __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
@@ -134,6 +141,9 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.srcv = p.srcv + (size_t)b * KL;
     B.row = p.row + (size_t)b * KL;
     B.mask = p.mask + b;
+    B.BDU = p.BDU ? (gdouble*)(p.BDU + o) : nullptr;
+    B.chm0 = p.chm ? p.chm + (size_t)b * 2 * p.Vp : nullptr;
+    B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
     return B;
 }
 
@@ -187,6 +197,14 @@ __global__ void k_init(Pools pools, int32_t V) {
         B.act0[i] = 0;
         B.act1[i] = 0;
     }
+    if (B.chm0) {
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+            B.BDU[i] = inf;
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
+            B.chm0[i] = 0;
+            B.chm1[i] = 0;
+        }
+    }
 }
 
 // sources: d(s) = 0, R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445); activate out-neighbours
@@ -215,7 +233,8 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
     const size_t uidx = (size_t)u * KL + lane;
     const uint32_t hu = B.H[uidx];
     const double ru = B.R[uidx];
-    const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? TAINT : 0u);
+    // local tie: two candidates share (fl(d(u)+w), d(u)), or the degenerate d(u) == d(v)
+    const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? (TAINT | LTIE) : 0u);
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
     const double r = ru * in_r[arc];
     if (bc != curD || h != curH || r != curR || arc != curP) {
@@ -350,17 +369,49 @@ __device__ __forceinline__ void relax_u(double du, double w, int32_t u, double& 
     }
 }
 
+// Dense-tile epilogue shared by the full sweeps: record each destination's new best,
+// its lex key d(pred) (BDU, read by the delta rounds), and the per-vertex change mask of
+// the round (lane = source) that the next delta round walks; the batch counter gets the
+// number of changed (vertex, source) pairs.
+__device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int32_t sv, int32_t v0, int32_t V,
+                                               const double* bc, const double* bdu, const int32_t* bu, uint32_t tie,
+                                               const int32_t* __restrict__ WI, int32_t Vp,
+                                               const double* __restrict__ in_r, int32_t parity,
+                                               int32_t* __restrict__ cnt, int32_t b) {
+    unsigned long long* chn = B.chm(parity);
+    int32_t nch = 0;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        const int32_t v = v0 + t;
+        if (v >= V) break;
+        bool ch = false;
+        if (bu[t] >= 0 && sv >= 0 && sv != v) {
+            const size_t idx = (size_t)v * KL + lane;
+            const int32_t arc = WI[(size_t)bu[t] * Vp + v];
+            ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx], B.H[idx],
+                               B.R[idx], B.P[idx]);
+            B.BDU[idx] = bdu[t];
+        }
+        const unsigned long long m = __ballot(ch);
+        if (lane == 0) chn[v] = m;
+        nch += __popcll(m);
+        __builtin_amdgcn_sched_barrier(0);  // keep the epilogues from being hoisted together (VGPRs)
+    }
+    if (nch && lane == 0) atomicAdd(&cnt[b], nch);
+}
+
 __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ W, const int32_t* __restrict__ WI,
                                                      int32_t Vp, const double* __restrict__ in_r,
                                                      Pools pools, int32_t V, int32_t nb,
-                                                     int32_t ntb, const int32_t* __restrict__ cnt_prev,
+                                                     int32_t ntb, int32_t parity, int32_t thresh,
+                                                     const int32_t* __restrict__ cnt_prev,
                                                      int32_t* __restrict__ cnt) {
     const int32_t L = blockIdx.x;
     const int32_t xcd = L & 7;
     const int32_t q = L >> 3;
     const int32_t b = xcd + 8 * (q / ntb);
     if (b >= nb) return;
-    if (cnt_prev[b] == 0) return;
+    if (cnt_prev[b] <= thresh) return;  // converged (0) or left to the delta round
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int32_t v0 = ((q % ntb) * 4 + wave) * DT;
     if (v0 >= V) return;
@@ -396,11 +447,11 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 #pragma unroll
         for (int r = 0; r < DR; ++r) {
             double c[DT];
-            bool hit = false;
+            unsigned long long hit = 0;  // wave-wide: the compares go straight to SGPR masks
 #pragma unroll
             for (int t = 0; t < DT; ++t) {
                 c[t] = du[r] + w[r][t];
-                hit |= c[t] <= bc[t];
+                hit |= __ballot(c[t] <= bc[t]);
             }
             if (hit) {  // rare once the running bests sit at the current distances
 #pragma unroll
@@ -408,21 +459,7 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
             }
         }
     }
-    bool any = false;
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-        const int32_t v = v0 + t;
-        if (v >= V) break;
-        bool ch = false;
-        if (bu[t] >= 0 && sv >= 0 && sv != v) {
-            const size_t idx = (size_t)v * KL + lane;
-            const int32_t arc = WI[(size_t)bu[t] * Vp + v];
-            ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx], B.H[idx],
-                               B.R[idx], B.P[idx]);
-        }
-        any |= ch;
-    }
-    if (__ballot(any) && lane == 0) cnt[b] = 1;
+    dense_epilogue(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b);
 }
 
 // LDS-staged variant: a 512-thread block owns 64 destinations (8 waves x DT); every
@@ -433,8 +470,8 @@ constexpr int LDS_ROWS = 32;
 
 __global__ __launch_bounds__(512) void k_relax_dense_lds(const double* __restrict__ W, const int32_t* __restrict__ WI,
                                                          int32_t Vp, const double* __restrict__ in_r, Pools pools,
-                                                         int32_t V, int32_t nb, int32_t ntb64,
-                                                         const int32_t* __restrict__ cnt_prev,
+                                                         int32_t V, int32_t nb, int32_t ntb64, int32_t parity,
+                                                         int32_t thresh, const int32_t* __restrict__ cnt_prev,
                                                          int32_t* __restrict__ cnt) {
     __shared__ __attribute__((aligned(16))) double sD[2][LDS_ROWS * KL];
     const int32_t L = blockIdx.x;
@@ -442,7 +479,7 @@ __global__ __launch_bounds__(512) void k_relax_dense_lds(const double* __restric
     const int32_t q = L >> 3;
     const int32_t b = xcd + 8 * (q / ntb64);
     if (b >= nb) return;  // block-uniform exits only: the loop below has barriers
-    if (cnt_prev[b] == 0) return;
+    if (cnt_prev[b] <= thresh) return;
     const int32_t vb = (q % ntb64) * 64;
     if (vb >= V) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -492,11 +529,11 @@ __global__ __launch_bounds__(512) void k_relax_dense_lds(const double* __restric
             const double du = rows[r * KL + lane];
             const double* w = W + (size_t)u * Vp + v0;
             double c[DT];
-            bool hit = false;
+            unsigned long long hit = 0;
 #pragma unroll
             for (int t = 0; t < DT; ++t) {
                 c[t] = du + w[t];
-                hit |= c[t] <= bc[t];
+                hit |= __ballot(c[t] <= bc[t]);
             }
             if (hit) {
 #pragma unroll
@@ -510,22 +547,7 @@ __global__ __launch_bounds__(512) void k_relax_dense_lds(const double* __restric
         }
         __syncthreads();
     }
-    bool any = false;
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-        const int32_t v = v0 + t;
-        if (v >= V) break;
-        bool ch = false;
-        if (bu[t] >= 0 && sv >= 0 && sv != v) {
-            const size_t idx = (size_t)v * KL + lane;
-            const int32_t arc = WI[(size_t)bu[t] * Vp + v];
-            ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx], B.H[idx],
-                               B.R[idx], B.P[idx]);
-        }
-        any |= ch;
-        __builtin_amdgcn_sched_barrier(0);  // keep the 8 epilogues from being hoisted together (VGPRs)
-    }
-    if (__ballot(any) && lane == 0) cnt[b] = 1;
+    dense_epilogue(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b);
 }
 
 // Dense round 0: every destination's only finite candidate is its source's direct arc
@@ -553,6 +575,167 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
         B.H[idx] = ((hs & HMASK) + 1u) | (hs & TAINT);
         B.R[idx] = rs * in_r[arc];
         B.P[idx] = arc;
+        B.BDU[idx] = 0.0;
+    }
+}
+
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long x, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// One candidate (u -> v for source lane s) with c <= d(v): the lexicographic update of
+// k_relax_dense applied incrementally against the recorded state.  The recorded lex key is
+// (D, BDU); the local-tie bit LTIE stays valid while the predecessor's key is unchanged.
+// Returns whether (v, s)'s D/H/R/P changed (its children must look again next round).
+__device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, int32_t s, int32_t u, double du,
+                                                double c, double cur, const int32_t* __restrict__ WI, int32_t Vp,
+                                                const int32_t* __restrict__ in_src, const double* __restrict__ in_r,
+                                                double* sdcell) {
+    const size_t idx = (size_t)v * KL + s;
+    const uint32_t hv = B.H[idx];
+    uint32_t lt = 0;
+    if (!(c < cur)) {  // c == d(v): the recorded predecessor refreshed, or a same-distance rival
+        const int32_t pa = B.P[idx];
+        const int32_t pu = pa >= 0 ? in_src[pa] : -1;
+        const double bdu = B.BDU[idx];
+        if (pu == u) {
+            // same predecessor: its key only moves down; with an unchanged key the recorded
+            // tie stands, a smaller key beats every unchanged rival (a changed rival with the
+            // new key is a candidate of this same round and re-marks the tie)
+            lt = (du == bdu) ? (hv & LTIE) : 0u;
+        } else if (du == bdu) {
+            const uint32_t nh = hv | LTIE | TAINT;
+            if (nh == hv) return false;
+            B.H[idx] = nh;
+            return (hv & TAINT) == 0;
+        } else if (du > bdu) {
+            return false;
+        }
+    }
+    if (du == c) lt = LTIE;  // degenerate d(u) == d(v): the reference order is heap-dependent
+    const int32_t arc = WI[(size_t)u * Vp + v];
+    const size_t uidx = (size_t)u * KL + s;
+    const uint32_t hu = B.H[uidx];
+    const double ru = B.R[uidx];
+    const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
+    const double r = ru * in_r[arc];
+    B.BDU[idx] = du;
+    *sdcell = c;
+    if (c != cur || h != hv || r != B.R[idx] || arc != B.P[idx]) {
+        B.D[idx] = c;
+        B.H[idx] = h;
+        B.R[idx] = r;
+        B.P[idx] = arc;
+        return true;
+    }
+    return false;
+}
+
+// Dense delta round.  A (u, source) pair whose state did not change in the previous round
+// was already evaluated by every destination against its final value, so only the pairs of
+// the previous round's change masks can improve anything.  One wave owns 64 destinations
+// (lane = v) of one batch and keeps their 64x64 current distances in LDS; it walks the
+// changed rows u in groups of DG (weights W[u][v0..v0+63] and the row d(u) for all 64
+// sources: 2 coalesced 512-B loads per row, all in flight together) and, per changed
+// source s of row u, compares fl(d_s(u) + w(u, v)) against d_s(v) -- one f64 add, one LDS
+// read and one compare for 64 destinations.  Candidates c <= d_s(v) (rare) take the exact
+// lexicographic path in delta_candidate.  The host picks this kernel for a batch when the
+// previous round changed at most `thresh` pairs, k_relax_dense otherwise.
+// Grid: the batches of one destination chunk sit on the same XCD (shared W rows in L2).
+constexpr int DG = 8;
+constexpr int DW = 4;        // waves per block: wave w takes the sources [16w, 16w+16) of the tile
+constexpr int SDS = KL + 1;  // LDS row stride (doubles): conflict-free transposed staging
+
+__global__ __launch_bounds__(64 * DW) void k_relax_dense_delta(const double* __restrict__ W,
+                                                               const int32_t* __restrict__ WI, int32_t Vp,
+                                                               const int32_t* __restrict__ in_src,
+                                                               const double* __restrict__ in_r, Pools pools,
+                                                               int32_t V, int32_t nb, int32_t nvc, int32_t parity,
+                                                               int32_t thresh, const int32_t* __restrict__ cnt_prev,
+                                                               int32_t* __restrict__ cnt) {
+    __shared__ double sD[KL * SDS];  // [s][v - v0]
+    __shared__ unsigned long long sM[DW][KL];
+    const int32_t L = blockIdx.x;
+    const int32_t q = L >> 3;
+    const int32_t b = q % nb;
+    const int32_t vc = (L & 7) + 8 * (q / nb);
+    if (vc >= nvc) return;  // block-uniform exits only (barriers below)
+    const int32_t cp = cnt_prev[b];
+    if (cp == 0 || cp > thresh) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int32_t v0 = vc * KL;
+    const int32_t v = v0 + lane;
+    const BatchDev B = batch_view(pools, b);
+    const gdouble* D = B.D;
+    for (int i = wave; i < KL; i += DW) sD[lane * SDS + i] = D[(size_t)(v0 + i) * KL + lane];
+    __syncthreads();
+    const int32_t s0 = wave * (KL / DW);
+    const unsigned long long srange = (DW == 1) ? ~0ull : (((1ull << (KL / DW)) - 1ull) << s0);
+    const unsigned long long* chp = B.chm(parity ^ 1);
+    const bool vok = v < V;
+    const double inf = dinf();
+    unsigned long long mine = 0;
+    for (int32_t u0 = 0; u0 < V; u0 += KL) {
+        const unsigned long long mk = ((u0 + lane < V) ? chp[u0 + lane] : 0ull) & srange;
+        unsigned long long nz = __ballot(mk != 0ull);
+        while (nz) {
+            int32_t us[DG];
+            int n = 0;
+#pragma unroll
+            for (int i = 0; i < DG; ++i) {
+                us[i] = 0;
+                if (nz) {
+                    us[i] = __builtin_ctzll(nz);
+                    nz &= nz - 1;
+                    n = i + 1;
+                }
+            }
+            double w[DG], dr[DG];
+#pragma unroll
+            for (int i = 0; i < DG; ++i) {
+                if (i < n) {
+                    const int32_t u = u0 + us[i];
+                    w[i] = W[(size_t)u * Vp + v];
+                    dr[i] = D[(size_t)u * KL + s0 + (lane & (KL / DW - 1))];  // this wave's sources only
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < DG; ++i) {
+                if (i >= n) break;
+                const int32_t u = u0 + us[i];
+                unsigned long long m = readlane_u64(mk, us[i]);
+                while (m) {
+                    const int32_t s = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const double du = readlane_d(dr[i], s - s0);
+                    const double c = du + w[i];
+                    double* cell = &sD[s * SDS + lane];
+                    const double cur = *cell;
+                    if (c <= cur && c < inf && vok) {
+                        if (delta_candidate(B, v, s, u, du, c, cur, WI, Vp, in_src, in_r, cell)) mine |= 1ull << s;
+                    }
+                }
+            }
+        }
+    }
+    sM[wave][lane] = mine;
+    __syncthreads();
+    if (wave == 0) {
+        unsigned long long all = 0;
+#pragma unroll
+        for (int k = 0; k < DW; ++k) all |= sM[k][lane];
+        B.chm(parity)[v] = all;
+        if (all) atomicAdd(&cnt[b], (int32_t)__popcll(all));
     }
 }
 
@@ -1008,9 +1191,10 @@ struct shadowtopo_engine {
     int32_t opt_force_replay = 0;
     int32_t opt_profile = 0;
     int32_t opt_dense_variant = 0;  // 0 = one row stream per wave (default), 1 = LDS-staged rows
+    int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
     shadowtopo_stats st{};
 };
 
@@ -1074,6 +1258,10 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.mask, sizeof(unsigned long long) * nb)))
         return rc;
+    if (eng->dense &&
+        ((rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double))) ||
+         (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb))))
+        return rc;
     eng->h_srcv.assign((size_t)KL * nb, -1);
     eng->h_row.assign((size_t)KL * nb, -1);
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
@@ -1100,7 +1288,7 @@ int ensure_replay(shadowtopo_engine* eng) {
 
 int32_t default_nb(const shadowtopo_engine* eng) {
     if (eng->opt_nb > 0) return eng->opt_nb;
-    const double per_batch = (double)eng->Vp * KL * 24.0 + 2.0 * eng->Vp;
+    const double per_batch = (double)eng->Vp * KL * (eng->dense ? 32.0 : 24.0) + 18.0 * eng->Vp;
     const double budget = 24.0e9;
     int32_t nb = (int32_t)std::max(1.0, std::min(16.0, std::floor(budget / per_batch)));
     return nb;
@@ -1142,9 +1330,15 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         hipLaunchKernelGGL(k_seed_dense, dim3(ntb, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp, g.in_r,
                            eng->pools, V);
         HIP_TRY(hipGetLastError());
-        // round 0 consumes "changed" flags of a virtual round -1: every batch changed
-        HIP_TRY(hipMemsetAsync(eng->d_cnt + eng->nb_cap, 0x01, sizeof(int32_t) * nbg, s));
+        // round 0 consumes the change counts of a virtual round -1: every batch changed
+        // everything (full sweep)
+        HIP_TRY(hipMemsetAsync(eng->d_cnt + eng->nb_cap, 0x7f, sizeof(int32_t) * nbg, s));
+        for (int32_t b = 0; b < nbg; ++b) eng->h_cnt[b] = 0x7f7f7f7f;
     }
+    const int32_t nvc = eng->Vp / KL;
+    const int64_t nblocks_delta = (int64_t)8 * nbg * ((nvc + 7) / 8);
+    const int32_t thresh = (int32_t)std::min<int64_t>(
+        0x7f7f7f7e, (int64_t)V * KL * eng->opt_delta_permille / 1000);
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
@@ -1152,13 +1346,37 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         int32_t* cnt_prev = eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
         HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
+        bool round_full = false, round_delta = false;
         if (eng->dense) {
-            if (eng->opt_dense_variant == 0)
-                hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W,
-                                   eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb, cnt_prev, cnt_cur);
-            else
-                hipLaunchKernelGGL(k_relax_dense_lds, dim3((uint32_t)nblocks_lds), dim3(512), 0, s, eng->d_W,
-                                   eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb64, cnt_prev, cnt_cur);
+            // per batch: full sweep when its previous round changed more than `thresh` pairs,
+            // delta round otherwise (each kernel skips the other's batches)
+            bool& any_full = round_full;
+            bool& any_delta = round_delta;
+            any_full = any_delta = false;
+            for (int32_t b = 0; b < nbg; ++b) {
+                any_full |= eng->h_cnt[b] > thresh;
+                any_delta |= eng->h_cnt[b] > 0 && eng->h_cnt[b] <= thresh;
+            }
+            const int32_t par = (int32_t)(round & 1);
+            if (any_full && any_delta && eng->opt_timing) HIP_TRY(hipEventRecord(eng->evm, s));
+            if (any_full) {
+                if (eng->opt_dense_variant == 0)
+                    hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W,
+                                       eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb, par, thresh, cnt_prev,
+                                       cnt_cur);
+                else
+                    hipLaunchKernelGGL(k_relax_dense_lds, dim3((uint32_t)nblocks_lds), dim3(512), 0, s, eng->d_W,
+                                       eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb64, par, thresh,
+                                       cnt_prev, cnt_cur);
+                eng->st.full_sweeps++;
+            }
+            if (any_full && any_delta && eng->opt_timing) HIP_TRY(hipEventRecord(eng->evm2, s));
+            if (any_delta) {
+                hipLaunchKernelGGL(k_relax_dense_delta, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s, eng->d_W,
+                                   eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par, thresh,
+                                   cnt_prev, cnt_cur);
+                eng->st.delta_sweeps++;
+            }
         } else {
             hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
                                g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
@@ -1174,6 +1392,19 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
             eng->st.relax_ms += ms;
+            if (eng->dense) {
+                if (round_full && round_delta) {
+                    float a = 0, b = 0;
+                    HIP_TRY(hipEventElapsedTime(&a, eng->evm, eng->evm2));
+                    HIP_TRY(hipEventElapsedTime(&b, eng->evm2, eng->ev1));
+                    eng->st.full_ms += a;
+                    eng->st.delta_ms += b;
+                } else if (round_full) {
+                    eng->st.full_ms += ms;
+                } else if (round_delta) {
+                    eng->st.delta_ms += ms;
+                }
+            }
         }
         int64_t changed = 0;
         for (int32_t b = 0; b < nbg; ++b) changed += eng->h_cnt[b];
@@ -1545,7 +1776,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->h_in_eid.swap(in_eid);
     eng->h_loop_eid.swap(loop_eid);
     if (hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess) {
+        hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess ||
+        hipEventCreate(&eng->evm) != hipSuccess || hipEventCreate(&eng->evm2) != hipSuccess) {
         shadowtopo_destroy(eng);
         return fail(SHADOWTOPO_EDEVICE, "stream/event create failed");
     }
@@ -1574,6 +1806,8 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->stage) (void)hipFree(eng->stage);
     if (eng->ev0) (void)hipEventDestroy(eng->ev0);
     if (eng->ev1) (void)hipEventDestroy(eng->ev1);
+    if (eng->evm) (void)hipEventDestroy(eng->evm);
+    if (eng->evm2) (void)hipEventDestroy(eng->evm2);
     if (eng->own_stream) (void)hipStreamDestroy(eng->own_stream);
     delete eng;
 }
@@ -1629,6 +1863,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DENSE_VARIANT:
             eng->opt_dense_variant = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DELTA_PERMILLE:
+            if (value < 0 || value > 1000) return fail(SHADOWTOPO_EINVAL, "delta per mille must be in [0, 1000]");
+            eng->opt_delta_permille = (int32_t)value;
             return SHADOWTOPO_OK;
         default:
             return fail(SHADOWTOPO_EINVAL, "unknown option %d", key);

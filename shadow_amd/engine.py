@@ -33,6 +33,7 @@ OPT_MAX_ROUNDS = 3
 OPT_FORCE_REPLAY = 4
 OPT_PROFILE = 5
 OPT_DENSE_VARIANT = 6
+OPT_DELTA_PERMILLE = 7
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (
@@ -55,6 +56,8 @@ class Stats(ctypes.Structure):
         ("replay_ms", ctypes.c_double), ("wall_ms", ctypes.c_double), ("device", ctypes.c_int32),
         ("multigraph", ctypes.c_int32), ("dense", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("visits", ctypes.c_int64), ("changes", ctypes.c_int64),
+        ("full_sweeps", ctypes.c_int64), ("delta_sweeps", ctypes.c_int64),
+        ("full_ms", ctypes.c_double), ("delta_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -173,3 +173,56 @@ def test_csr_forced_on_dense_graph():
 def test_dense_variants_agree(variant):
     g = synth.random_sparse(V=333, avg_deg=6, seed=23)
     assert compare(g, layout="dense", dense_variant=variant)["dense"] == 1
+
+
+# ---- dense delta rounds (k_relax_dense_delta): change-mask rounds after the first sweep
+@pytest.mark.parametrize("permille", [0, 1000])
+@pytest.mark.parametrize("case", ["sparse", "directed", "ties", "vloss_prefer", "multigraph", "geometric"])
+def test_dense_delta_rounds(case, permille):
+    if case == "sparse":
+        g = synth.random_sparse(V=301, avg_deg=5, seed=2)
+    elif case == "directed":
+        g = synth.random_sparse(V=203, avg_deg=4, seed=5, directed=True)
+    elif case == "ties":
+        g = synth.integer_grid(rows=9, cols=11, seed=2)
+    elif case == "vloss_prefer":
+        rng = np.random.default_rng(4)
+        g = synth.random_sparse(V=150, avg_deg=8, seed=6, vloss=rng.uniform(0, 0.1, 150))
+        g.prefer_direct = True
+    elif case == "multigraph":
+        g = synth.random_sparse(V=100, avg_deg=4, seed=17)
+        rng = np.random.default_rng(1)
+        pick = rng.choice(np.nonzero(g.src != g.dst)[0], 30, replace=False)
+        g.src = np.concatenate([g.src, g.dst[pick]])
+        g.dst = np.concatenate([g.dst, g.src[pick]])
+        g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.3, 1.7, 30)])
+        g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 30)])
+    else:
+        g = synth.geometric_complete_ish(V=700, A=130)
+    st = compare(g, layout="dense", delta_permille=permille)
+    assert st["dense"] == 1
+    if permille == 0:
+        assert st["delta_sweeps"] == 0
+    else:
+        assert st["delta_sweeps"] > 0 and st["full_sweeps"] == 1  # only the first sweep is full
+
+
+@pytest.mark.parametrize("case", ["ties", "sparse"])
+def test_dense_delta_same_fixed_point(case):
+    """Full sweeps and delta rounds must reach the same state: distances bit-exact, tie flags
+    identical, predecessor and hops identical wherever no heap-order tie is involved."""
+    g = synth.integer_grid(rows=12, cols=13, seed=4) if case == "ties" else synth.random_sparse(V=400, avg_deg=6, seed=8)
+    srcs = np.arange(0, g.n, 3, dtype=np.int32)
+    outs = []
+    for permille in (0, 1000):
+        eng = E.Engine.from_synth(g, layout="dense")
+        eng.set_option(E.OPT_DELTA_PERMILLE, permille)
+        outs.append(eng.sssp(srcs))
+        eng.close()
+    (d0, p0, h0, t0), (d1, p1, h1, t1) = outs
+    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+    assert np.array_equal(t0, t1)
+    ok = t0 == 0
+    assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
+    if case == "ties":
+        assert (t0 != 0).any()
