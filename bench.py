@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+F64_VALU_OPS = 78.6e12 / 2  # f64 vector FMA/s (78.6 TFLOP/s counts an FMA as 2)
 METRIC = "SSSP source-paths/sec + attached-pair matrix build time; % HBM peak, 1/2/4/8 GPU"
 
 
@@ -101,7 +102,7 @@ def main():
     ap.add_argument("--cpu-sources", type=int, default=12)
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
-    ap.add_argument("--dense-variant", type=int, default=0, help="0 = per-wave row streams (default), 1 = LDS-staged")
+    ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
     args = ap.parse_args()
 
     import torch
@@ -185,7 +186,8 @@ def main():
     # SURVEY.md 8d's B_src times the sources it covers.
     B_src = algorithmic_bytes_per_source(g.n, st["n_arcs"], A)
     if st["dense"]:
-        kname, launches, kms = "k_relax_dense", max(1, st["full_sweeps"]), st["full_ms"]
+        kname = "k_relax_dense" if args.dense_variant == 1 else "k_relax_dense_f"
+        launches, kms = max(1, st["full_sweeps"]), st["full_ms"]
     else:
         kname, launches, kms = "k_relax", max(1, st["relax_launches"]), st["relax_ms"]
     bytes_per_launch = rows * args.steps * B_src / launches
@@ -198,8 +200,18 @@ def main():
                 "launches_per_step": launches / args.steps,
                 "algorithmic_bytes_per_source": B_src, "algorithmic_bytes_per_launch": bytes_per_launch,
                 "measured_hbm_gbs": (traffic / avg_launch_s / 1e9) if (traffic and avg_launch_s > 0) else None}
+    if st["dense"]:
+        # the dense sweep is VALU-bound, not HBM-bound: price it also against the f64 VALU
+        # roofline of a naive exact kernel (one f64 add + one f64 compare per candidate
+        # (u, v, source); MI355X_MICROARCH.md: 78.6 TF/s f64 vector = 39.3e12 ops/s)
+        cand = float(g.n) * float(g.n) * rows * args.steps / launches
+        ach = cand / avg_launch_s if avg_launch_s > 0 else None
+        roofline["valu"] = {"unit": "candidates/s", "achieved": ach, "peak": F64_VALU_OPS / 2,
+                            "frac": ach / (F64_VALU_OPS / 2) if ach else None,
+                            "candidates_per_launch": cand,
+                            "note": "peak = f64 add+compare per candidate; the kernel filters in f32"}
     if st["dense"] and st["delta_sweeps"]:
-        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta",
+        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if args.dense_variant == 1 else "k_relax_dense_delta_p",
                                     "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
                                     "launches_per_step": st["delta_sweeps"] / args.steps}
 

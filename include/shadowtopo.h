@@ -69,7 +69,11 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_MAX_ROUNDS 3        /* iteration guard (default 4*V+64) */
 #define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
 #define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count (vertex, batch) visits and changes (CSR relax) */
-#define SHADOWTOPO_OPT_DENSE_VARIANT 6     /* dense relax kernel: 0 = per-wave row streams (default), 1 = LDS-staged rows */
+#define SHADOWTOPO_OPT_DENSE_VARIANT 6     /* dense relax kernels: SHADOWTOPO_DENSE_F32 (default) or _F64 */
+/* dense relaxation kernels (both exact; F32 pre-filters every candidate in f32 against a
+ * conservative threshold and re-evaluates the survivors in f64, F64 evaluates everything in f64) */
+#define SHADOWTOPO_DENSE_F32 0
+#define SHADOWTOPO_DENSE_F64 1
 #define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
                                               (vertex, source) pairs gets a change-mask delta round instead of a full
                                               sweep (default 125; 0 = always full sweeps) */

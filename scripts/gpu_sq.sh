@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${1:-sq}
 ARGS=${2:-"--steps 1 --warmup 1 --no-cpu-baseline"}
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU"
-P2="SQ_INSTS_SMEM SQ_INST_CYCLES_VALU SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_WAVES GRBM_GUI_ACTIVE"
+P2="SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAVES GRBM_GUI_ACTIVE"
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))

@@ -92,6 +92,7 @@ struct GraphDev {
 // Per-batch state lives in contiguous pools (slot b at offset b * vk), addressed from the
 // kernel argument itself: no dependent load of a descriptor before the first useful load.
 typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) float gfloat;
 typedef __attribute__((address_space(1))) uint32_t guint;
 typedef __attribute__((address_space(1))) int32_t gint;
 typedef __attribute__((address_space(1))) uint8_t gbyte;
@@ -107,6 +108,7 @@ struct Pools {
     unsigned long long* mask;  // [slot] lanes whose rows need the heap-exact replay
     double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
     unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
+    float* D32;         // dense mode: [slot][Vp][64] distance rounded down to f32 (NaN = unreached), filter key
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -125,6 +127,7 @@ struct BatchDev {
     gdouble* BDU;
     unsigned long long* chm0;
     unsigned long long* chm1;
+    gfloat* D32;
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
     __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
@@ -144,6 +147,7 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.BDU = p.BDU ? (gdouble*)(p.BDU + o) : nullptr;
     B.chm0 = p.chm ? p.chm + (size_t)b * 2 * p.Vp : nullptr;
     B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
+    B.D32 = p.D32 ? (gfloat*)(p.D32 + o) : nullptr;
     return B;
 }
 
@@ -162,6 +166,24 @@ constexpr int CSR_PAD = 8;  // in_src / in_w carry 8 padding arcs (u = 0, w = +i
 
 __device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000000000000LL); }
 __device__ __forceinline__ double dmax() { return __longlong_as_double(0x7fefffffffffffffLL); }
+
+// f32 filter key of a distance: rounded toward -inf, NaN when unreached (see k_relax_dense_f)
+__device__ __forceinline__ float f32_key(double d) {
+    return d < dinf() ? __double2float_rd(d) : __int_as_float(0x7fc00000);
+}
+
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long x, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
 
 __device__ __forceinline__ int64_t find_arc(const GraphDev& g, int32_t v, int32_t u) {
     int64_t lo = g.in_ptr[v], end = g.in_ptr[v + 1], hi = end;
@@ -198,8 +220,10 @@ __global__ void k_init(Pools pools, int32_t V) {
         B.act1[i] = 0;
     }
     if (B.chm0) {
-        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
             B.BDU[i] = inf;
+            B.D32[i] = __int_as_float(0x7fc00000);
+        }
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
             B.chm0[i] = 0;
             B.chm1[i] = 0;
@@ -219,6 +243,7 @@ __global__ void k_seed(GraphDev g, Pools pools) {
         B.H[idx] = 0;
         B.R[idx] = g.vfac[s];
         B.P[idx] = -1;
+        if (B.D32) B.D32[idx] = 0.0f;
     }
     for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act0[g.out_dst[x]] = 1;
 }
@@ -239,6 +264,7 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
     const double r = ru * in_r[arc];
     if (bc != curD || h != curH || r != curR || arc != curP) {
         B.D[idx] = bc;
+        if (B.D32) B.D32[idx] = f32_key(bc);
         B.H[idx] = h;
         B.R[idx] = r;
         B.P[idx] = arc;
@@ -373,6 +399,7 @@ __device__ __forceinline__ void relax_u(double du, double w, int32_t u, double& 
 // its lex key d(pred) (BDU, read by the delta rounds), and the per-vertex change mask of
 // the round (lane = source) that the next delta round walks; the batch counter gets the
 // number of changed (vertex, source) pairs.
+template <int TDT = DT>
 __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int32_t sv, int32_t v0, int32_t V,
                                                const double* bc, const double* bdu, const int32_t* bu, uint32_t tie,
                                                const int32_t* __restrict__ WI, int32_t Vp,
@@ -381,7 +408,7 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
     unsigned long long* chn = B.chm(parity);
     int32_t nch = 0;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
+    for (int t = 0; t < TDT; ++t) {
         const int32_t v = v0 + t;
         if (v >= V) break;
         bool ch = false;
@@ -462,92 +489,182 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
     dense_epilogue(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b);
 }
 
-// LDS-staged variant: a 512-thread block owns 64 destinations (8 waves x DT); every
-// 32-row chunk of d(u) (16 KB) is loaded from global memory once per block, double-buffered
-// in LDS, and read by all 8 waves (conflict-free ds_read_b64, lane = source) -- 8x less
-// L2/MALL traffic than one row stream per wave.  Weights stay on the scalar path.
-constexpr int LDS_ROWS = 32;
+// f32-filtered full sweep (default for dense graphs).  Every candidate is first tested in
+// f32 against a conservative threshold: D32 = d rounded down (NaN when unreached), W32 = w
+// rounded down (NaN when no arc), thr = bc rounded up plus 4 ulps (+inf when unreached).
+// fl32(D32 + W32) <= thr is implied by fl64(d + w) <= bc (the roundings lose < 2^-22
+// relative), so a failing filter proves the exact candidate cannot beat or tie the running
+// best and the lane can skip it; rows where any lane passes redo the exact f64
+// lexicographic update.  The f32 stream costs half the VALU cycles of f64 add + compare and
+// half the bytes per row.
+__device__ __forceinline__ float f32_thr(double bc) {
+    if (!(bc < dmax())) return __int_as_float(0x7f800000);  // unreached: any finite candidate passes
+    const float r = __double2float_ru(bc);
+    if (!(r < __int_as_float(0x7f800000))) return r;
+    return __int_as_float(__float_as_int(r) + 4);
+}
 
-__global__ __launch_bounds__(512) void k_relax_dense_lds(const double* __restrict__ W, const int32_t* __restrict__ WI,
-                                                         int32_t Vp, const double* __restrict__ in_r, Pools pools,
-                                                         int32_t V, int32_t nb, int32_t ntb64, int32_t parity,
-                                                         int32_t thresh, const int32_t* __restrict__ cnt_prev,
-                                                         int32_t* __restrict__ cnt) {
-    __shared__ __attribute__((aligned(16))) double sD[2][LDS_ROWS * KL];
+// One full sweep, f32-filtered and LDS-staged.  A 256-thread block owns 4*TDT consecutive
+// destinations (wave w: TDT of them) of one batch; the rows u stream through LDS in chunks
+// of SRS rows, double-buffered: the block's global loads of chunk k+1 (D32 rows, lane =
+// source, and the block's W32 columns) are in flight while chunk k is filtered.
+//  * lexicographic state starts at the seed candidate (source -> v arc: fl(0 + w), d = 0,
+//    u = s), so row u = s is skipped for that lane instead of re-offered;
+//  * filter per row: a lane passes iff D32(u) <= max_t fl32(thr_t - W32(u, v_t)), one
+//    subtraction per candidate plus a max tree (conservative: see f32_thr);
+//  * rows where any lane passes are collected and, at the end of the chunk, re-evaluated
+//    exactly in f64 (D and W from global memory) in row order -- the same lexicographic
+//    minimum and tie flag as a sequential scan.
+constexpr int SRS = 32;  // rows per LDS chunk
+
+template <int TDT, int XR>
+__global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
+                                                       const int32_t* __restrict__ WI, int32_t Vp,
+                                                       const double* __restrict__ in_r, Pools pools, int32_t V,
+                                                       int32_t nb, int32_t ntb, int32_t parity, int32_t thresh,
+                                                       const int32_t* __restrict__ cnt_prev,
+                                                       int32_t* __restrict__ cnt,
+                                                       unsigned long long* __restrict__ prof) {
+    constexpr int BW = 4 * TDT;                 // block columns
+    constexpr int WQ = BW / 4;                  // float4 per W32 chunk row
+    __shared__ __attribute__((aligned(16))) float sD[2][SRS * KL];
+    __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
     const int32_t L = blockIdx.x;
     const int32_t xcd = L & 7;
     const int32_t q = L >> 3;
-    const int32_t b = xcd + 8 * (q / ntb64);
-    if (b >= nb) return;  // block-uniform exits only: the loop below has barriers
+    const int32_t b = xcd + 8 * (q / ntb);
+    if (b >= nb) return;                        // block-uniform exits only (barriers below)
     if (cnt_prev[b] <= thresh) return;
-    const int32_t vb = (q % ntb64) * 64;
+    const int32_t vb = (q % ntb) * BW;
     if (vb >= V) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int32_t v0 = vb + wave * DT;
+    const int32_t v0 = vb + wave * TDT;
     const BatchDev B = batch_view(pools, b);
     const int32_t sv = B.srcv[lane];
-    double bc[DT], bdu[DT];
-    int32_t bu[DT];
+    double bc[TDT], bdu[TDT];
+    int32_t bu[TDT];
+    float thr[TDT];
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-        // seeded with the current distance (see k_relax_dense); padding rows are +inf
-        const double cd = B.D[(size_t)(v0 + t) * KL + lane];
-        bc[t] = cd < dinf() ? cd : dmax();
-        bdu[t] = dinf();
-        bu[t] = -1;
+    for (int t = 0; t < TDT; ++t) {
+        const int32_t v = v0 + t;
+        const double cd = B.D[(size_t)v * KL + lane];  // padding rows are +inf
+        const double ws = (sv >= 0 && sv != v) ? W[(size_t)sv * Vp + v] : dinf();
+        if (ws < dinf()) {
+            bc[t] = 0.0 + ws;
+            bdu[t] = 0.0;
+            bu[t] = sv;
+        } else {
+            bc[t] = dmax();
+            bdu[t] = dinf();
+            bu[t] = -1;
+        }
+        thr[t] = f32_thr(cd < bc[t] ? cd : bc[t]);
     }
     uint32_t tie = 0;
-    // chunk fill: thread -> (row fr, 4 consecutive lanes fc..fc+3)
-    const int fr = threadIdx.x >> 4;
-    const int fc = (threadIdx.x & 15) * 4;
-    typedef double dbl2 __attribute__((ext_vector_type(2)));
-    typedef __attribute__((address_space(1))) const dbl2 gd2;
-    const int32_t nchunks = (V + LDS_ROWS - 1) / LDS_ROWS;
-    dbl2 p0, p1;
-    {
-        const gd2* src = (const gd2*)(B.D + (size_t)fr * KL + fc);
-        p0 = src[0];
-        p1 = src[1];
-        dbl2* dst = (dbl2*)&sD[0][fr * KL + fc];
-        dst[0] = p0;
-        dst[1] = p1;
-    }
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const f4 gf4;
+    const gfloat* D32 = B.D32;
+    const int32_t nrows = (V + SRS - 1) / SRS * SRS;  // <= Vp: rows past V are NaN padding
+    // chunk fill: D32 rows = SRS*64 floats (2 float4 per thread), W32 = SRS*BW floats
+    constexpr int DQ = SRS * KL / 4 / 256;             // float4 of D32 per thread
+    constexpr int WQT = (SRS * WQ + 255) / 256;        // float4 of W32 per thread
+    f4 pd[DQ], pw[WQT];
+    auto fetch = [&](int32_t u0) {
+#pragma unroll
+        for (int i = 0; i < DQ; ++i) {
+            const int e = (threadIdx.x + i * 256);   // float4 index within the chunk
+            pd[i] = *(gf4*)(D32 + (size_t)u0 * KL + (size_t)e * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < WQT; ++i) {
+            const int e = threadIdx.x + i * 256;
+            if (e < SRS * WQ) {
+                const int r = e / WQ, c = e % WQ;
+                pw[i] = *(gf4*)((const gfloat*)W32 + (size_t)(u0 + r) * Vp + vb + c * 4);
+            }
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < DQ; ++i) *(f4*)&sD[buf][(threadIdx.x + i * 256) * 4] = pd[i];
+#pragma unroll
+        for (int i = 0; i < WQT; ++i) {
+            const int e = threadIdx.x + i * 256;
+            if (e < SRS * WQ) *(f4*)&sW[buf][e * 4] = pw[i];
+        }
+    };
+    fetch(0);
+    stash(0);
     __syncthreads();
-    for (int32_t k = 0; k < nchunks; ++k) {
-        const int cur = k & 1;
-        const bool more = k + 1 < nchunks;
-        if (more) {  // prefetch the next chunk into registers (rows past V are +inf padding)
-            const gd2* src = (const gd2*)(B.D + (size_t)((k + 1) * LDS_ROWS + fr) * KL + fc);
-            p0 = src[0];
-            p1 = src[1];
-        }
-        const double* rows = sD[cur];
-#pragma unroll 2
-        for (int r = 0; r < LDS_ROWS; ++r) {
-            const int32_t u = k * LDS_ROWS + r;
-            const double du = rows[r * KL + lane];
-            const double* w = W + (size_t)u * Vp + v0;
-            double c[DT];
-            unsigned long long hit = 0;
+    const gdouble* Dl = B.D + lane;
+    for (int32_t u0 = 0; u0 < nrows; u0 += SRS) {
+        const int cur = (u0 / SRS) & 1;
+        const bool more = u0 + SRS < nrows;
+        if (more) fetch(u0 + SRS);
+        // per lane: bit r = row u0 + r passed this lane's filter (no per-row wave vote)
+        uint32_t lhit = 0;
+#pragma unroll 4
+        for (int r = 0; r < SRS; ++r) {
+            const float du = sD[cur][r * KL + lane];
+            const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
+            float g = __int_as_float(0x7fc00000);
 #pragma unroll
-            for (int t = 0; t < DT; ++t) {
-                c[t] = du + w[t];
-                hit |= __ballot(c[t] <= bc[t]);
+            for (int j = 0; j < TDT / 4; ++j) {
+                const f4 w4 = wr[j];
+                g = fmaxf(g, fmaxf(fmaxf(thr[4 * j] - w4.x, thr[4 * j + 1] - w4.y),
+                                   fmaxf(thr[4 * j + 2] - w4.z, thr[4 * j + 3] - w4.w)));
             }
-            if (hit) {
+            lhit |= (du <= g) ? (1u << r) : 0u;
+        }
+        // the lane's own source row carries the seed candidate already
+        if ((uint32_t)(sv - u0) < (uint32_t)SRS) lhit &= ~(1u << (sv - u0));
+        // wave OR of the per-lane masks
 #pragma unroll
-                for (int t = 0; t < DT; ++t) lex_update(c[t], du, u, bc[t], bdu[t], bu[t], tie, 1u << t);
+        for (int off = 32; off > 0; off >>= 1) lhit |= (uint32_t)__shfl_xor((int)lhit, off);
+        unsigned long long hits = (uint32_t)__builtin_amdgcn_readfirstlane(lhit);
+        // exact f64 pass over the flagged rows, in row order, XR rows' loads in flight at
+        // once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column j % TDT,
+        // broadcast by readlane)
+        if (prof && hits && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hits));
+        while (hits) {
+            int32_t ur[XR];
+            int nr = 0;
+#pragma unroll
+            for (int k = 0; k < XR; ++k) {
+                ur[k] = u0;
+                if (hits) {
+                    ur[k] = u0 + __builtin_ctzll(hits);
+                    hits &= hits - 1;
+                    nr = k + 1;
+                }
+            }
+            double d64[XR], wl[XR];
+#pragma unroll
+            for (int k = 0; k < XR; ++k) {
+                d64[k] = Dl[(size_t)ur[k] * KL];
+                wl[k] = W[(size_t)ur[k] * Vp + v0 + (lane & (TDT - 1))];
+            }
+#pragma unroll
+            for (int k = 0; k < XR; ++k) {
+                if (k >= nr) break;
+                const int32_t u = ur[k];
+                const bool own = (u == sv);
+#pragma unroll
+                for (int t = 0; t < TDT; ++t) {
+                    const double c = d64[k] + readlane_d(wl[k], t);
+                    if (__ballot((c <= bc[t]) & !own)) {
+                        if (!own) lex_update(c, d64[k], u, bc[t], bdu[t], bu[t], tie, 1u << t);
+                        const float nt = f32_thr(bc[t]);
+                        thr[t] = nt < thr[t] ? nt : thr[t];
+                    }
+                }
             }
         }
-        if (more) {
-            dbl2* dst = (dbl2*)&sD[cur ^ 1][fr * KL + fc];
-            dst[0] = p0;
-            dst[1] = p1;
-        }
+        if (more) stash(cur ^ 1);
         __syncthreads();
     }
-    dense_epilogue(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b);
+    if (v0 < V) dense_epilogue<TDT>(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b);
 }
 
 // Dense round 0: every destination's only finite candidate is its source's direct arc
@@ -572,24 +689,12 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
         const size_t idx = (size_t)v * KL + lane;
         const int32_t arc = WI[(size_t)sv * Vp + v];
         B.D[idx] = 0.0 + w;
+        B.D32[idx] = f32_key(0.0 + w);
         B.H[idx] = ((hs & HMASK) + 1u) | (hs & TAINT);
         B.R[idx] = rs * in_r[arc];
         B.P[idx] = arc;
         B.BDU[idx] = 0.0;
     }
-}
-
-__device__ __forceinline__ double readlane_d(double x, int l) {
-    const long long b = __double_as_longlong(x);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long x, int l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
-    return ((unsigned long long)hi << 32) | lo;
 }
 
 // One candidate (u -> v for source lane s) with c <= d(v): the lexicographic update of
@@ -599,7 +704,7 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long x,
 __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, int32_t s, int32_t u, double du,
                                                 double c, double cur, const int32_t* __restrict__ WI, int32_t Vp,
                                                 const int32_t* __restrict__ in_src, const double* __restrict__ in_r,
-                                                double* sdcell) {
+                                                double* sdcell, float* tcell = nullptr) {
     const size_t idx = (size_t)v * KL + s;
     const uint32_t hv = B.H[idx];
     uint32_t lt = 0;
@@ -629,9 +734,11 @@ __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, in
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
     const double r = ru * in_r[arc];
     B.BDU[idx] = du;
-    *sdcell = c;
+    if (sdcell) *sdcell = c;
+    if (tcell) *tcell = f32_thr(c);
     if (c != cur || h != hv || r != B.R[idx] || arc != B.P[idx]) {
         B.D[idx] = c;
+        B.D32[idx] = f32_key(c);
         B.H[idx] = h;
         B.R[idx] = r;
         B.P[idx] = arc;
@@ -715,19 +822,142 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta(const double* __r
                 const int32_t u = u0 + us[i];
                 unsigned long long m = readlane_u64(mk, us[i]);
                 while (m) {
-                    const int32_t s = __builtin_ctzll(m);
+                    const int32_t sj = __builtin_ctzll(m);
                     m &= m - 1;
-                    const double du = readlane_d(dr[i], s - s0);
+                    const double du = readlane_d(dr[i], sj - s0);
                     const double c = du + w[i];
-                    double* cell = &sD[s * SDS + lane];
+                    double* cell = &sD[sj * SDS + lane];
                     const double cur = *cell;
                     if (c <= cur && c < inf && vok) {
-                        if (delta_candidate(B, v, s, u, du, c, cur, WI, Vp, in_src, in_r, cell)) mine |= 1ull << s;
+                        if (delta_candidate(B, v, sj, u, du, c, cur, WI, Vp, in_src, in_r, cell)) mine |= 1ull << sj;
                     }
                 }
             }
         }
     }
+    sM[wave][lane] = mine;
+    __syncthreads();
+    if (wave == 0) {
+        unsigned long long all = 0;
+#pragma unroll
+        for (int k = 0; k < DW; ++k) all |= sM[k][lane];
+        B.chm(parity)[v] = all;
+        if (all) atomicAdd(&cnt[b], (int32_t)__popcll(all));
+    }
+}
+
+// f32-filtered dense delta round, lane = candidate pair.  Same round semantics as
+// k_relax_dense_delta: every (u, s) pair that changed in the previous round is re-offered to
+// the block's 64 destinations.  Here the wave's changed pairs (its 16 sources) are listed in
+// an LDS ring in row order, and 64 of them are filtered at once, one per lane: the lane
+// streams W32(u, v0..v0+63) (lanes sharing a row share the loads) against the thresholds
+// sT[s][v] = f32_thr(d_s(v)) and passes iff D32(u, s) <= max_v fl32(sT[s][v] - W32(u, v))
+// (conservative, see k_relax_dense_f).  Passing pairs (rare) are then re-offered one at a
+// time with lane = destination, exactly in f64 through delta_candidate -- serialised, so no
+// two lanes ever update one (v, s) state.  No per-pair scalar work in the common path.
+constexpr int RING = 2048;  // > 63 pending + 64 rows x 16 sources
+
+__device__ __forceinline__ int sT_col(int s, int v) { return (v + 4 * s) & (KL - 1); }  // rotated rows
+
+__global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_p(const float* __restrict__ W32,
+                                                                 const double* __restrict__ W,
+                                                                 const int32_t* __restrict__ WI, int32_t Vp,
+                                                                 const int32_t* __restrict__ in_src,
+                                                                 const double* __restrict__ in_r, Pools pools,
+                                                                 int32_t V, int32_t nb, int32_t nvc, int32_t parity,
+                                                                 int32_t thresh, const int32_t* __restrict__ cnt_prev,
+                                                                 int32_t* __restrict__ cnt) {
+    constexpr int SW = KL / DW;  // sources per wave
+    __shared__ __attribute__((aligned(16))) float sT[KL * KL];
+    __shared__ int32_t sP[DW][RING];  // (u << 6) | s
+    __shared__ unsigned long long sM[DW][KL];
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const f4 gf4;
+    const int32_t L = blockIdx.x;
+    const int32_t q = L >> 3;
+    const int32_t b = q % nb;
+    const int32_t vc = (L & 7) + 8 * (q / nb);
+    if (vc >= nvc) return;  // block-uniform exits only (barriers below)
+    const int32_t cp = cnt_prev[b];
+    if (cp == 0 || cp > thresh) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int32_t v0 = vc * KL;
+    const int32_t v = v0 + lane;
+    const BatchDev B = batch_view(pools, b);
+    const gdouble* D = B.D;
+    for (int i = wave; i < KL; i += DW) sT[lane * KL + sT_col(lane, i)] = f32_thr(D[(size_t)(v0 + i) * KL + lane]);
+    __syncthreads();
+    const int32_t s0 = wave * SW;
+    const unsigned long long srange = ((1ull << SW) - 1ull) << s0;
+    const unsigned long long* chp = B.chm(parity ^ 1);
+    const gfloat* D32 = B.D32;
+    const gfloat* W32g = (const gfloat*)W32;
+    const bool vok = v < V;
+    const double inf = dinf();
+    int32_t* ring = sP[wave];
+    unsigned long long mine = 0;
+    int32_t head = 0, tail = 0;
+
+    // filter 64 pending pairs (lane = pair), then settle the passing ones exactly
+    auto drain = [&](int n) {
+        const bool valid = lane < n;
+        const int32_t e = ring[(head + (valid ? lane : 0)) & (RING - 1)];
+        const int32_t u = e >> 6, sp = e & 63;
+        const float du = D32[(size_t)u * KL + sp];
+        const gf4* wrow = (const gf4*)(W32g + (size_t)u * Vp + v0);
+        const float* trow = &sT[sp * KL];
+        float g = __int_as_float(0x7fc00000);
+#pragma unroll 4
+        for (int j = 0; j < KL / 4; ++j) {
+            const f4 w4 = wrow[j];
+            const f4 t4 = *(const f4*)&trow[sT_col(sp, 4 * j)];
+            g = fmaxf(g, fmaxf(fmaxf(t4.x - w4.x, t4.y - w4.y), fmaxf(t4.z - w4.z, t4.w - w4.w)));
+        }
+        unsigned long long pm = __ballot(valid && du <= g);
+        while (pm) {
+            const int pl = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const int32_t ue = __builtin_amdgcn_readlane(e, pl);
+            const int32_t uu = ue >> 6, ss = ue & 63;
+            float* tc = &sT[ss * KL + sT_col(ss, lane)];
+            const float c32 = D32[(size_t)uu * KL + ss] + W32g[(size_t)uu * Vp + v];
+            if (vok && c32 <= *tc) {
+                const double du64 = D[(size_t)uu * KL + ss];
+                const double c = du64 + W[(size_t)uu * Vp + v];
+                const double cur = D[(size_t)v * KL + ss];
+                if (c <= cur && c < inf &&
+                    delta_candidate(B, v, ss, uu, du64, c, cur, WI, Vp, in_src, in_r, nullptr, tc))
+                    mine |= 1ull << ss;
+            }
+        }
+        head += n;
+    };
+
+    for (int32_t u0 = 0; u0 < V; u0 += KL) {
+        const unsigned long long m = (u0 + lane < V) ? (chp[u0 + lane] & srange) : 0ull;
+        const int p = __popcll(m);
+        int incl = p;  // inclusive prefix sum over lanes
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off);
+            if (lane >= off) incl += o;
+        }
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        if (tot) {
+            int pos = tail + incl - p;
+            unsigned long long mm = m;
+            while (mm) {
+                ring[pos & (RING - 1)] = ((u0 + lane) << 6) | __builtin_ctzll(mm);
+                mm &= mm - 1;
+                ++pos;
+            }
+            tail += tot;
+            __builtin_amdgcn_wave_barrier();
+            while (tail - head >= KL) drain(KL);
+        }
+    }
+    if (tail > head) drain(tail - head);
     sM[wave][lane] = mine;
     __syncthreads();
     if (wave == 0) {
@@ -1150,6 +1380,7 @@ struct shadowtopo_engine {
     int32_t dense = 0;
     const double* d_W = nullptr;    // dense mode: [Vp][Vp] arc latency, +inf if none
     const int32_t* d_WI = nullptr;  // dense mode: [Vp][Vp] in-arc index, -1 if none
+    const float* d_W32 = nullptr;   // dense mode: [Vp][Vp] arc latency rounded down to f32, NaN if none
     int64_t E = 0;
     int64_t n_arcs = 0;
     uint32_t flags = 0;
@@ -1190,7 +1421,7 @@ struct shadowtopo_engine {
     int64_t opt_max_rounds = 0;
     int32_t opt_force_replay = 0;
     int32_t opt_profile = 0;
-    int32_t opt_dense_variant = 0;  // 0 = one row stream per wave (default), 1 = LDS-staged rows
+    int32_t opt_dense_variant = 0;  // SHADOWTOPO_DENSE_F32 (default) or SHADOWTOPO_DENSE_F64
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
@@ -1216,6 +1447,13 @@ int upload(shadowtopo_engine* eng, const std::vector<T>& h, const T** out) {
     if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
     *out = static_cast<const T*>(p);
     return SHADOWTOPO_OK;
+}
+
+// host twin of f32_key for finite values: the largest float <= x
+float f32_round_down(double x) {
+    float f = (float)x;  // round to nearest
+    if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
 }
 
 // stable counting sort of `idx` by key[idx]
@@ -1260,7 +1498,8 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
         return rc;
     if (eng->dense &&
         ((rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double))) ||
-         (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb))))
+         (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb)) ||
+         (rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))))
         return rc;
     eng->h_srcv.assign((size_t)KL * nb, -1);
     eng->h_row.assign((size_t)KL * nb, -1);
@@ -1288,7 +1527,7 @@ int ensure_replay(shadowtopo_engine* eng) {
 
 int32_t default_nb(const shadowtopo_engine* eng) {
     if (eng->opt_nb > 0) return eng->opt_nb;
-    const double per_batch = (double)eng->Vp * KL * (eng->dense ? 32.0 : 24.0) + 18.0 * eng->Vp;
+    const double per_batch = (double)eng->Vp * KL * (eng->dense ? 36.0 : 24.0) + 18.0 * eng->Vp;
     const double budget = 24.0e9;
     int32_t nb = (int32_t)std::max(1.0, std::min(16.0, std::floor(budget / per_batch)));
     return nb;
@@ -1303,6 +1542,18 @@ int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
     }
     eng->self_ready = true;
     return SHADOWTOPO_OK;
+}
+
+// the f32-filtered full sweep: 8 destinations per wave, exact rows settled 2 at a time
+hipError_t launch_dense_f(const shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
+                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
+    constexpr int TDT = 8, XR = 2;
+    const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
+    const int64_t nblocks = (int64_t)8 * ntb * ((nbg + 7) / 8);
+    hipLaunchKernelGGL((k_relax_dense_f<TDT, XR>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32, eng->d_W,
+                       eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
+                       cnt_cur, eng->d_prof);
+    return hipGetLastError();
 }
 
 // relax rounds for the batch slots [0, nbg) until no vertex changes
@@ -1320,8 +1571,6 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int64_t nblocks = (int64_t)8 * nvb * ((nbg + 7) / 8);
     const int32_t ntb = (V + 4 * DT - 1) / (4 * DT);
     const int64_t nblocks_dense = (int64_t)8 * ntb * ((nbg + 7) / 8);
-    const int32_t ntb64 = (V + 63) / 64;
-    const int64_t nblocks_lds = (int64_t)8 * ntb64 * ((nbg + 7) / 8);
     if (nblocks > 0x7fffffff) return fail(SHADOWTOPO_EINVAL, "grid too large");
     const int64_t max_rounds = eng->opt_max_rounds > 0 ? eng->opt_max_rounds : 4LL * V + 64;
     eng->d_prof = eng->opt_profile ? eng->prof_buf : nullptr;
@@ -1360,21 +1609,24 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             const int32_t par = (int32_t)(round & 1);
             if (any_full && any_delta && eng->opt_timing) HIP_TRY(hipEventRecord(eng->evm, s));
             if (any_full) {
-                if (eng->opt_dense_variant == 0)
+                if (eng->opt_dense_variant == SHADOWTOPO_DENSE_F64)
                     hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W,
                                        eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb, par, thresh, cnt_prev,
                                        cnt_cur);
                 else
-                    hipLaunchKernelGGL(k_relax_dense_lds, dim3((uint32_t)nblocks_lds), dim3(512), 0, s, eng->d_W,
-                                       eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb64, par, thresh,
-                                       cnt_prev, cnt_cur);
+                    HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s));
                 eng->st.full_sweeps++;
             }
             if (any_full && any_delta && eng->opt_timing) HIP_TRY(hipEventRecord(eng->evm2, s));
             if (any_delta) {
-                hipLaunchKernelGGL(k_relax_dense_delta, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s, eng->d_W,
-                                   eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par, thresh,
-                                   cnt_prev, cnt_cur);
+                if (eng->opt_dense_variant == SHADOWTOPO_DENSE_F64)
+                    hipLaunchKernelGGL(k_relax_dense_delta, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
+                                       eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par,
+                                       thresh, cnt_prev, cnt_cur);
+                else
+                    hipLaunchKernelGGL(k_relax_dense_delta_p, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
+                                       eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
+                                       nbg, nvc, par, thresh, cnt_prev, cnt_cur);
                 eng->st.delta_sweeps++;
             }
         } else {
@@ -1725,7 +1977,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->Vp = (V + 63) / 64 * 64;  // dense tiles of 64 destinations, 32-row LDS chunks
     {
         const double VV = (double)V * (double)V;
-        const bool fits = (double)eng->Vp * eng->Vp * 12.0 <= 24.0e9;
+        const bool fits = (double)eng->Vp * eng->Vp * 16.0 <= 24.0e9;
         if (flags & SHADOWTOPO_F_FORCE_DENSE)
             eng->dense = fits ? 1 : 0;
         else if (flags & SHADOWTOPO_F_FORCE_CSR)
@@ -1752,12 +2004,15 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         const size_t Vp = (size_t)eng->Vp;
         std::vector<double> W(Vp * Vp, std::numeric_limits<double>::infinity());
         std::vector<int32_t> WI(Vp * Vp, -1);
+        std::vector<float> W32(Vp * Vp, std::numeric_limits<float>::quiet_NaN());
         for (int32_t v = 0; v < V; ++v)
             for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) {
                 W[(size_t)in_src[x] * Vp + v] = in_w[x];
                 WI[(size_t)in_src[x] * Vp + v] = (int32_t)x;
+                W32[(size_t)in_src[x] * Vp + v] = f32_round_down(in_w[x]);
             }
-        if ((rc = upload(eng, W, &eng->d_W)) || (rc = upload(eng, WI, &eng->d_WI))) {
+        if ((rc = upload(eng, W, &eng->d_W)) || (rc = upload(eng, WI, &eng->d_WI)) ||
+            (rc = upload(eng, W32, &eng->d_W32))) {
             shadowtopo_destroy(eng);
             return rc;
         }
@@ -1862,6 +2117,8 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_profile = value ? 1 : 0;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DENSE_VARIANT:
+            if (value != SHADOWTOPO_DENSE_F32 && value != SHADOWTOPO_DENSE_F64)
+                return fail(SHADOWTOPO_EINVAL, "unknown dense variant %lld", (long long)value);
             eng->opt_dense_variant = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_PERMILLE:

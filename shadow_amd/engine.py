@@ -33,6 +33,8 @@ OPT_MAX_ROUNDS = 3
 OPT_FORCE_REPLAY = 4
 OPT_PROFILE = 5
 OPT_DENSE_VARIANT = 6
+DENSE_F32 = 0  # f32-filtered full sweep + lane-per-pair delta rounds (default)
+DENSE_F64 = 1  # f64 row-stream kernels (cross-check)
 OPT_DELTA_PERMILLE = 7
 
 # every symbol include/shadowtopo.h declares

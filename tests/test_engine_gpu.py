@@ -169,16 +169,17 @@ def test_csr_forced_on_dense_graph():
     assert st["dense"] == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [E.DENSE_F32, E.DENSE_F64])
 def test_dense_variants_agree(variant):
     g = synth.random_sparse(V=333, avg_deg=6, seed=23)
     assert compare(g, layout="dense", dense_variant=variant)["dense"] == 1
 
 
 # ---- dense delta rounds (k_relax_dense_delta): change-mask rounds after the first sweep
+@pytest.mark.parametrize("variant", [E.DENSE_F32, E.DENSE_F64])
 @pytest.mark.parametrize("permille", [0, 1000])
 @pytest.mark.parametrize("case", ["sparse", "directed", "ties", "vloss_prefer", "multigraph", "geometric"])
-def test_dense_delta_rounds(case, permille):
+def test_dense_delta_rounds(case, permille, variant):
     if case == "sparse":
         g = synth.random_sparse(V=301, avg_deg=5, seed=2)
     elif case == "directed":
@@ -199,7 +200,7 @@ def test_dense_delta_rounds(case, permille):
         g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 30)])
     else:
         g = synth.geometric_complete_ish(V=700, A=130)
-    st = compare(g, layout="dense", delta_permille=permille)
+    st = compare(g, layout="dense", delta_permille=permille, dense_variant=variant)
     assert st["dense"] == 1
     if permille == 0:
         assert st["delta_sweeps"] == 0
@@ -214,15 +215,17 @@ def test_dense_delta_same_fixed_point(case):
     g = synth.integer_grid(rows=12, cols=13, seed=4) if case == "ties" else synth.random_sparse(V=400, avg_deg=6, seed=8)
     srcs = np.arange(0, g.n, 3, dtype=np.int32)
     outs = []
-    for permille in (0, 1000):
+    for permille, variant in ((0, E.DENSE_F32), (1000, E.DENSE_F32), (1000, E.DENSE_F64), (0, E.DENSE_F64)):
         eng = E.Engine.from_synth(g, layout="dense")
         eng.set_option(E.OPT_DELTA_PERMILLE, permille)
+        eng.set_option(E.OPT_DENSE_VARIANT, variant)
         outs.append(eng.sssp(srcs))
         eng.close()
-    (d0, p0, h0, t0), (d1, p1, h1, t1) = outs
-    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
-    assert np.array_equal(t0, t1)
-    ok = t0 == 0
-    assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
+    (d0, p0, h0, t0) = outs[0]
+    for d1, p1, h1, t1 in outs[1:]:
+        assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+        assert np.array_equal(t0, t1)
+        ok = t0 == 0
+        assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
     if case == "ties":
         assert (t0 != 0).any()

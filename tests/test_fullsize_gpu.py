@@ -1,0 +1,85 @@
+"""Full-size parity on BASELINE.json's configs C2-C5 (SURVEY.md 8d generators, fixed seeds).
+
+The engine computes whole attached rows at the real graph size (C2: every one of the 1000
+sources, i.e. the bench workload itself; C3-C5: a source block spanning several batches).
+A sample of those rows is checked bit-exact against the CPU oracle (heap-exact igraph
+restatement, a second or two per row at these sizes); every computed row is checked for
+size-independent properties: the reference's pair kinds, hop/latency consistency, and
+d(s, t) <= w(s, t) wherever the arc exists (a shortest path is never longer than the edge).
+"""
+import numpy as np
+import pytest
+
+from paritylib import assert_bitexact, oracle_for
+from shadow_amd import engine as E
+from shadow_amd import synth
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+KIND_DIJKSTRA = 3
+
+
+def _run(g, r0, r1, sample, **opts):
+    eng = E.Engine.from_synth(g)
+    for k, v in opts.items():
+        eng.set_option(getattr(E, "OPT_" + k.upper()), v)
+    eng.set_attached(g.attached)
+    lat, rel, hops, kind = eng.compute_rows(r0, r1)
+    st = eng.stats()
+    eng.close()
+    og = oracle_for(g)
+    flags = og.flags(prefer_direct=g.prefer_direct)
+    for r in sample:
+        olat, orel, ohops, okind, _ = og.pair_rows(flags, g.attached, r, r + 1, nthreads=1)
+        i = r - r0
+        assert_bitexact(f"kind row {r}", kind[i:i + 1], okind)
+        assert_bitexact(f"latency row {r}", lat[i:i + 1], olat)
+        assert_bitexact(f"hops row {r}", hops[i:i + 1], ohops)
+        assert_bitexact(f"reliability row {r}", rel[i:i + 1], orel)
+    # properties of every computed row
+    dj = kind == KIND_DIJKSTRA
+    assert dj.any()
+    assert (lat[dj] > 0).all() and (hops[dj] >= 1).all()
+    assert ((rel[dj] > 0) & (rel[dj] <= 1)).all()
+    assert (lat[kind == 0] == -1).all()
+    # shortest path <= the direct arc: check against the edge list
+    A = len(g.attached)
+    pos = np.full(g.n, -1, np.int64)
+    pos[g.attached] = np.arange(A)
+    src, dst = g.src.astype(np.int64), g.dst.astype(np.int64)
+    for a, b in ((src, dst), (dst, src)):
+        pa, pb = pos[a], pos[b]
+        keep = (pa >= r0) & (pa < r1) & (pb >= 0) & (a != b)
+        i, j = pa[keep] - r0, pb[keep]
+        w = g.latency[keep]
+        ok = (kind[i, j] != KIND_DIJKSTRA) | (lat[i, j] <= w)
+        assert ok.all(), f"{(~ok).sum()} pairs longer than their direct arc"
+    return st
+
+
+def test_c2_geometric_full_matrix():
+    """The bench workload: V=10^4 complete-ish graph, all 1000 attached sources (16 batches)."""
+    g = synth.geometric_complete_ish(V=10_000, A=1_000)
+    st = _run(g, 0, 1000, sample=[0, 63, 64, 517, 999])
+    assert st["dense"] == 1 and st["replayed_sources"] == 0
+
+
+def test_c2_geometric_f64_kernels():
+    g = synth.geometric_complete_ish(V=10_000, A=1_000)
+    st = _run(g, 0, 192, sample=[5, 130], dense_variant=E.DENSE_F64)
+    assert st["dense"] == 1
+
+
+def test_c3_knn_full_size():
+    g = synth.knn_geographic(V=7_000)
+    _run(g, 0, 256, sample=[0, 100, 255])
+
+
+def test_c4_barabasi_albert_full_size():
+    g = synth.barabasi_albert(V=100_000, A=10_000)
+    _run(g, 4_000, 4_256, sample=[4_000, 4_191])
+
+
+def test_c5_chung_lu_full_size():
+    g = synth.chung_lu(V=1_000_000, A=50_000)
+    _run(g, 20_000, 20_128, sample=[20_001])
