@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
+    ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
+    ap.add_argument("--csr-variant", type=int, default=1, help="1 = full recomputation (default), 0 = delta rounds")
     args = ap.parse_args()
 
     import torch
@@ -136,6 +138,9 @@ def main():
     if args.batches:
         eng.set_option(E.OPT_BATCHES_IN_FLIGHT, args.batches)
     eng.set_option(E.OPT_DENSE_VARIANT, args.dense_variant)
+    if args.dense_tb:
+        eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
+    eng.set_option(E.OPT_CSR_VARIANT, args.csr_variant)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0

@@ -77,6 +77,15 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
                                               (vertex, source) pairs gets a change-mask delta round instead of a full
                                               sweep (default 125; 0 = always full sweeps) */
+#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default) or _DELTA */
+#define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1, 2 = default, 4) */
+
+/* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every
+ * in-arc of every active vertex; DELTA folds only the in-neighbours whose state changed for
+ * the lane's source into the recorded lexicographic state (fewer row bytes, more
+ * instructions and dependent loads: slower on the C3/C4 graphs, kept as a cross-check) */
+#define SHADOWTOPO_CSR_DELTA 0
+#define SHADOWTOPO_CSR_FULL 1
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;

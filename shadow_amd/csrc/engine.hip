@@ -222,7 +222,7 @@ __global__ void k_init(Pools pools, int32_t V) {
     if (B.chm0) {
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
             B.BDU[i] = inf;
-            B.D32[i] = __int_as_float(0x7fc00000);
+            if (B.D32) B.D32[i] = __int_as_float(0x7fc00000);
         }
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
             B.chm0[i] = 0;
@@ -243,7 +243,11 @@ __global__ void k_seed(GraphDev g, Pools pools) {
         B.H[idx] = 0;
         B.R[idx] = g.vfac[s];
         B.P[idx] = -1;
-        if (B.D32) B.D32[idx] = 0.0f;
+        // f32 filter key NaN: the source's own row never passes a dense filter (its seed
+        // candidate starts every lexicographic state, k_relax_dense_f)
+        if (B.D32) B.D32[idx] = __int_as_float(0x7fc00000);
+        // round 0 of the CSR delta rounds reads the change masks of a virtual round -1
+        if (B.chm1) atomicOr(&B.chm1[s], 1ull << j);
     }
     for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act0[g.out_dst[x]] = 1;
 }
@@ -349,6 +353,135 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
     bool ch = false;
     if (be >= 0 && sv >= 0 && sv != v) ch = finish_vertex(B, lane, v, be, bu, bc, bdu, tie, in_r, curD, curH, curR, curP);
     if (__ballot(ch)) {
+        gbyte* act_nxt = B.act(parity ^ 1);
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7)) + 1], 1ull);
+    }
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7))], 1ull);
+}
+
+// CSR delta round (default for sparse graphs).  Same pull schedule as k_relax (one wave per
+// active destination v, in-arcs in chunks of 8), but a lane only looks at in-neighbours u
+// whose state changed for ITS source in the previous round (chm: per-vertex 64-bit lane
+// masks), and folds those candidates into v's recorded lexicographic state (D, BDU = d(pred),
+// P, local-tie bit) with the rules of delta_candidate.  Unchanged (u, source) pairs were
+// folded in when they last changed, so the recorded state plus the changed candidates is
+// the full minimum.  The d(u) row loads are masked to the changed lanes: a row whose
+// single changed source shares one 64-byte line with 7 unchanged ones costs one line,
+// not 512 bytes.
+__global__ __launch_bounds__(256) void k_relax_delta(const int64_t* __restrict__ in_ptr,
+                                                     const int32_t* __restrict__ in_src,
+                                                     const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                                     const int64_t* __restrict__ out_ptr,
+                                                     const int32_t* __restrict__ out_dst, Pools pools, int32_t V,
+                                                     int32_t nb, int32_t nvb, int32_t parity, int32_t* __restrict__ cnt,
+                                                     unsigned long long* __restrict__ prof) {
+    const int32_t L = blockIdx.x;
+    const int32_t xcd = L & 7;
+    const int32_t q = L >> 3;
+    const int32_t b = xcd + 8 * (q / nvb);
+    if (b >= nb) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v = (q % nvb) * 4 + wave;
+    if (v >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    gbyte* act_cur = B.act(parity);
+    if (act_cur[v] == 0) {
+        if (lane == 0) B.chm(parity)[v] = 0ull;  // every (v, batch) has a wave: clear the stale mask
+        return;
+    }
+    if (lane == 0) act_cur[v] = 0;
+    const unsigned long long* chp = B.chm(parity ^ 1);
+    // masks written earlier in this same round too (Gauss-Seidel: a change made this round
+    // reaches v now instead of a round later; a mask seen twice re-offers an unchanged
+    // candidate, which the rules below leave as it is)
+    const unsigned long long* chc = B.chm(parity);
+    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
+    const int32_t sv = B.srcv[lane];
+    const size_t idx = (size_t)v * KL + lane;
+    const double D0 = B.D[idx];
+    const double B0 = B.BDU[idx];
+    const int32_t P0 = B.P[idx];
+    const uint32_t H0 = B.H[idx];
+    double d = D0, bdu = B0;
+    int32_t pa = P0;
+    int32_t pu = P0 >= 0 ? in_src[P0] : -1;
+    bool lt = (H0 & LTIE) != 0;
+    bool touched = false;
+    const gdouble* Dl = B.D + lane;
+    for (int32_t e = beg; e < end; e += 8) {
+        int32_t u[8];
+        double w[8];
+        unsigned long long m[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u[k] = in_src[e + k];
+            w[k] = in_w[e + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m[k] = (e + k < end) ? (chp[u[k]] | chc[u[k]]) : 0ull;
+        double du[8];
+        bool on[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            on[k] = (m[k] >> lane) & 1ull;
+            du[k] = on[k] ? Dl[(size_t)u[k] * KL] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (!on[k]) continue;
+            const double c = du[k] + w[k];  // igraph: altdist = mindist + weights[edge]
+            // a same-round mask can become visible before the d(u) it announces (no fence):
+            // the stale d(u) is a weaker candidate, re-offered next round from chp; an
+            // unreached one (+inf) must not enter the equal-distance rules below
+            if (!(c < dinf())) continue;
+            if (c < d) {
+                d = c;
+                bdu = du[k];
+                pa = e + k;
+                pu = u[k];
+                lt = du[k] == c;  // degenerate d(u) == d(v): heap-order dependent
+                touched = true;
+            } else if (c == d) {
+                if (pu == u[k]) {  // the recorded predecessor refreshed
+                    lt = (du[k] == bdu && lt) || du[k] == c;
+                    bdu = du[k];
+                    touched = true;
+                } else if (du[k] < bdu) {
+                    bdu = du[k];
+                    pa = e + k;
+                    pu = u[k];
+                    lt = du[k] == c;
+                    touched = true;
+                } else if (du[k] == bdu) {
+                    lt = true;  // two predecessors at the same d(u): heap pop order decides
+                    touched = true;
+                }
+            }
+        }
+    }
+    bool ch = false;
+    if (touched && sv >= 0 && sv != v) {
+        const size_t uidx = (size_t)pu * KL + lane;
+        const uint32_t hu = B.H[uidx];
+        const double ru = B.R[uidx];
+        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
+        const double r = ru * in_r[pa];
+        const double R0 = B.R[idx];
+        ch = d != D0 || h != H0 || r != R0 || pa != P0;
+        if (ch) {
+            B.D[idx] = d;
+            B.H[idx] = h;
+            B.R[idx] = r;
+            B.P[idx] = pa;
+        }
+        if (bdu != B0) B.BDU[idx] = bdu;
+    }
+    const unsigned long long mask = __ballot(ch);
+    if (lane == 0) B.chm(parity)[v] = mask;
+    if (mask) {
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
         if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
@@ -517,7 +650,7 @@ __device__ __forceinline__ float f32_thr(double bc) {
 //    minimum and tie flag as a sequential scan.
 constexpr int SRS = 32;  // rows per LDS chunk
 
-template <int TDT, int XR>
+template <int TDT, int XR, int TB>
 __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
@@ -525,57 +658,73 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
                                                        const int32_t* __restrict__ cnt_prev,
                                                        int32_t* __restrict__ cnt,
                                                        unsigned long long* __restrict__ prof) {
-    constexpr int BW = 4 * TDT;                 // block columns
-    constexpr int WQ = BW / 4;                  // float4 per W32 chunk row
-    __shared__ __attribute__((aligned(16))) float sD[2][SRS * KL];
+    constexpr int BW = 4 * TDT;  // block columns
+    constexpr int WQ = BW / 4;   // float4 per W32 chunk row
+    __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
     __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
     const int32_t L = blockIdx.x;
     const int32_t xcd = L & 7;
     const int32_t q = L >> 3;
-    const int32_t b = xcd + 8 * (q / ntb);
-    if (b >= nb) return;                        // block-uniform exits only (barriers below)
-    if (cnt_prev[b] <= thresh) return;
+    const int32_t b0 = (xcd + 8 * (q / ntb)) * TB;  // this block's TB batches
+    if (b0 >= nb) return;                           // block-uniform exits only (barriers below)
+    bool live[TB];
+    int32_t first = -1;
+#pragma unroll
+    for (int k = 0; k < TB; ++k) {
+        live[k] = b0 + k < nb && cnt_prev[b0 + k] > thresh;
+        if (live[k] && first < 0) first = b0 + k;
+    }
+    if (first < 0) return;
     const int32_t vb = (q % ntb) * BW;
     if (vb >= V) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int32_t v0 = vb + wave * TDT;
-    const BatchDev B = batch_view(pools, b);
-    const int32_t sv = B.srcv[lane];
-    double bc[TDT], bdu[TDT];
-    int32_t bu[TDT];
-    float thr[TDT];
+    BatchDev B[TB];
+    int32_t sv[TB];
+    double bc[TB][TDT], bdu[TB][TDT];
+    int32_t bu[TB][TDT];
+    float thr[TB][TDT];
+    uint32_t tie[TB];
 #pragma unroll
-    for (int t = 0; t < TDT; ++t) {
-        const int32_t v = v0 + t;
-        const double cd = B.D[(size_t)v * KL + lane];  // padding rows are +inf
-        const double ws = (sv >= 0 && sv != v) ? W[(size_t)sv * Vp + v] : dinf();
-        if (ws < dinf()) {
-            bc[t] = 0.0 + ws;
-            bdu[t] = 0.0;
-            bu[t] = sv;
-        } else {
-            bc[t] = dmax();
-            bdu[t] = dinf();
-            bu[t] = -1;
+    for (int k = 0; k < TB; ++k) {
+        // a batch of the group that is past nb or left to the delta round stages a live
+        // batch's rows with NaN thresholds: it never passes and is never written
+        B[k] = batch_view(pools, live[k] ? b0 + k : first);
+        sv[k] = B[k].srcv[lane];
+        tie[k] = 0;
+#pragma unroll
+        for (int t = 0; t < TDT; ++t) {
+            const int32_t v = v0 + t;
+            const double cd = B[k].D[(size_t)v * KL + lane];  // padding rows are +inf
+            const double ws = (sv[k] >= 0 && sv[k] != v) ? W[(size_t)sv[k] * Vp + v] : dinf();
+            if (ws < dinf()) {
+                bc[k][t] = 0.0 + ws;
+                bdu[k][t] = 0.0;
+                bu[k][t] = sv[k];
+            } else {
+                bc[k][t] = dmax();
+                bdu[k][t] = dinf();
+                bu[k][t] = -1;
+            }
+            thr[k][t] = live[k] ? f32_thr(cd < bc[k][t] ? cd : bc[k][t]) : __int_as_float(0x7fc00000);
         }
-        thr[t] = f32_thr(cd < bc[t] ? cd : bc[t]);
     }
-    uint32_t tie = 0;
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const f4 gf4;
-    const gfloat* D32 = B.D32;
     const int32_t nrows = (V + SRS - 1) / SRS * SRS;  // <= Vp: rows past V are NaN padding
-    // chunk fill: D32 rows = SRS*64 floats (2 float4 per thread), W32 = SRS*BW floats
-    constexpr int DQ = SRS * KL / 4 / 256;             // float4 of D32 per thread
-    constexpr int WQT = (SRS * WQ + 255) / 256;        // float4 of W32 per thread
-    f4 pd[DQ], pw[WQT];
+    // chunk fill: TB x D32 rows = SRS*64 floats each (2 float4 per thread), W32 = SRS*BW floats
+    constexpr int DQ = SRS * KL / 4 / 256;       // float4 of one batch's D32 chunk per thread
+    constexpr int WQT = (SRS * WQ + 255) / 256;  // float4 of W32 per thread
+    f4 pd[TB][DQ], pw[WQT];
     auto fetch = [&](int32_t u0) {
 #pragma unroll
-        for (int i = 0; i < DQ; ++i) {
-            const int e = (threadIdx.x + i * 256);   // float4 index within the chunk
-            pd[i] = *(gf4*)(D32 + (size_t)u0 * KL + (size_t)e * 4);
-        }
+        for (int k = 0; k < TB; ++k)
+#pragma unroll
+            for (int i = 0; i < DQ; ++i) {
+                const int e = threadIdx.x + i * 256;  // float4 index within the chunk
+                pd[k][i] = *(gf4*)(B[k].D32 + (size_t)u0 * KL + (size_t)e * 4);
+            }
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
             const int e = threadIdx.x + i * 256;
@@ -587,7 +736,9 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     };
     auto stash = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < DQ; ++i) *(f4*)&sD[buf][(threadIdx.x + i * 256) * 4] = pd[i];
+        for (int k = 0; k < TB; ++k)
+#pragma unroll
+            for (int i = 0; i < DQ; ++i) *(f4*)&sD[buf][k][(threadIdx.x + i * 256) * 4] = pd[k][i];
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
             const int e = threadIdx.x + i * 256;
@@ -597,66 +748,76 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     fetch(0);
     stash(0);
     __syncthreads();
-    const gdouble* Dl = B.D + lane;
     for (int32_t u0 = 0; u0 < nrows; u0 += SRS) {
         const int cur = (u0 / SRS) & 1;
         const bool more = u0 + SRS < nrows;
         if (more) fetch(u0 + SRS);
-        // per lane: bit r = row u0 + r passed this lane's filter (no per-row wave vote)
-        uint32_t lhit = 0;
-#pragma unroll 4
+        // per lane and batch: bit r = row u0 + r passed the filter (no per-row wave vote);
+        // one broadcast read of the row's TDT weights serves all TB batches
+        uint32_t lhit[TB];
+#pragma unroll
+        for (int k = 0; k < TB; ++k) lhit[k] = 0;
+#pragma unroll 2
         for (int r = 0; r < SRS; ++r) {
-            const float du = sD[cur][r * KL + lane];
             const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
-            float g = __int_as_float(0x7fc00000);
+            f4 w4[TDT / 4];
 #pragma unroll
-            for (int j = 0; j < TDT / 4; ++j) {
-                const f4 w4 = wr[j];
-                g = fmaxf(g, fmaxf(fmaxf(thr[4 * j] - w4.x, thr[4 * j + 1] - w4.y),
-                                   fmaxf(thr[4 * j + 2] - w4.z, thr[4 * j + 3] - w4.w)));
+            for (int j = 0; j < TDT / 4; ++j) w4[j] = wr[j];
+#pragma unroll
+            for (int k = 0; k < TB; ++k) {
+                const float du = sD[cur][k][r * KL + lane];
+                float g = __int_as_float(0x7fc00000);
+#pragma unroll
+                for (int j = 0; j < TDT / 4; ++j)
+                    g = fmaxf(g, fmaxf(fmaxf(thr[k][4 * j] - w4[j].x, thr[k][4 * j + 1] - w4[j].y),
+                                       fmaxf(thr[k][4 * j + 2] - w4[j].z, thr[k][4 * j + 3] - w4[j].w)));
+                lhit[k] |= (du <= g) ? (1u << r) : 0u;
             }
-            lhit |= (du <= g) ? (1u << r) : 0u;
         }
-        // the lane's own source row carries the seed candidate already
-        if ((uint32_t)(sv - u0) < (uint32_t)SRS) lhit &= ~(1u << (sv - u0));
-        // wave OR of the per-lane masks
+        // exact f64 pass over each batch's flagged rows, in row order, XR rows' loads in
+        // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
+        // j % TDT, broadcast by readlane).  A source's own row never passes (its D32 is NaN:
+        // the seed candidate is in the lexicographic state already).
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) lhit |= (uint32_t)__shfl_xor((int)lhit, off);
-        unsigned long long hits = (uint32_t)__builtin_amdgcn_readfirstlane(lhit);
-        // exact f64 pass over the flagged rows, in row order, XR rows' loads in flight at
-        // once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column j % TDT,
-        // broadcast by readlane)
-        if (prof && hits && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hits));
-        while (hits) {
-            int32_t ur[XR];
-            int nr = 0;
+        for (int k = 0; k < TB; ++k) {
+            if (!live[k]) continue;
+            uint32_t lh = lhit[k];
 #pragma unroll
-            for (int k = 0; k < XR; ++k) {
-                ur[k] = u0;
-                if (hits) {
-                    ur[k] = u0 + __builtin_ctzll(hits);
-                    hits &= hits - 1;
-                    nr = k + 1;
+            for (int off = 32; off > 0; off >>= 1) lh |= (uint32_t)__shfl_xor((int)lh, off);
+            unsigned long long hits = (uint32_t)__builtin_amdgcn_readfirstlane(lh);
+            if (prof && hits && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hits));
+            const gdouble* Dl = B[k].D + lane;
+            while (hits) {
+                int32_t ur[XR];
+                int nr = 0;
+#pragma unroll
+                for (int x = 0; x < XR; ++x) {
+                    ur[x] = u0;
+                    if (hits) {
+                        ur[x] = u0 + __builtin_ctzll(hits);
+                        hits &= hits - 1;
+                        nr = x + 1;
+                    }
                 }
-            }
-            double d64[XR], wl[XR];
+                double d64[XR], wl[XR];
 #pragma unroll
-            for (int k = 0; k < XR; ++k) {
-                d64[k] = Dl[(size_t)ur[k] * KL];
-                wl[k] = W[(size_t)ur[k] * Vp + v0 + (lane & (TDT - 1))];
-            }
+                for (int x = 0; x < XR; ++x) {
+                    d64[x] = Dl[(size_t)ur[x] * KL];
+                    wl[x] = W[(size_t)ur[x] * Vp + v0 + (lane & (TDT - 1))];
+                }
 #pragma unroll
-            for (int k = 0; k < XR; ++k) {
-                if (k >= nr) break;
-                const int32_t u = ur[k];
-                const bool own = (u == sv);
+                for (int x = 0; x < XR; ++x) {
+                    if (x >= nr) break;
+                    const int32_t u = ur[x];
+                    const bool own = (u == sv[k]);
 #pragma unroll
-                for (int t = 0; t < TDT; ++t) {
-                    const double c = d64[k] + readlane_d(wl[k], t);
-                    if (__ballot((c <= bc[t]) & !own)) {
-                        if (!own) lex_update(c, d64[k], u, bc[t], bdu[t], bu[t], tie, 1u << t);
-                        const float nt = f32_thr(bc[t]);
-                        thr[t] = nt < thr[t] ? nt : thr[t];
+                    for (int t = 0; t < TDT; ++t) {
+                        const double c = d64[x] + readlane_d(wl[x], t);
+                        if (__ballot((c <= bc[k][t]) & !own)) {
+                            if (!own) lex_update(c, d64[x], u, bc[k][t], bdu[k][t], bu[k][t], tie[k], 1u << t);
+                            const float nt = f32_thr(bc[k][t]);
+                            thr[k][t] = nt < thr[k][t] ? nt : thr[k][t];
+                        }
                     }
                 }
             }
@@ -664,7 +825,13 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         if (more) stash(cur ^ 1);
         __syncthreads();
     }
-    if (v0 < V) dense_epilogue<TDT>(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b);
+    if (v0 < V) {
+#pragma unroll
+        for (int k = 0; k < TB; ++k)
+            if (live[k])
+                dense_epilogue<TDT>(B[k], lane, sv[k], v0, V, bc[k], bdu[k], bu[k], tie[k], WI, Vp, in_r, parity,
+                                    cnt, b0 + k);
+    }
 }
 
 // Dense round 0: every destination's only finite candidate is its source's direct arc
@@ -1422,6 +1589,8 @@ struct shadowtopo_engine {
     int32_t opt_force_replay = 0;
     int32_t opt_profile = 0;
     int32_t opt_dense_variant = 0;  // SHADOWTOPO_DENSE_F32 (default) or SHADOWTOPO_DENSE_F64
+    int32_t opt_csr_variant = 1;    // SHADOWTOPO_CSR_FULL (default) or SHADOWTOPO_CSR_DELTA
+    int32_t opt_dense_tb = 1;       // batches per wave in the f32-filtered full sweep (1, 2 or 4)
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
@@ -1496,11 +1665,10 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.mask, sizeof(unsigned long long) * nb)))
         return rc;
-    if (eng->dense &&
-        ((rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double))) ||
-         (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb)) ||
-         (rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))))
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double))) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb)))
         return rc;
+    if (eng->dense && (rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))) return rc;
     eng->h_srcv.assign((size_t)KL * nb, -1);
     eng->h_row.assign((size_t)KL * nb, -1);
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
@@ -1525,12 +1693,20 @@ int ensure_replay(shadowtopo_engine* eng) {
     return SHADOWTOPO_OK;
 }
 
-int32_t default_nb(const shadowtopo_engine* eng) {
-    if (eng->opt_nb > 0) return eng->opt_nb;
-    const double per_batch = (double)eng->Vp * KL * (eng->dense ? 36.0 : 24.0) + 18.0 * eng->Vp;
-    const double budget = 24.0e9;
-    int32_t nb = (int32_t)std::max(1.0, std::min(16.0, std::floor(budget / per_batch)));
-    return nb;
+// batch slots in flight: enough for every requested row when HBM allows.  Sparse rounds
+// cost a launch + a flag read-back each, so more batches per round means fewer rounds in
+// total; the budget is 40 % of the free HBM (MI355X: 288 GB) beside the resident graph.
+int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
+    const int32_t need = std::max(1, (rows + KL - 1) / KL);
+    if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
+    const double per_batch = (double)eng->Vp * KL * (eng->dense ? 36.0 : 32.0) + 18.0 * eng->Vp;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
+    const double budget = std::max(24.0e9, 0.4 * ((double)free_b + held));
+    const double cap = eng->dense ? 16.0 : 256.0;
+    const int32_t nb = (int32_t)std::max(1.0, std::min(cap, std::floor(budget / per_batch)));
+    return std::min(nb, need);
 }
 
 int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
@@ -1545,15 +1721,26 @@ int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
 }
 
 // the f32-filtered full sweep: 8 destinations per wave, exact rows settled 2 at a time
-hipError_t launch_dense_f(const shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
-                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
+template <int TB>
+hipError_t launch_dense_ft(const shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
+                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
     constexpr int TDT = 8, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
-    const int64_t nblocks = (int64_t)8 * ntb * ((nbg + 7) / 8);
-    hipLaunchKernelGGL((k_relax_dense_f<TDT, XR>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32, eng->d_W,
+    const int32_t ngroups = (nbg + TB - 1) / TB;
+    const int64_t nblocks = (int64_t)8 * ntb * ((ngroups + 7) / 8);
+    hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32, eng->d_W,
                        eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
                        cnt_cur, eng->d_prof);
     return hipGetLastError();
+}
+
+hipError_t launch_dense_f(const shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
+                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
+    switch (eng->opt_dense_tb) {
+        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
+        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
+        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
+    }
 }
 
 // relax rounds for the batch slots [0, nbg) until no vertex changes
@@ -1629,9 +1816,13 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur);
                 eng->st.delta_sweeps++;
             }
-        } else {
+        } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FULL) {
             hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
                                g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
+                               eng->d_prof);
+        } else {
+            hipLaunchKernelGGL(k_relax_delta, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                               g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
                                eng->d_prof);
         }
         HIP_TRY(hipGetLastError());
@@ -1679,7 +1870,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const bool complete = (eng->flags & SHADOWTOPO_F_COMPLETE) != 0;
     int rc;
     if ((rc = ensure_self(eng, s))) return rc;
-    const int32_t nb = default_nb(eng);
+    const int32_t nb = default_nb(eng, row_end - row_begin);
     if ((rc = ensure_batches(eng, nb))) return rc;
     const int32_t group = nb * KL;
     // device destinations (user buffers or staging)
@@ -2101,7 +2292,7 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
     if (!eng) return fail(SHADOWTOPO_EINVAL, "NULL engine");
     switch (key) {
         case SHADOWTOPO_OPT_BATCHES_IN_FLIGHT:
-            if (value < 0 || value > 64) return fail(SHADOWTOPO_EINVAL, "batches in flight out of range");
+            if (value < 0 || value > 1024) return fail(SHADOWTOPO_EINVAL, "batches in flight out of range");
             eng->opt_nb = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_TIMING:
@@ -2120,6 +2311,16 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value != SHADOWTOPO_DENSE_F32 && value != SHADOWTOPO_DENSE_F64)
                 return fail(SHADOWTOPO_EINVAL, "unknown dense variant %lld", (long long)value);
             eng->opt_dense_variant = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE:
+            if (value != 1 && value != 2 && value != 4)
+                return fail(SHADOWTOPO_EINVAL, "dense batches per wave must be 1, 2 or 4");
+            eng->opt_dense_tb = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_CSR_VARIANT:
+            if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL)
+                return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
+            eng->opt_csr_variant = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_PERMILLE:
             if (value < 0 || value > 1000) return fail(SHADOWTOPO_EINVAL, "delta per mille must be in [0, 1000]");

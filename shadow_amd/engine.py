@@ -36,6 +36,10 @@ OPT_DENSE_VARIANT = 6
 DENSE_F32 = 0  # f32-filtered full sweep + lane-per-pair delta rounds (default)
 DENSE_F64 = 1  # f64 row-stream kernels (cross-check)
 OPT_DELTA_PERMILLE = 7
+OPT_CSR_VARIANT = 8
+OPT_DENSE_BATCHES_PER_WAVE = 9
+CSR_DELTA = 0  # fold changed in-neighbours into the recorded state (cross-check)
+CSR_FULL = 1  # recompute every active vertex over all in-arcs (default)
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (

@@ -1,0 +1,74 @@
+"""CSR relaxation variants (k_relax_delta, the default, and k_relax) against the oracle and
+against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops, kind and
+reliability; the delta rounds and the full recomputation must reach the same fixed point."""
+import numpy as np
+import pytest
+
+from paritylib import compare
+from shadow_amd import engine as E
+from shadow_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(case):
+    if case == "sparse":
+        return synth.random_sparse(V=400, avg_deg=5, seed=31)
+    if case == "directed":
+        return synth.random_sparse(V=300, avg_deg=4, seed=32, directed=True)
+    if case == "ties":
+        return synth.integer_grid(rows=12, cols=12, seed=5)
+    if case == "int_random":
+        return synth.random_sparse(V=300, avg_deg=5, seed=33, int_lat=True)
+    if case == "vloss_prefer":
+        rng = np.random.default_rng(7)
+        g = synth.random_sparse(V=250, avg_deg=6, seed=34, vloss=np.where(rng.random(250) < 0.5, 0.02, np.nan))
+        g.prefer_direct = True
+        return g
+    if case == "no_loops":
+        return synth.random_sparse(V=250, avg_deg=3, seed=36, loops=False)
+    g = synth.random_sparse(V=150, avg_deg=4, seed=35)  # multigraph: parallel edges
+    rng = np.random.default_rng(3)
+    pick = rng.choice(np.nonzero(g.src != g.dst)[0], 40, replace=False)
+    g.src = np.concatenate([g.src, g.dst[pick]])
+    g.dst = np.concatenate([g.dst, g.src[pick]])
+    g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.3, 1.7, 40)])
+    g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 40)])
+    return g
+
+
+CASES = ["sparse", "directed", "ties", "int_random", "vloss_prefer", "no_loops", "multigraph"]
+
+
+@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL])
+@pytest.mark.parametrize("case", CASES)
+def test_csr_variants(case, variant):
+    g = _case(case)
+    st = compare(g, layout="csr", csr_variant=variant)
+    assert st["dense"] == 0
+
+
+def test_csr_delta_several_groups():
+    g = synth.random_sparse(V=500, avg_deg=4, seed=37)
+    compare(g, layout="csr", batches_in_flight=3)  # 500 sources -> 8 batches -> 3 groups
+
+
+@pytest.mark.parametrize("case", ["ties", "sparse", "int_random", "directed"])
+def test_csr_delta_same_fixed_point(case):
+    """Distances bit-exact, tie flags identical, predecessor and hops identical wherever no
+    heap-order tie is involved."""
+    g = _case(case)
+    srcs = np.arange(0, g.n, 2, dtype=np.int32)
+    outs = []
+    for variant in (E.CSR_FULL, E.CSR_DELTA):
+        eng = E.Engine.from_synth(g, layout="csr")
+        eng.set_option(E.OPT_CSR_VARIANT, variant)
+        outs.append(eng.sssp(srcs))
+        eng.close()
+    (d0, p0, h0, t0), (d1, p1, h1, t1) = outs
+    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+    assert np.array_equal(t0, t1)
+    ok = t0 == 0
+    assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
+    if case in ("ties", "int_random"):
+        assert (t0 != 0).any()
