@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
+    ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
+                    "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--csr-variant", type=int, default=1, help="1 = full recomputation (default), 0 = delta rounds")
     args = ap.parse_args()
@@ -144,23 +146,33 @@ def main():
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0
-    # every rank contributes `per` rows to the all-gather (last rank's tail is padding)
-    lat = torch.zeros((per, A), dtype=torch.float64, device=dev)
-    rel = torch.zeros((per, A), dtype=torch.float64, device=dev)
-    hops = torch.zeros((per, A), dtype=torch.int32, device=dev)
-    if world > 1:
-        full_lat = torch.empty((per * world, A), dtype=torch.float64, device=dev)
-        full_rel = torch.empty((per * world, A), dtype=torch.float64, device=dev)
-        full_hops = torch.empty((per * world, A), dtype=torch.int32, device=dev)
+    # The rank's `per` rows (the last rank's tail is padding, so every rank contributes the
+    # same bytes) are computed in `chunks` row chunks; each chunk's lat/rel/hops rows live in
+    # ONE packed byte buffer [lat f64 | rel f64 | hops i32], so one RCCL all-gather per chunk
+    # moves all three, and chunk c's all-gather (RCCL's own stream, xGMI) overlaps the
+    # computation of chunk c+1 on the engine's stream.  Every rank ends with the full matrix
+    # in the layout [chunk][rank][lat | rel | hops][chunk rows][A] (shard.pack_views).
+    # (measured at N=1: 2 chunks cost +0.9 ms of per-chunk overhead, so overlap pays only
+    # where the exchange is long: 8 ranks move ~1.1 GB into every GPU per step)
+    chunks = args.chunks or (2 if world >= 8 else 1)
+    bounds = shard.chunk_rows(per, chunks)
+    packs = [torch.zeros(shard.packed_bytes(n, A), dtype=torch.uint8, device=dev) for _, n in bounds]
+    views = [shard.pack_views(b, n, A) for b, (_, n) in zip(packs, bounds)]
+    gathered = ([torch.empty(world * p.numel(), dtype=torch.uint8, device=dev) for p in packs]
+                if world > 1 else None)
 
     def step():
         stream = torch.cuda.current_stream(dev).cuda_stream
-        if rows > 0:
-            eng.compute_rows_device(r0, r1, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
-        if world > 1:  # RCCL all-gather over xGMI: every rank ends with the full matrix
-            dist.all_gather_into_tensor(full_lat, lat)
-            dist.all_gather_into_tensor(full_rel, rel)
-            dist.all_gather_into_tensor(full_hops, hops)
+        works = []
+        for c, (c0, n) in enumerate(bounds):
+            a, z = r0 + c0, min(r1, r0 + c0 + n)  # this chunk's real rows
+            if z > a:
+                lat, rel, hops = views[c]
+                eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
+            if world > 1:  # returns after the chunk is computed; the gather runs behind the next chunk
+                works.append(dist.all_gather_into_tensor(gathered[c], packs[c], async_op=True))
+        for w in works:
+            w.wait()
 
     for _ in range(args.warmup):
         step()
@@ -243,7 +255,7 @@ def main():
             "data": "synthetic (SURVEY.md 8d generator, fixed seeds)",
             "config": {"workload": desc, "n_vertices": g.n, "n_edges": g.m, "n_arcs": st["n_arcs"],
                        "attached": A, "sources_per_gpu": rows, "matrix_build_ms": ms_per_step,
-                       "parallelism": f"sources sharded x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+                       "parallelism": f"sources sharded x{world}" + (f" + RCCL all-gather ({chunks} chunks, overlapped)" if world > 1 else "")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "engine": {"rounds_per_step": st["rounds"] / args.steps, "replayed_sources": st["replayed_sources"],

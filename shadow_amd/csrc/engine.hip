@@ -167,6 +167,19 @@ constexpr int CSR_PAD = 8;  // in_src / in_w carry 8 padding arcs (u = 0, w = +i
 __device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000000000000LL); }
 __device__ __forceinline__ double dmax() { return __longlong_as_double(0x7fefffffffffffffLL); }
 
+// Block -> (group, tile) with every XCD busy whatever the group count: the grid has
+// 8 * S blocks, S = ceil(groups * tiles / 8), and XCD x (blockIdx % 8) takes the contiguous
+// range [x*S, (x+1)*S) of the group-major (group, tile) order -- so a group's tiles share
+// one XCD (its [V][64] state stays in that L2) when there are >= 8 groups, and a group is
+// spread over several XCDs when there are fewer.  Placement is a speed hint only.
+__device__ __forceinline__ bool xcd_tile(int32_t L, int32_t ngroups, int32_t ntiles, int32_t& grp, int32_t& tile) {
+    const int64_t S = ((int64_t)ngroups * ntiles + 7) / 8;
+    const int64_t i = (int64_t)(L & 7) * S + (L >> 3);
+    grp = (int32_t)(i / ntiles);
+    tile = (int32_t)(i - (int64_t)grp * ntiles);
+    return grp < ngroups;
+}
+
 // f32 filter key of a distance: rounded toward -inf, NaN when unreached (see k_relax_dense_f)
 __device__ __forceinline__ float f32_key(double d) {
     return d < dinf() ? __double2float_rd(d) : __int_as_float(0x7fc00000);
@@ -306,13 +319,10 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
                                                const int32_t* __restrict__ out_dst, Pools pools,
                                                int32_t V, int32_t nb, int32_t nvb, int32_t parity,
                                                int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
-    const int32_t L = blockIdx.x;
-    const int32_t xcd = L & 7;
-    const int32_t q = L >> 3;
-    const int32_t b = xcd + 8 * (q / nvb);
-    if (b >= nb) return;
+    int32_t b, vt;
+    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int32_t v = (q % nvb) * 4 + wave;
+    const int32_t v = vt * 4 + wave;
     if (v >= V) return;
     const int lane = threadIdx.x & 63;
     const BatchDev B = batch_view(pools, b);
@@ -356,9 +366,9 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
         if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
-        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7)) + 1], 1ull);
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
     }
-    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7))], 1ull);
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
 }
 
 // CSR delta round (default for sparse graphs).  Same pull schedule as k_relax (one wave per
@@ -377,13 +387,10 @@ __global__ __launch_bounds__(256) void k_relax_delta(const int64_t* __restrict__
                                                      const int32_t* __restrict__ out_dst, Pools pools, int32_t V,
                                                      int32_t nb, int32_t nvb, int32_t parity, int32_t* __restrict__ cnt,
                                                      unsigned long long* __restrict__ prof) {
-    const int32_t L = blockIdx.x;
-    const int32_t xcd = L & 7;
-    const int32_t q = L >> 3;
-    const int32_t b = xcd + 8 * (q / nvb);
-    if (b >= nb) return;
+    int32_t b, vt;
+    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int32_t v = (q % nvb) * 4 + wave;
+    const int32_t v = vt * 4 + wave;
     if (v >= V) return;
     const int lane = threadIdx.x & 63;
     const BatchDev B = batch_view(pools, b);
@@ -485,9 +492,9 @@ __global__ __launch_bounds__(256) void k_relax_delta(const int64_t* __restrict__
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
         if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
-        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7)) + 1], 1ull);
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
     }
-    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (L & 7))], 1ull);
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
 }
 
 // Lexicographic (candidate, d(u)) minimum with heap-order tie detection, branch-free so the
@@ -566,14 +573,11 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
                                                      int32_t ntb, int32_t parity, int32_t thresh,
                                                      const int32_t* __restrict__ cnt_prev,
                                                      int32_t* __restrict__ cnt) {
-    const int32_t L = blockIdx.x;
-    const int32_t xcd = L & 7;
-    const int32_t q = L >> 3;
-    const int32_t b = xcd + 8 * (q / ntb);
-    if (b >= nb) return;
+    int32_t b, vt;
+    if (!xcd_tile(blockIdx.x, nb, ntb, b, vt)) return;
     if (cnt_prev[b] <= thresh) return;  // converged (0) or left to the delta round
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int32_t v0 = ((q % ntb) * 4 + wave) * DT;
+    const int32_t v0 = (vt * 4 + wave) * DT;
     if (v0 >= V) return;
     const int lane = threadIdx.x & 63;
     const BatchDev B = batch_view(pools, b);
@@ -662,11 +666,9 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
     __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
-    const int32_t L = blockIdx.x;
-    const int32_t xcd = L & 7;
-    const int32_t q = L >> 3;
-    const int32_t b0 = (xcd + 8 * (q / ntb)) * TB;  // this block's TB batches
-    if (b0 >= nb) return;                           // block-uniform exits only (barriers below)
+    int32_t grp, vt;
+    if (!xcd_tile(blockIdx.x, (nb + TB - 1) / TB, ntb, grp, vt)) return;  // block-uniform exits only (barriers below)
+    const int32_t b0 = grp * TB;  // this block's TB batches
     bool live[TB];
     int32_t first = -1;
 #pragma unroll
@@ -675,7 +677,7 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         if (live[k] && first < 0) first = b0 + k;
     }
     if (first < 0) return;
-    const int32_t vb = (q % ntb) * BW;
+    const int32_t vb = vt * BW;
     if (vb >= V) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -1727,7 +1729,7 @@ hipError_t launch_dense_ft(const shadowtopo_engine* eng, int32_t nbg, int32_t pa
     constexpr int TDT = 8, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
-    const int64_t nblocks = (int64_t)8 * ntb * ((ngroups + 7) / 8);
+    const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32, eng->d_W,
                        eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
                        cnt_cur, eng->d_prof);
@@ -1755,9 +1757,9 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         HIP_TRY(hipGetLastError());
     }
     const int32_t nvb = (V + 3) / 4;
-    const int64_t nblocks = (int64_t)8 * nvb * ((nbg + 7) / 8);
+    const int64_t nblocks = 8 * (((int64_t)nbg * nvb + 7) / 8);
     const int32_t ntb = (V + 4 * DT - 1) / (4 * DT);
-    const int64_t nblocks_dense = (int64_t)8 * ntb * ((nbg + 7) / 8);
+    const int64_t nblocks_dense = 8 * (((int64_t)nbg * ntb + 7) / 8);
     if (nblocks > 0x7fffffff) return fail(SHADOWTOPO_EINVAL, "grid too large");
     const int64_t max_rounds = eng->opt_max_rounds > 0 ? eng->opt_max_rounds : 4LL * V + 64;
     eng->d_prof = eng->opt_profile ? eng->prof_buf : nullptr;

@@ -22,6 +22,40 @@ def shard_rows(A: int, world: int, rank: int):
     return r0, r1, per
 
 
+def chunk_rows(per: int, chunks: int):
+    """[(offset, rows)] splitting a rank's `per` rows into `chunks` pieces of whole 64-source
+    batches (the last may be short); the same split on every rank, so chunk c's buffers have
+    one size everywhere (all-gather needs equal contributions)"""
+    chunks = max(1, chunks)
+    n = max(64, -(-per // chunks // 64) * 64) if per else 0
+    out, o = [], 0
+    while o < per:
+        out.append((o, min(n, per - o)))
+        o += n
+    return out or [(0, 0)]
+
+
+def packed_bytes(rows: int, A: int) -> int:
+    """one chunk's lat (f64) + rel (f64) + hops (i32) rows in one buffer"""
+    return rows * A * 20
+
+
+def pack_views(buf, rows: int, A: int):
+    """(lat, rel, hops) views [rows, A] into a packed uint8 buffer of packed_bytes(rows, A)"""
+    import torch
+    n = rows * A
+    lat = buf[: 8 * n].view(torch.float64).view(rows, A)
+    rel = buf[8 * n: 16 * n].view(torch.float64).view(rows, A)
+    hops = buf[16 * n: 20 * n].view(torch.int32).view(rows, A)
+    return lat, rel, hops
+
+
+def unpack_gathered(gathered, world: int, rows: int, A: int):
+    """the all-gathered packed buffer of one chunk -> per-rank (lat, rel, hops) views"""
+    per_rank = packed_bytes(rows, A)
+    return [pack_views(gathered[r * per_rank:(r + 1) * per_rank], rows, A) for r in range(world)]
+
+
 def gather_rows(dist, local, per, world):
     """all_gather of a [per, A] row block -> [world*per, A] (torch tensors, same device)"""
     import torch

@@ -75,3 +75,67 @@ def test_two_rank_gloo_assembly(A_sel):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert q.get(timeout=10) == (True, True, True)
+
+
+def _worker_packed(rank, world, port, A_sel, chunks, q):
+    """bench.py's exchange: packed [lat | rel | hops] chunk buffers, one all-gather each"""
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from shadow_amd import synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = synth.random_sparse(V=150, avg_deg=4, seed=78, A=A_sel)
+    og = O.OracleGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss)
+    flags = og.flags()
+    A = len(g.attached)
+    r0, r1, per = shard.shard_rows(A, world, rank)
+    bounds = shard.chunk_rows(per, chunks)
+    full = og.pair_rows(flags, g.attached)
+    ok = True
+    for c0, n in bounds:
+        buf = torch.zeros(shard.packed_bytes(n, A), dtype=torch.uint8)
+        lat, rel, hops = shard.pack_views(buf, n, A)
+        a, z = r0 + c0, min(r1, r0 + c0 + n)
+        if z > a:
+            l, r, h, _, _ = og.pair_rows(flags, g.attached, a, z)
+            lat[:z - a] = torch.from_numpy(l)
+            rel[:z - a] = torch.from_numpy(r)
+            hops[:z - a] = torch.from_numpy(h.astype(np.int32))
+        gathered = torch.empty(world * buf.numel(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(gathered, buf)
+        for rr, (gl, gr, gh) in enumerate(shard.unpack_gathered(gathered, world, n, A)):
+            s0, s1, _ = shard.shard_rows(A, world, rr)
+            a, z = s0 + c0, min(s1, s0 + c0 + n)
+            if z > a:
+                ok &= np.array_equal(gl[:z - a].numpy().view(np.uint64), full[0][a:z].view(np.uint64))
+                ok &= np.array_equal(gr[:z - a].numpy().view(np.uint64), full[1][a:z].view(np.uint64))
+                ok &= np.array_equal(gh[:z - a].numpy(), full[2][a:z].astype(np.int32))
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("A_sel,chunks", [(150, 2), (131, 3)])
+def test_two_rank_packed_chunked_exchange(A_sel, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_packed, args=(r, 2, port, A_sel, chunks, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert res == [(0, True), (1, True)]
+
+
+def test_chunk_rows_cover_exactly():
+    for per in (0, 1, 63, 64, 500, 1000, 1001):
+        for chunks in (1, 2, 3, 4, 8):
+            b = shard.chunk_rows(per, chunks)
+            assert sum(n for _, n in b) == per
+            assert all(o % 64 == 0 for o, _ in b)
+            assert [o for o, _ in b] == sorted(o for o, _ in b)
