@@ -29,10 +29,14 @@ typedef struct topology_hip_info {
     double min_path_latency;  /* value handed to worker_updateMinTimeJump */
     double compute_seconds;   /* wall time of the eager attached-pair computation */
     int64_t compute_count;    /* sources computed ("shortest paths with dijkstra") */
+    int32_t n_devices;        /* GPUs the attached-pair rows are sharded over */
 } topology_hip_info;
 
 /* HIP device the engine uses (default: $SHADOWTOPO_DEVICE or 0); before the first query */
 int topology_hip_set_device(Topology* top, int32_t device);
+/* shard the attached-pair rows over several devices (one engine and one host thread per
+ * entry; default: $SHADOWTOPO_DEVICES, e.g. "0,1,2,3,4,5,6,7"); before the first query */
+int topology_hip_set_devices(Topology* top, const int32_t* devices, int32_t count);
 /* alternative self-pair rule (see shadowtopo.h SHADOWTOPO_F_SELF_DIJKSTRA_LOOP) */
 int topology_hip_set_self_rule(Topology* top, int32_t dijkstra_loop);
 /* run the eager computation now instead of on the first query; 0 on success */

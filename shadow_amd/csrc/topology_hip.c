@@ -45,6 +45,7 @@ extern double random_nextDouble(Random* random);
 extern void worker_updateMinTimeJump(double minPathLatency);
 
 #define TOPO_MAGIC 0x70B01060u
+#define SHADOWTOPO_MAX_DEVICES 64
 
 /* ------------------------------------------------------------ IP -> vertex table */
 typedef struct {
@@ -163,8 +164,13 @@ struct _Topology {
     _Atomic(matrix*) mat;
     matrix* retired;
     pthread_mutex_t cnt_lock;
-    shadowtopo_engine* eng;
+    shadowtopo_engine* eng;  /* engine on devices[0] */
     int32_t device;
+    /* in-process multi-GPU: one engine per device, each computing a
+     * contiguous block of source rows straight into the host matrix */
+    int32_t ndev;
+    int32_t devices[SHADOWTOPO_MAX_DEVICES];
+    shadowtopo_engine* engs[SHADOWTOPO_MAX_DEVICES];
     int self_rule;
     double min_latency;
     double compute_s;
@@ -632,7 +638,9 @@ void topology_free(Topology* top) {
         free_matrix(r);
         r = n;
     }
-    if (top->eng) shadowtopo_destroy(top->eng);
+    for (int32_t k = 0; k < top->ndev; k++)
+        if (top->engs[k]) shadowtopo_destroy(top->engs[k]);
+    top->eng = NULL;
     free(top->ips.keys);
     free(top->ips.vals);
     free(top->ips.state);
@@ -659,6 +667,24 @@ Topology* topology_new(const char* graphPath) {
     pthread_mutex_init(&top->cnt_lock, NULL);
     const char* dev = getenv("SHADOWTOPO_DEVICE");
     top->device = dev ? atoi(dev) : 0;
+    top->ndev = 1;
+    top->devices[0] = top->device;
+    /* SHADOWTOPO_DEVICES: comma-separated device list, e.g. "0,1,2,3,4,5,6,7" */
+    const char* devs = getenv("SHADOWTOPO_DEVICES");
+    if (devs && *devs) {
+        int32_t n = 0;
+        for (const char* c = devs; *c && n < SHADOWTOPO_MAX_DEVICES;) {
+            char* end = NULL;
+            long d = strtol(c, &end, 10);
+            if (end == c) break;
+            top->devices[n++] = (int32_t)d;
+            c = (*end == ',') ? end + 1 : end;
+        }
+        if (n > 0) {
+            top->ndev = n;
+            top->device = top->devices[0];
+        }
+    }
     atomic_store(&top->mat, NULL);
 
     char err[512] = {0};
@@ -886,24 +912,49 @@ static int ensure_engine(Topology* top) {
     if (top->complete) flags |= SHADOWTOPO_F_COMPLETE;
     if (top->prefer_direct) flags |= SHADOWTOPO_F_PREFER_DIRECT;
     if (top->self_rule) flags |= SHADOWTOPO_F_SELF_DIJKSTRA_LOOP;
-    int rc = shadowtopo_create(top->V, top->E, top->gml->src, top->gml->dst, top->elat, top->eloss, top->vloss, flags,
-                               top->device, &top->eng);
-    if (rc != SHADOWTOPO_OK) {
-        st_critical("GPU topology engine unavailable (%d): %s", rc, shadowtopo_last_error());
-        top->eng = NULL;
-        return -1;
+    for (int32_t k = 0; k < top->ndev; k++) {
+        int rc = shadowtopo_create(top->V, top->E, top->gml->src, top->gml->dst, top->elat, top->eloss, top->vloss,
+                                   flags, top->devices[k], &top->engs[k]);
+        if (rc != SHADOWTOPO_OK) {
+            st_critical("GPU topology engine unavailable on device %d (%d): %s", (int)top->devices[k], rc,
+                        shadowtopo_last_error());
+            for (int32_t j = 0; j <= k; j++) {
+                if (top->engs[j]) shadowtopo_destroy(top->engs[j]);
+                top->engs[j] = NULL;
+            }
+            return -1;
+        }
     }
+    top->eng = top->engs[0];
     return 0;
+}
+
+/* one device's share of the attached-pair matrix: rows [r0, r1) written in place */
+typedef struct {
+    shadowtopo_engine* eng;
+    const int32_t* attached;
+    int32_t A, r0, r1;
+    matrix* m;
+    int rc;
+    char err[256];
+} row_block;
+
+static void* compute_block(void* arg) {
+    row_block* w = arg;
+    w->rc = shadowtopo_set_attached(w->eng, w->attached, w->A);
+    if (w->rc == SHADOWTOPO_OK && w->r1 > w->r0) {
+        size_t o = (size_t)w->r0 * (size_t)w->A;
+        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->m->lat + o, w->m->rel + o, w->m->hops + o,
+                                        w->m->kind + o, SHADOWTOPO_MEM_HOST, NULL);
+    }
+    if (w->rc != SHADOWTOPO_OK) snprintf(w->err, sizeof w->err, "%s", shadowtopo_last_error());
+    return NULL;
 }
 
 static matrix* compute_matrix(Topology* top, int32_t A) {
     if (ensure_engine(top)) return NULL;
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
-    if (shadowtopo_set_attached(top->eng, top->attached, A) != SHADOWTOPO_OK) {
-        st_critical("shadowtopo_set_attached: %s", shadowtopo_last_error());
-        return NULL;
-    }
     matrix* m = calloc(1, sizeof(matrix));
     size_t n = (size_t)A * (size_t)A;
     m->A = A;
@@ -917,11 +968,39 @@ static matrix* compute_matrix(Topology* top, int32_t A) {
         free_matrix(m);
         return NULL;
     }
-    int rc = shadowtopo_compute_rows(top->eng, 0, A, m->lat, m->rel, m->hops, m->kind, SHADOWTOPO_MEM_HOST, NULL);
-    if (rc != SHADOWTOPO_OK) {
-        st_critical("attached-pair computation failed (%d): %s", rc, shadowtopo_last_error());
-        free_matrix(m);
-        return NULL;
+    /* sources shard naturally: device k computes the contiguous row block
+     * k of ceil(A / ndev) rows against all A targets, on its own thread, straight into the
+     * host matrix; no exchange between devices is needed in one process */
+    int32_t nd = top->ndev;
+    row_block blocks[SHADOWTOPO_MAX_DEVICES];
+    pthread_t th[SHADOWTOPO_MAX_DEVICES];
+    int32_t per = (A + nd - 1) / nd;
+    for (int32_t k = 0; k < nd; k++) {
+        blocks[k].eng = top->engs[k];
+        blocks[k].attached = top->attached;
+        blocks[k].A = A;
+        blocks[k].r0 = k * per < A ? k * per : A;
+        blocks[k].r1 = (k + 1) * per < A ? (k + 1) * per : A;
+        blocks[k].m = m;
+        blocks[k].rc = 0;
+        blocks[k].err[0] = 0;
+    }
+    int spawned[SHADOWTOPO_MAX_DEVICES] = {0};
+    for (int32_t k = 1; k < nd; k++) spawned[k] = pthread_create(&th[k], NULL, compute_block, &blocks[k]) == 0;
+    compute_block(&blocks[0]);
+    for (int32_t k = 1; k < nd; k++) {
+        if (spawned[k])
+            pthread_join(th[k], NULL);
+        else
+            compute_block(&blocks[k]);
+    }
+    for (int32_t k = 0; k < nd; k++) {
+        if (blocks[k].rc != SHADOWTOPO_OK) {
+            st_critical("attached-pair computation failed on device %d (%d): %s", (int)top->devices[k],
+                        blocks[k].rc, blocks[k].err);
+            free_matrix(m);
+            return NULL;
+        }
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
@@ -936,8 +1015,8 @@ static matrix* compute_matrix(Topology* top, int32_t A) {
         top->min_latency = mn;
         worker_updateMinTimeJump(top->min_latency);
     }
-    st_info("computed %d x %d attached-pair matrix on device %d in %f seconds", A, A, top->device,
-            top->compute_s);
+    st_info("computed %d x %d attached-pair matrix on %d device(s) (first %d) in %f seconds", A, A, (int)nd,
+            (int)top->device, top->compute_s);
     return m;
 }
 
@@ -1068,6 +1147,16 @@ void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Add
 int topology_hip_set_device(Topology* top, int32_t device) {
     if (!top || top->eng) return -1;
     top->device = device;
+    top->ndev = 1;
+    top->devices[0] = device;
+    return 0;
+}
+
+int topology_hip_set_devices(Topology* top, const int32_t* devices, int32_t count) {
+    if (!top || top->eng || !devices || count < 1 || count > SHADOWTOPO_MAX_DEVICES) return -1;
+    for (int32_t k = 0; k < count; k++) top->devices[k] = devices[k];
+    top->ndev = count;
+    top->device = devices[0];
     return 0;
 }
 
@@ -1097,6 +1186,7 @@ int topology_hip_get_info(Topology* top, topology_hip_info* out) {
     matrix* m = atomic_load(&top->mat);
     out->computed_for = m ? m->A : 0;
     out->device = top->device;
+    out->n_devices = top->ndev;
     out->min_path_latency = top->min_latency;
     out->compute_seconds = top->compute_s;
     out->compute_count = top->compute_count;

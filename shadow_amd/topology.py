@@ -21,7 +21,7 @@ TOPOLOGY_SYMBOLS = (
     "topology_getLatency", "topology_getReliability", "topology_incrementPathPacketCounter",
 )
 EXT_SYMBOLS = (
-    "topology_hip_set_device", "topology_hip_set_self_rule", "topology_hip_prepare", "topology_hip_get_info",
+    "topology_hip_set_device", "topology_hip_set_devices", "topology_hip_set_self_rule", "topology_hip_prepare", "topology_hip_get_info",
     "topology_hip_attached", "topology_hip_vertex_of_ip", "topology_hip_vertex_of_id", "topology_hip_packet_count",
     "topology_hip_edges", "shadowtopo_address_new", "shadowtopo_address_free", "shadowtopo_random_new",
     "shadowtopo_random_free", "shadowtopo_last_min_time_jump", "shadowtopo_set_log_level",
@@ -34,7 +34,7 @@ class Info(ctypes.Structure):
         ("is_complete", ctypes.c_int32), ("is_connected", ctypes.c_int32), ("cluster_count", ctypes.c_int32),
         ("prefers_direct_paths", ctypes.c_int32), ("n_attached", ctypes.c_int32), ("computed_for", ctypes.c_int32),
         ("device", ctypes.c_int32), ("min_path_latency", ctypes.c_double), ("compute_seconds", ctypes.c_double),
-        ("compute_count", ctypes.c_int64),
+        ("compute_count", ctypes.c_int64), ("n_devices", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -64,6 +64,7 @@ def lib():
         L.topology_getReliability.argtypes = [vp, vp, vp]
         L.topology_incrementPathPacketCounter.argtypes = [vp, vp, vp]
         L.topology_hip_set_device.argtypes = [vp, ctypes.c_int32]
+        L.topology_hip_set_devices.argtypes = [vp, vp, ctypes.c_int32]
         L.topology_hip_set_self_rule.argtypes = [vp, ctypes.c_int32]
         L.topology_hip_prepare.argtypes = [vp]
         L.topology_hip_get_info.argtypes = [vp, ctypes.POINTER(Info)]
@@ -177,6 +178,10 @@ class Topology:
     # ---- extensions (topology_hip_ext.h)
     def set_device(self, device: int):
         return lib().topology_hip_set_device(self._h, device)
+
+    def set_devices(self, devices):
+        arr = np.ascontiguousarray(devices, np.int32)
+        return lib().topology_hip_set_devices(self._h, arr.ctypes.data_as(ctypes.c_void_p), len(arr))
 
     def set_self_rule(self, dijkstra_loop: bool):
         return lib().topology_hip_set_self_rule(self._h, int(dijkstra_loop))

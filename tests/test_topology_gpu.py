@@ -146,3 +146,22 @@ def test_late_attach_recomputes(tmp_path):
     assert top.info()["computed_for"] == 12
     assert top.getLatency(hosts[0], hosts[1]) == l01
     top.free()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_rows_sharded_over_engines(tmp_path, devices):
+    """in-process multi-GPU: one engine per listed device, each computing a
+    contiguous block of source rows on its own thread into the host matrix; the same device
+    listed several times exercises the sharding on a one-GPU box"""
+    g = synth.random_sparse(V=200, avg_deg=4, seed=46, A=70)
+    va, ips = with_vertex_ips(g)
+    top = T.Topology.new(write(tmp_path, "m.xml", synth.to_graphml(g, extra_vattr=va)))
+    assert top.set_devices(devices) == 0
+    hosts = attach_all(top, ips, g.attached)
+    lat_o, rel_o, _, _, _ = oracle_matrix(g)
+    for i in range(0, len(hosts), 3):
+        for j in range(len(hosts)):
+            assert top.getLatency(hosts[i], hosts[j]) == lat_o[i, j]
+            assert top.getReliability(hosts[i], hosts[j]) == rel_o[i, j]
+    assert top.info()["n_devices"] == len(devices)
+    top.free()
