@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-rate", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
     ap.add_argument("--cpu-sources", type=int, default=12)
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
@@ -232,6 +233,14 @@ def main():
                                     "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
                                     "launches_per_step": st["delta_sweeps"] / args.steps}
 
+    # the drop-in boundary hands host buffers over (topology_hip.c: MEM_HOST); its
+    # PCIe-inclusive rate, measured once outside the timed region (never `value`)
+    host_ms = None
+    if rank == 0 and world == 1 and rows > 0 and not args.no_host_rate:
+        h0 = time.perf_counter()
+        eng.compute_rows(r0, r1, want_kind=True)
+        host_ms = (time.perf_counter() - h0) * 1e3
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -263,7 +272,9 @@ def main():
                        "compose_ms_per_step": st["compose_ms"] / args.steps, "dense": st["dense"],
                        "visits_per_step": st["visits"] / args.steps, "changes_per_step": st["changes"] / args.steps,
                        "full_sweeps_per_step": st["full_sweeps"] / args.steps,
-                       "delta_sweeps_per_step": st["delta_sweeps"] / args.steps},
+                       "delta_sweeps_per_step": st["delta_sweeps"] / args.steps,
+                       "host_buffers_ms": host_ms,
+                       "host_buffers_source_paths_per_s": (rows / host_ms * 1e3) if host_ms else None},
         }
         print(json.dumps(out), flush=True)
     eng.close()
