@@ -768,12 +768,21 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
                 const float du = sD[cur][k][r * KL + lane];
-                float g = __int_as_float(0x7fc00000);
+                // max over the TDT slacks thr_t - w_t as a chain of 3-input maxima (v_max3)
+                float x[TDT];
 #pragma unroll
-                for (int j = 0; j < TDT / 4; ++j)
-                    g = fmaxf(g, fmaxf(fmaxf(thr[k][4 * j] - w4[j].x, thr[k][4 * j + 1] - w4[j].y),
-                                       fmaxf(thr[k][4 * j + 2] - w4[j].z, thr[k][4 * j + 3] - w4[j].w)));
-                lhit[k] |= (du <= g) ? (1u << r) : 0u;
+                for (int j = 0; j < TDT / 4; ++j) {
+                    x[4 * j] = thr[k][4 * j] - w4[j].x;
+                    x[4 * j + 1] = thr[k][4 * j + 1] - w4[j].y;
+                    x[4 * j + 2] = thr[k][4 * j + 2] - w4[j].z;
+                    x[4 * j + 3] = thr[k][4 * j + 3] - w4[j].w;
+                }
+                float g = fmaxf(fmaxf(x[0], x[1]), x[2]);
+#pragma unroll
+                for (int t = 3; t + 1 < TDT; t += 2) g = fmaxf(fmaxf(g, x[t]), x[t + 1]);
+                if (TDT % 2 == 0) g = fmaxf(g, x[TDT - 1]);
+                // rows enter the mask LSB-last: lhit = 2*lhit + pass (v_cmp + v_addc)
+                lhit[k] = lhit[k] + lhit[k] + ((du <= g) ? 1u : 0u);
             }
         }
         // exact f64 pass over each batch's flagged rows, in row order, XR rows' loads in
@@ -786,7 +795,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
             uint32_t lh = lhit[k];
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) lh |= (uint32_t)__shfl_xor((int)lh, off);
-            unsigned long long hits = (uint32_t)__builtin_amdgcn_readfirstlane(lh);
+            // bit SRS-1-r = row r (shifted in LSB-last): reverse to bit r = row r
+            unsigned long long hits = __builtin_bitreverse32((uint32_t)__builtin_amdgcn_readfirstlane(lh));
             if (prof && hits && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hits));
             const gdouble* Dl = B[k].D + lane;
             while (hits) {
