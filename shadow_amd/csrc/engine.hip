@@ -661,7 +661,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
                                                        int32_t nb, int32_t ntb, int32_t parity, int32_t thresh,
                                                        const int32_t* __restrict__ cnt_prev,
                                                        int32_t* __restrict__ cnt,
-                                                       unsigned long long* __restrict__ prof) {
+                                                       unsigned long long* __restrict__ prof,
+                                                       uint32_t* __restrict__ hitlog) {
     constexpr int BW = 4 * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
@@ -715,6 +716,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const f4 gf4;
     const int32_t nrows = (V + SRS - 1) / SRS * SRS;  // <= Vp: rows past V are NaN padding
+    const int32_t nchunks = nrows / SRS;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + wave;  // this wave's hit log: [TB][nchunks] row masks
     // chunk fill: TB x D32 rows = SRS*64 floats each (2 float4 per thread), W32 = SRS*BW floats
     constexpr int DQ = SRS * KL / 4 / 256;       // float4 of one batch's D32 chunk per thread
     constexpr int WQT = (SRS * WQ + 255) / 256;  // float4 of W32 per thread
@@ -754,11 +757,14 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         const int cur = (u0 / SRS) & 1;
         const bool more = u0 + SRS < nrows;
         if (more) fetch(u0 + SRS);
-        // per lane and batch: bit r = row u0 + r passed the filter (no per-row wave vote);
-        // one broadcast read of the row's TDT weights serves all TB batches
-        uint32_t lhit[TB];
+        // per batch: bit r = row u0 + r passed the filter in some lane.  One broadcast read
+        // of the row's TDT weights serves all TB batches.  A passing row tightens the
+        // thresholds at once with an f32 upper bound of its candidates -- the exact f64 work
+        // is deferred to after the sweep, so no wave ever waits on a global load inside the
+        // chunk loop (that wait would hold the whole block at the next barrier).
+        uint32_t hits[TB];
 #pragma unroll
-        for (int k = 0; k < TB; ++k) lhit[k] = 0;
+        for (int k = 0; k < TB; ++k) hits[k] = 0;
 #pragma unroll 2
         for (int r = 0; r < SRS; ++r) {
             const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
@@ -768,74 +774,100 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
                 const float du = sD[cur][k][r * KL + lane];
-                // max over the TDT slacks thr_t - w_t as a chain of 3-input maxima (v_max3)
+                // slacks thr_t - w_t two at a time (v_pk_add_f32), their max as a chain of
+                // 3-input maxima (v_max3)
+                typedef float f2 __attribute__((ext_vector_type(2)));
                 float x[TDT];
 #pragma unroll
                 for (int j = 0; j < TDT / 4; ++j) {
-                    x[4 * j] = thr[k][4 * j] - w4[j].x;
-                    x[4 * j + 1] = thr[k][4 * j + 1] - w4[j].y;
-                    x[4 * j + 2] = thr[k][4 * j + 2] - w4[j].z;
-                    x[4 * j + 3] = thr[k][4 * j + 3] - w4[j].w;
+                    const f2 a = f2{thr[k][4 * j], thr[k][4 * j + 1]} - f2{w4[j].x, w4[j].y};
+                    const f2 c = f2{thr[k][4 * j + 2], thr[k][4 * j + 3]} - f2{w4[j].z, w4[j].w};
+                    x[4 * j] = a.x;
+                    x[4 * j + 1] = a.y;
+                    x[4 * j + 2] = c.x;
+                    x[4 * j + 3] = c.y;
                 }
                 float g = fmaxf(fmaxf(x[0], x[1]), x[2]);
 #pragma unroll
                 for (int t = 3; t + 1 < TDT; t += 2) g = fmaxf(fmaxf(g, x[t]), x[t + 1]);
                 if (TDT % 2 == 0) g = fmaxf(g, x[TDT - 1]);
-                // rows enter the mask LSB-last: lhit = 2*lhit + pass (v_cmp + v_addc)
-                lhit[k] = lhit[k] + lhit[k] + ((du <= g) ? 1u : 0u);
-            }
-        }
-        // exact f64 pass over each batch's flagged rows, in row order, XR rows' loads in
-        // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
-        // j % TDT, broadcast by readlane).  A source's own row never passes (its D32 is NaN:
-        // the seed candidate is in the lexicographic state already).
+                if (__ballot(du <= g)) {
+                    hits[k] |= 1u << r;
+                    // c_exact <= fl32(D32 + W32) * (1 + 2^-22) <= that + 5 ulps, and f32_thr
+                    // adds 4 ulps: every lane may lower thr_t to bits(c32) + 9 (a no-op where
+                    // the row did not pass)
 #pragma unroll
-        for (int k = 0; k < TB; ++k) {
-            if (!live[k]) continue;
-            uint32_t lh = lhit[k];
+                    for (int j = 0; j < TDT / 4; ++j) {
+                        const float wj[4] = {w4[j].x, w4[j].y, w4[j].z, w4[j].w};
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) lh |= (uint32_t)__shfl_xor((int)lh, off);
-            // bit SRS-1-r = row r (shifted in LSB-last): reverse to bit r = row r
-            unsigned long long hits = __builtin_bitreverse32((uint32_t)__builtin_amdgcn_readfirstlane(lh));
-            if (prof && hits && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hits));
-            const gdouble* Dl = B[k].D + lane;
-            while (hits) {
-                int32_t ur[XR];
-                int nr = 0;
-#pragma unroll
-                for (int x = 0; x < XR; ++x) {
-                    ur[x] = u0;
-                    if (hits) {
-                        ur[x] = u0 + __builtin_ctzll(hits);
-                        hits &= hits - 1;
-                        nr = x + 1;
-                    }
-                }
-                double d64[XR], wl[XR];
-#pragma unroll
-                for (int x = 0; x < XR; ++x) {
-                    d64[x] = Dl[(size_t)ur[x] * KL];
-                    wl[x] = W[(size_t)ur[x] * Vp + v0 + (lane & (TDT - 1))];
-                }
-#pragma unroll
-                for (int x = 0; x < XR; ++x) {
-                    if (x >= nr) break;
-                    const int32_t u = ur[x];
-                    const bool own = (u == sv[k]);
-#pragma unroll
-                    for (int t = 0; t < TDT; ++t) {
-                        const double c = d64[x] + readlane_d(wl[x], t);
-                        if (__ballot((c <= bc[k][t]) & !own)) {
-                            if (!own) lex_update(c, d64[x], u, bc[k][t], bdu[k][t], bu[k][t], tie[k], 1u << t);
-                            const float nt = f32_thr(bc[k][t]);
-                            thr[k][t] = nt < thr[k][t] ? nt : thr[k][t];
+                        for (int i = 0; i < 4; ++i) {
+                            const float c32 = du + wj[i];
+                            if (c32 < __int_as_float(0x7f800000))
+                                thr[k][4 * j + i] = fminf(thr[k][4 * j + i], __int_as_float(__float_as_int(c32) + 9));
                         }
                     }
                 }
             }
         }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + (u0 / SRS)] = hits[k];
+        }
         if (more) stash(cur ^ 1);
         __syncthreads();
+    }
+    // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
+    // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
+    // j % TDT, broadcast by readlane).  A source's own row never passes (its D32 is NaN: the
+    // seed candidate is in the lexicographic state already).
+#pragma unroll
+    for (int k = 0; k < TB; ++k) {
+        if (!live[k]) continue;
+        const uint32_t* hl = hitlog + ((size_t)gw * TB + k) * nchunks;
+        const gdouble* Dl = B[k].D + lane;
+        for (int32_t c0 = 0; c0 < nchunks; c0 += 64) {
+            const uint32_t e = (c0 + lane < nchunks) ? hl[c0 + lane] : 0u;
+            unsigned long long cm = __ballot(e != 0u);
+            while (cm) {
+                const int ci = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                unsigned long long hrows = (uint32_t)__builtin_amdgcn_readlane((int)e, ci);
+                const int32_t u0 = (c0 + ci) * SRS;
+                if (prof && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hrows));
+                while (hrows) {
+                    int32_t ur[XR];
+                    int nr = 0;
+#pragma unroll
+                    for (int x = 0; x < XR; ++x) {
+                        ur[x] = u0;
+                        if (hrows) {
+                            ur[x] = u0 + __builtin_ctzll(hrows);
+                            hrows &= hrows - 1;
+                            nr = x + 1;
+                        }
+                    }
+                    double d64[XR], wl[XR];
+#pragma unroll
+                    for (int x = 0; x < XR; ++x) {
+                        d64[x] = Dl[(size_t)ur[x] * KL];
+                        wl[x] = W[(size_t)ur[x] * Vp + v0 + (lane & (TDT - 1))];
+                    }
+#pragma unroll
+                    for (int x = 0; x < XR; ++x) {
+                        if (x >= nr) break;
+                        const int32_t u = ur[x];
+                        const bool own = (u == sv[k]);
+#pragma unroll
+                        for (int t = 0; t < TDT; ++t) {
+                            const double c = d64[x] + readlane_d(wl[x], t);
+                            if (__ballot((c <= bc[k][t]) & !own)) {
+                                if (!own) lex_update(c, d64[x], u, bc[k][t], bdu[k][t], bu[k][t], tie[k], 1u << t);
+                            }
+                        }
+                    }
+                }
+            }
+        }
     }
     if (v0 < V) {
 #pragma unroll
@@ -1560,6 +1592,8 @@ struct shadowtopo_engine {
     const double* d_W = nullptr;    // dense mode: [Vp][Vp] arc latency, +inf if none
     const int32_t* d_WI = nullptr;  // dense mode: [Vp][Vp] in-arc index, -1 if none
     const float* d_W32 = nullptr;   // dense mode: [Vp][Vp] arc latency rounded down to f32, NaN if none
+    uint32_t* d_hitlog = nullptr;   // dense full sweep: per wave, per batch, per 32-row chunk: rows to settle in f64
+    size_t hitlog_n = 0;
     int64_t E = 0;
     int64_t n_arcs = 0;
     uint32_t flags = 0;
@@ -1734,19 +1768,29 @@ int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
 
 // the f32-filtered full sweep: 8 destinations per wave, exact rows settled 2 at a time
 template <int TB>
-hipError_t launch_dense_ft(const shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
+hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
                            const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
     constexpr int TDT = 8, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
     const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
+    const size_t nchunks = (size_t)((eng->V + SRS - 1) / SRS);
+    const size_t need = (size_t)nblocks * 4 * TB * nchunks;
+    if (eng->hitlog_n < need) {
+        if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
+        eng->d_hitlog = nullptr;
+        eng->hitlog_n = 0;
+        hipError_t e = hipMalloc((void**)&eng->d_hitlog, need * sizeof(uint32_t));
+        if (e != hipSuccess) return e;
+        eng->hitlog_n = need;
+    }
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32, eng->d_W,
                        eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof);
+                       cnt_cur, eng->d_prof, eng->d_hitlog);
     return hipGetLastError();
 }
 
-hipError_t launch_dense_f(const shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
+hipError_t launch_dense_f(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
     switch (eng->opt_dense_tb) {
         case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
@@ -2262,6 +2306,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_self_hops) (void)hipFree(eng->d_self_hops);
     if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
     if (eng->stage) (void)hipFree(eng->stage);
+    if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
     if (eng->ev0) (void)hipEventDestroy(eng->ev0);
     if (eng->ev1) (void)hipEventDestroy(eng->ev1);
     if (eng->evm) (void)hipEventDestroy(eng->evm);
