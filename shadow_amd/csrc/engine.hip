@@ -1907,6 +1907,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         }
         int64_t changed = 0;
         for (int32_t b = 0; b < nbg; ++b) changed += eng->h_cnt[b];
+        if (eng->dense && eng->opt_profile) eng->st.changes += changed;  // changed (vertex, source) pairs
         if (changed == 0) break;
     }
     if (eng->d_prof) {
