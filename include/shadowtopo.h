@@ -68,7 +68,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_TIMING 2            /* 1 = record HIP events around every relax launch */
 #define SHADOWTOPO_OPT_MAX_ROUNDS 3        /* iteration guard (default 4*V+64) */
 #define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
-#define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count (vertex, batch) visits and changes (CSR relax) */
+#define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count visits and changes per round (see shadowtopo_stats) */
 #define SHADOWTOPO_OPT_DENSE_VARIANT 6     /* dense relax kernels: SHADOWTOPO_DENSE_F32 (default) or _F64 */
 /* dense relaxation kernels (both exact; F32 pre-filters every candidate in f32 against a
  * conservative threshold and re-evaluates the survivors in f64, F64 evaluates everything in f64) */
@@ -106,8 +106,9 @@ typedef struct shadowtopo_stats {
     int32_t multigraph;
     int32_t dense;           /* 1 = dense-tile relaxation in use */
     int32_t reserved;
-    int64_t visits;          /* OPT_PROFILE: active (vertex, batch) waves processed */
-    int64_t changes;         /* OPT_PROFILE: (vertex, batch) waves that changed */
+    int64_t visits;          /* OPT_PROFILE, CSR: active (vertex, batch) waves processed */
+    int64_t changes;         /* OPT_PROFILE: CSR: (vertex, batch) waves that changed;
+                                dense: (vertex, source) pairs that changed */
     int64_t full_sweeps;     /* dense: full-sweep relax launches */
     int64_t delta_sweeps;    /* dense: change-mask (delta) relax launches */
     double full_ms;          /* OPT_TIMING: HIP-event time of the dense full sweeps (k_relax_dense) */
