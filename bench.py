@@ -229,7 +229,7 @@ def main():
                             "candidates_per_launch": cand,
                             "note": "peak = f64 add+compare per candidate; the kernel filters in f32"}
     if st["dense"] and st["delta_sweeps"]:
-        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if args.dense_variant == 1 else "k_relax_dense_delta_p",
+        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if args.dense_variant == 1 else "k_relax_dense_delta_s",
                                     "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
                                     "launches_per_step": st["delta_sweeps"] / args.steps}
 

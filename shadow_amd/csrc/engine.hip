@@ -770,7 +770,9 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
             const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
             f4 w4[TDT / 4];
 #pragma unroll
-            for (int j = 0; j < TDT / 4; ++j) w4[j] = wr[j];
+            for (int j = 0; j < TDT / 4; ++j) {
+                w4[j] = wr[j];
+            }
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
                 const float du = sD[cur][k][r * KL + lane];
@@ -1057,178 +1059,6 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta(const double* __r
     }
 }
 
-// f32-filtered dense delta round, lane = candidate pair.  Same round semantics as
-// k_relax_dense_delta: every (u, s) pair that changed in the previous round is re-offered to
-// the block's 64 destinations.  Here the wave's changed pairs (its 16 sources) are listed in
-// an LDS ring in row order, and 64 of them are filtered at once, one per lane: the lane
-// streams W32(u, v0..v0+63) (lanes sharing a row share the loads) against the thresholds
-// sT[s][v] = f32_thr(d_s(v)) and passes iff D32(u, s) <= max_v fl32(sT[s][v] - W32(u, v))
-// (conservative, see k_relax_dense_f).  Passing pairs (rare) are then re-offered one at a
-// time with lane = destination, exactly in f64 through delta_candidate -- serialised, so no
-// two lanes ever update one (v, s) state.  No per-pair scalar work in the common path.
-constexpr int RING = 2048;  // > 63 pending + 64 rows x 16 sources
-#ifdef EXP_WAVECOUNT
-__device__ long long g_dbg[1 << 17];
-#endif
-
-__device__ __forceinline__ int sT_col(int s, int v) { return (v + 4 * s) & (KL - 1); }  // rotated rows
-
-__global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_p(const float* __restrict__ W32,
-                                                                 const double* __restrict__ W,
-                                                                 const int32_t* __restrict__ WI, int32_t Vp,
-                                                                 const int32_t* __restrict__ in_src,
-                                                                 const double* __restrict__ in_r, Pools pools,
-                                                                 int32_t V, int32_t nb, int32_t nvc, int32_t parity,
-                                                                 int32_t thresh, const int32_t* __restrict__ cnt_prev,
-                                                                 int32_t* __restrict__ cnt) {
-    constexpr int SW = KL / DW;  // sources per wave
-    __shared__ __attribute__((aligned(16))) float sT[KL * KL];
-    __shared__ int32_t sP[DW][RING];  // (u << 6) | s
-    __shared__ unsigned long long sM[DW][KL];
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(1))) const f4 gf4;
-    const int32_t L = blockIdx.x;
-    const int32_t q = L >> 3;
-    const int32_t b = q % nb;
-    const int32_t vc = (L & 7) + 8 * (q / nb);
-    if (vc >= nvc) return;  // block-uniform exits only (barriers below)
-    const int32_t cp = cnt_prev[b];
-    if (cp == 0 || cp > thresh) return;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int32_t v0 = vc * KL;
-    const int32_t v = v0 + lane;
-    const BatchDev B = batch_view(pools, b);
-    const gdouble* D = B.D;
-#ifdef EXP_WAVECOUNT
-    const long long t_start = wall_clock64();
-    int n_drains = 0, n_pass = 0;
-#endif
-    for (int i = wave; i < KL; i += DW) sT[lane * KL + sT_col(lane, i)] = f32_thr(D[(size_t)(v0 + i) * KL + lane]);
-    __syncthreads();
-    const int32_t s0 = wave * SW;
-    const unsigned long long srange = ((1ull << SW) - 1ull) << s0;
-    const unsigned long long* chp = B.chm(parity ^ 1);
-    const gfloat* D32 = B.D32;
-    const gfloat* W32g = (const gfloat*)W32;
-    const bool vok = v < V;
-    const double inf = dinf();
-    int32_t* ring = sP[wave];
-    unsigned long long mine = 0;
-    int32_t head = 0, tail = 0;
-
-    // filter 64 pending pairs (lane = pair), then settle the passing ones exactly
-    auto drain = [&](int n) {
-        const bool valid = lane < n;
-        const int32_t e = ring[(head + (valid ? lane : 0)) & (RING - 1)];
-        const int32_t u = e >> 6, sp = e & 63;
-#ifdef EXP_NOD32
-        const float du = (float)(thresh + lane) * 1e30f;
-#else
-        const float du = D32[(size_t)u * KL + sp];
-#endif
-        const gf4* wrow = (const gf4*)(W32g + (size_t)u * Vp + v0);
-        const float* trow = &sT[sp * KL];
-        // all 16 row loads in flight at once (one memory round trip per drain)
-        f4 w4[KL / 4];
-#pragma unroll
-        for (int j = 0; j < KL / 4; ++j) {
-#ifdef EXP_NOWG
-            const float wc = (float)(thresh + j) * 1e30f;
-            w4[j] = f4{wc, wc, wc, wc};
-#else
-            w4[j] = wrow[j];
-#endif
-        }
-        float g = __int_as_float(0x7fc00000);
-#pragma unroll
-        for (int j = 0; j < KL / 4; ++j) {
-#ifdef EXP_NOSTAGE
-            const float tc = -(float)(thresh + j + lane);
-            const f4 t4 = f4{tc, tc, tc, tc};
-#else
-            const f4 t4 = *(const f4*)&trow[sT_col(sp, 4 * j)];
-#endif
-            const f4 w = w4[j];
-            g = fmaxf(g, fmaxf(fmaxf(t4.x - w.x, t4.y - w.y), fmaxf(t4.z - w.z, t4.w - w.w)));
-        }
-        unsigned long long pm = __ballot(valid && du <= g);
-#ifdef EXP_WAVECOUNT
-        ++n_drains;
-        n_pass += __popcll(pm);
-#endif
-        while (pm) {
-            const int pl = __builtin_ctzll(pm);
-            pm &= pm - 1;
-            const int32_t ue = __builtin_amdgcn_readlane(e, pl);
-            const int32_t uu = ue >> 6, ss = ue & 63;
-            float* tc = &sT[ss * KL + sT_col(ss, lane)];
-            const float c32 = D32[(size_t)uu * KL + ss] + W32g[(size_t)uu * Vp + v];
-            if (vok && c32 <= *tc) {
-                const double du64 = D[(size_t)uu * KL + ss];
-                const double c = du64 + W[(size_t)uu * Vp + v];
-                const double cur = D[(size_t)v * KL + ss];
-                if (c <= cur && c < inf &&
-                    delta_candidate(B, v, ss, uu, du64, c, cur, WI, Vp, in_src, in_r, nullptr, tc))
-                    mine |= 1ull << ss;
-            }
-        }
-        head += n;
-    };
-
-#ifdef EXP_MPREF
-    unsigned long long mnext = (lane < V) ? chp[lane] : 0ull;
-#endif
-    for (int32_t u0 = 0; u0 < V; u0 += KL) {
-#ifdef EXP_MPREF
-        const unsigned long long m = mnext & srange;
-        // next chunk's change masks in flight while this one drains
-        mnext = (u0 + KL + lane < V) ? chp[u0 + KL + lane] : 0ull;
-#else
-        const unsigned long long m = (u0 + lane < V) ? (chp[u0 + lane] & srange) : 0ull;
-#endif
-        const int p = __popcll(m);
-        int incl = p;  // inclusive prefix sum over lanes
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(incl, off);
-            if (lane >= off) incl += o;
-        }
-        const int tot = __builtin_amdgcn_readlane(incl, 63);
-        if (tot) {
-            int pos = tail + incl - p;
-            unsigned long long mm = m;
-            while (mm) {
-                ring[pos & (RING - 1)] = ((u0 + lane) << 6) | __builtin_ctzll(mm);
-                mm &= mm - 1;
-                ++pos;
-            }
-            tail += tot;
-            __builtin_amdgcn_wave_barrier();
-            while (tail - head >= KL) drain(KL);
-        }
-    }
-    if (tail > head) drain(tail - head);
-#ifdef EXP_WAVECOUNT
-    if (lane == 0 && (size_t)blockIdx.x * DW + wave < (1 << 15)) {
-        long long* o = &g_dbg[((size_t)blockIdx.x * DW + wave) * 4];
-        o[0] = tail;
-        o[1] = n_drains;
-        o[2] = n_pass;
-        o[3] = wall_clock64() - t_start;
-    }
-#endif
-    sM[wave][lane] = mine;
-    __syncthreads();
-    if (wave == 0) {
-        unsigned long long all = 0;
-#pragma unroll
-        for (int k = 0; k < DW; ++k) all |= sM[k][lane];
-        B.chm(parity)[v] = all;
-        if (all) atomicAdd(&cnt[b], (int32_t)__popcll(all));
-    }
-}
-
 // Staged f32 dense delta round, lane = candidate pair (the round semantics of
 // k_relax_dense_delta).  The block (one batch, 64 destinations, 4 waves of 16 sources) walks
 // the rows in 64-row chunks; each chunk's W32 slab W32[u0..u0+63][v0..v0+63] is loaded once,
@@ -1238,9 +1068,10 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_p(const float* __
 // sT[s][v] = f32_thr(d_s(v)): pass iff D32(u, s) <= max_v fl32(sT[s][v] - W32(u, v))
 // (conservative, see k_relax_dense_f).  Passing pairs (rare) are settled one at a time with
 // lane = destination, exactly in f64 through delta_candidate, so no two lanes ever update one
-// (v, s) state.  Per-lane 16-byte gathers of W32 rows from global memory (one address per
-// lane per load, 64 TA cycles each) were this round's cost before the slab staging.
-constexpr int SWS = KL + 4;              // staged W32 row stride (floats): rows r != r' (mod 16) on distinct bank quads
+// (v, s) state.  (Gathering each pair's W32 row from global memory instead, 16 bytes per lane
+// per load, cost 1.6x this kernel's time: one texture-address cycle per lane.)
+constexpr int SWS = KL + 4;              // LDS row stride (floats) of the staged W32 slab and the thresholds:
+                                         // rows r != r' (mod 16) on distinct bank quads
 constexpr int RING_S = KL * (KL / DW);   // one chunk's changed pairs of one wave, at most
 
 __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __restrict__ W32,
@@ -1253,7 +1084,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
                                                                  int32_t* __restrict__ cnt) {
     constexpr int SW = KL / DW;  // sources per wave
     constexpr int PF = KL * KL / 4 / (64 * DW);  // float4 of one W32 slab per thread
-    __shared__ __attribute__((aligned(16))) float sT[KL * KL];
+    __shared__ __attribute__((aligned(16))) float sT[KL * SWS];  // [s][v] thresholds
     __shared__ __attribute__((aligned(16))) float sW[KL * SWS];
     __shared__ int32_t sP[DW][RING_S];  // (row in chunk << 6) | s
     __shared__ unsigned long long sM[DW][KL];
@@ -1272,7 +1103,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     const int32_t v = v0 + lane;
     const BatchDev B = batch_view(pools, b);
     const gdouble* D = B.D;
-    for (int i = wave; i < KL; i += DW) sT[lane * KL + sT_col(lane, i)] = f32_thr(D[(size_t)(v0 + i) * KL + lane]);
+    for (int i = wave; i < KL; i += DW) sT[lane * SWS + i] = f32_thr(D[(size_t)(v0 + i) * KL + lane]);
     const int32_t s0 = wave * SW;
     const unsigned long long srange = ((1ull << SW) - 1ull) << s0;
     const unsigned long long* chp = B.chm(parity ^ 1);
@@ -1284,12 +1115,23 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     unsigned long long mine = 0;
 
     f4 pw[PF];
+    // The prefetch addresses are held live until the stash: the compiler must not reuse a
+    // VGPR that a load in flight addresses (it would wait for that load right there, i.e. at
+    // the first drain instead of after the drains).
+    const gf4* pwa[PF];
+    const unsigned long long* pma = chp;
     auto fetch = [&](int32_t u0) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             const int e = threadIdx.x + i * 64 * DW;  // float4 index within the slab: row e / 16, column 4 (e % 16)
-            pw[i] = *(gf4*)(W32g + (size_t)(u0 + (e >> 4)) * Vp + v0 + 4 * (e & 15));
+            pwa[i] = (gf4*)(W32g + (size_t)(u0 + (e >> 4)) * Vp + v0 + 4 * (e & 15));
+            pw[i] = *pwa[i];
         }
+    };
+    auto hold = [&]() {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) asm volatile("" ::"v"(pwa[i]));
+        asm volatile("" ::"v"(pma));
     };
     auto stash = [&]() {
 #pragma unroll
@@ -1304,24 +1146,32 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         const bool valid = lane < n;
         const int32_t e = ring[h + (valid ? lane : n - 1)];
         const int32_t r = e >> 6, sp = e & 63;
-        const float du = D32[(size_t)(u0 + r) * KL + sp];
+        const gfloat* dua = D32 + (size_t)(u0 + r) * KL + sp;
+        const float du = *dua;
         const float* wrow = &sW[r * SWS];
-        const float* trow = &sT[sp * KL];
+        const float* trow = &sT[sp * SWS];
+        // slacks two at a time (v_pk_add_f32), their maximum as a v_max3 chain; both rows are
+        // read at immediate offsets from one base each
+        typedef float f2 __attribute__((ext_vector_type(2)));
         float g = __int_as_float(0x7fc00000);
 #pragma unroll
         for (int j = 0; j < KL / 4; ++j) {
             const f4 w4 = *(const f4*)&wrow[4 * j];
-            const f4 t4 = *(const f4*)&trow[sT_col(sp, 4 * j)];
-            g = fmaxf(g, fmaxf(fmaxf(t4.x - w4.x, t4.y - w4.y), fmaxf(t4.z - w4.z, t4.w - w4.w)));
+            const f4 t4 = *(const f4*)&trow[4 * j];
+            const f2 a = f2{t4.x, t4.y} - f2{w4.x, w4.y};
+            const f2 c = f2{t4.z, t4.w} - f2{w4.z, w4.w};
+            g = fmaxf(fmaxf(g, a.x), a.y);
+            g = fmaxf(fmaxf(g, c.x), c.y);
         }
         unsigned long long pm = __ballot(valid && du <= g);
+        asm volatile("" ::"v"(dua));
         while (pm) {
             const int pl = __builtin_ctzll(pm);
             pm &= pm - 1;
             const int32_t pe = __builtin_amdgcn_readlane(e, pl);
             const int32_t rr = pe >> 6, ss = pe & 63;
             const int32_t uu = u0 + rr;
-            float* tc = &sT[ss * KL + sT_col(ss, lane)];
+            float* tc = &sT[ss * SWS + lane];
             const float c32 = D32[(size_t)uu * KL + ss] + sW[rr * SWS + lane];
             if (vok && c32 <= *tc) {
                 const double du64 = D[(size_t)uu * KL + ss];
@@ -1336,21 +1186,28 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
 
     fetch(0);
     stash();
+    unsigned long long mnext = chp[lane];  // rows < Vp exist; rows >= V are masked at use
     __syncthreads();
     for (int32_t u0 = 0; u0 < V; u0 += KL) {
         const bool more = u0 + KL < V;
-        if (more) fetch(u0 + KL);  // next slab in flight while this chunk drains
-        const unsigned long long m = (u0 + lane < V) ? (chp[u0 + lane] & srange) : 0ull;
+        const unsigned long long m = (u0 + lane < V) ? (mnext & srange) : 0ull;
+        // exclusive prefix sum of the per-row pair counts (<= 16, five bits) from ballots
+        // and mbcnt: no cross-lane LDS round trips
         const int p = __popcll(m);
-        int incl = p;  // inclusive prefix sum over lanes (= rows)
+        int pos = 0, tot = 0;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(incl, off);
-            if (lane >= off) incl += o;
+        for (int bit = 0; bit < 5; ++bit) {
+            const unsigned long long bm = __ballot((p >> bit) & 1);
+            pos += __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << bit;
+            tot += __popcll(bm) << bit;
         }
-        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        // the next chunk's change masks and W32 slab are in flight while this chunk drains
+        // (issued after this chunk's masks are consumed, waited for at the stash);
+        // u0 + KL + 63 < Vp when `more`
+        pma = chp + (more ? u0 + KL : 0) + lane;
+        mnext = *pma;
+        if (more) fetch(u0 + KL);
         if (tot) {
-            int pos = incl - p;
             unsigned long long mm = m;
             while (mm) {
                 ring[pos++] = (lane << 6) | __builtin_ctzll(mm);
@@ -1359,6 +1216,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
             __builtin_amdgcn_wave_barrier();
             for (int h = 0; h < tot; h += KL) drain(u0, h, tot - h < KL ? tot - h : KL);
         }
+        hold();
         __syncthreads();  // every wave is done with this slab
         if (more) stash();
         __syncthreads();
@@ -2061,11 +1919,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                                        eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par,
                                        thresh, cnt_prev, cnt_cur);
                 else
-#ifdef EXP_DELTA_P
-                    hipLaunchKernelGGL(k_relax_dense_delta_p, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
-#else
                     hipLaunchKernelGGL(k_relax_dense_delta_s, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
-#endif
                                        eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur);
                 eng->st.delta_sweeps++;
@@ -2241,13 +2095,6 @@ int shadowtopo_device_count(void) {
 
 const char* shadowtopo_last_error(void) { return g_err.c_str(); }
 
-#ifdef EXP_WAVECOUNT
-int shadowtopo_exp_dump(long long* out, int n) {
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(long long) * (size_t)n));
-    return 0;
-}
-#endif
 
 int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_source, const int32_t* edge_target,
                       const double* edge_latency, const double* edge_packetloss, const double* vertex_packetloss,
