@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
+    ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--csr-variant", type=int, default=1, help="1 = full recomputation (default), 0 = delta rounds")
     args = ap.parse_args()
 
@@ -156,6 +157,7 @@ def main():
     eng.set_option(E.OPT_DENSE_VARIANT, args.dense_variant)
     if args.dense_tb:
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
+    eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_CSR_VARIANT, args.csr_variant)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")

@@ -79,6 +79,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               sweep (default 125; 0 = always full sweeps) */
 #define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default) or _DELTA */
 #define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
+#define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Morton
+                                              order of distances to three attached landmarks), 0 = attach order.
+                                              Results are identical; only which sources share a wave changes. */
 
 /* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every
  * in-arc of every active vertex; DELTA folds only the in-neighbours whose state changed for

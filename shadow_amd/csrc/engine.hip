@@ -1622,11 +1622,13 @@ __global__ void k_extract(GraphDev g, Pools pools, int32_t nsrc, double* dist, i
     const BatchDev B = batch_view(pools, 0);
     const size_t idx = (size_t)v * KL + j;
     const size_t o = (size_t)j * g.V + v;
-    dist[o] = B.D[idx];
-    const int32_t p = B.P[idx];
-    pred[o] = p >= 0 ? g.in_src[p] : -1;
-    hops[o] = B.H[idx] & HMASK;
-    tie[o] = (B.H[idx] & TAINT) ? 1 : 0;
+    if (dist) dist[o] = B.D[idx];
+    if (pred) {
+        const int32_t p = B.P[idx];
+        pred[o] = p >= 0 ? g.in_src[p] : -1;
+    }
+    if (hops) hops[o] = B.H[idx] & HMASK;
+    if (tie) tie[o] = (B.H[idx] & TAINT) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- host side
@@ -1660,6 +1662,9 @@ struct shadowtopo_engine {
     // attached
     int32_t A = 0;
     std::vector<int32_t> h_attached;
+    std::vector<uint64_t> h_key;  // locality key per attached index (OPT_SOURCE_ORDER)
+    bool key_ready = false;
+    int32_t opt_source_order = 1;
     int32_t* d_attached = nullptr;
     double* d_self_lat = nullptr;
     double* d_self_rel = nullptr;
@@ -1973,6 +1978,86 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     return SHADOWTOPO_OK;
 }
 
+// Source order for the label-correcting (CSR) rounds.  A batch's wave is active at a vertex
+// when ANY of its 64 sources has a changed in-neighbour there, so 64 scattered sources make
+// every vertex busy in almost every round (C3: 24 visits per vertex and batch).  Sources
+// that are near each other improve the same vertices in the same rounds.  The key: distances
+// from three attached landmarks (farthest-point: attached[0], then the attached vertex
+// farthest from the landmarks so far), quantised to 21 bits each and bit-interleaved
+// (Morton order), computed once per attached set with the engine's own rounds.  Results do
+// not depend on it: every lane converges to its own source's fixed point.
+int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
+    if (eng->key_ready) return SHADOWTOPO_OK;
+    constexpr double HINF = std::numeric_limits<double>::infinity();
+    const int32_t A = eng->A, V = eng->V;
+    eng->h_key.assign((size_t)A, 0);
+    if (A <= KL) {
+        eng->key_ready = true;
+        return SHADOWTOPO_OK;
+    }
+    int rc;
+    if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
+    const shadowtopo_stats keep = eng->st;
+    constexpr int NL = 3;
+    std::vector<std::vector<double>> dl;
+    double* d_dist = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V));
+    int32_t land = eng->h_attached[0];
+    for (int k = 0; k < NL && land >= 0 && rc == 0; ++k) {
+        for (int j = 0; j < KL; ++j) {
+            eng->h_srcv[j] = j == 0 ? land : -1;
+            eng->h_row[j] = -1;
+        }
+        dl.emplace_back((size_t)V);
+        bool ok = hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL, hipMemcpyHostToDevice,
+                                 s) == hipSuccess;
+        if (!ok) {
+            rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
+            break;
+        }
+        if ((rc = run_rounds(eng, 1, s))) break;
+        hipLaunchKernelGGL(k_extract, dim3((V + 255) / 256, 1), dim3(256), 0, s, eng->g, eng->pools, 1, d_dist,
+                           nullptr, nullptr, nullptr);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(dl.back().data(), d_dist, sizeof(double) * (size_t)V, hipMemcpyDeviceToHost, s) ==
+                 hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+        if (!ok) {
+            rc = fail(SHADOWTOPO_EDEVICE, "landmark distances");
+            break;
+        }
+        // next landmark: the attached vertex farthest (finite) from all landmarks so far
+        double best = -1.0;
+        land = -1;
+        for (int32_t i = 0; i < A; ++i) {
+            const int32_t a = eng->h_attached[i];
+            double m = HINF;
+            for (const auto& d : dl) m = std::min(m, d[a]);
+            if (m < HINF && m > best) best = m, land = a;
+        }
+    }
+    (void)hipFree(d_dist);
+    eng->st = keep;
+    if (rc) return rc;
+    constexpr int QB = 21;
+    const uint64_t qmax = (1ull << QB) - 1;
+    for (size_t k = 0; k < dl.size(); ++k) {
+        double lo = HINF, hi = -HINF;
+        for (int32_t i = 0; i < A; ++i) {
+            const double d = dl[k][eng->h_attached[i]];
+            if (d < HINF) lo = std::min(lo, d), hi = std::max(hi, d);
+        }
+        const double span = hi > lo ? hi - lo : 1.0;
+        for (int32_t i = 0; i < A; ++i) {
+            const double d = dl[k][eng->h_attached[i]];
+            const uint64_t q = d < HINF ? std::min<uint64_t>(qmax, (uint64_t)((d - lo) / span * (double)qmax)) : qmax;
+            for (int b = 0; b < QB; ++b) eng->h_key[i] |= ((q >> b) & 1ull) << (b * NL + k);
+        }
+    }
+    eng->key_ready = true;
+    return SHADOWTOPO_OK;
+}
+
 int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
                       uint32_t* hops, uint8_t* kind, int32_t mem, hipStream_t s) {
     const int32_t A = eng->A;
@@ -1982,6 +2067,11 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const int32_t nb = default_nb(eng, row_end - row_begin);
     if ((rc = ensure_batches(eng, nb))) return rc;
     const int32_t group = nb * KL;
+    // rows of a group go to batch lanes in locality order (CSR rounds only: the dense sweeps
+    // cost the same for any batch)
+    const bool order = eng->opt_source_order && !eng->dense && !complete && row_end - row_begin > KL;
+    if (order && (rc = ensure_locality(eng, s))) return rc;
+    std::vector<int32_t> lane_row;
     // device destinations (user buffers or staging)
     double *dl = lat, *dr = rel;
     uint32_t* dh = hops;
@@ -2009,12 +2099,15 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             dk = kind ? reinterpret_cast<uint8_t*>(p + n * 20) : nullptr;
             row_base = r0;
         }
-        for (int32_t b = 0; b < nbg; ++b) {
-            for (int j = 0; j < KL; ++j) {
-                const int32_t row = r0 + b * KL + j;
-                eng->h_srcv[(size_t)b * KL + j] = row < r1 ? eng->h_attached[row] : -1;
-                eng->h_row[(size_t)b * KL + j] = row < r1 ? row : -1;
-            }
+        lane_row.resize((size_t)nbg * KL);
+        for (size_t i = 0; i < lane_row.size(); ++i) lane_row[i] = r0 + (int32_t)i < r1 ? r0 + (int32_t)i : -1;
+        if (order)
+            std::stable_sort(lane_row.begin(), lane_row.begin() + (r1 - r0),
+                             [&](int32_t x, int32_t y) { return eng->h_key[x] < eng->h_key[y]; });
+        for (size_t i = 0; i < lane_row.size(); ++i) {
+            const int32_t row = lane_row[i];
+            eng->h_srcv[i] = row >= 0 ? eng->h_attached[row] : -1;
+            eng->h_row[i] = row;
         }
         HIP_TRY(hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL * nbg,
                                hipMemcpyHostToDevice, s));
@@ -2041,8 +2134,8 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         std::vector<std::pair<int32_t, int32_t>> jobs;  // (vertex, row)
         for (int32_t b = 0; b < nbg; ++b) {
             for (int j = 0; j < KL; ++j) {
-                const int32_t row = r0 + b * KL + j;
-                if (row >= r1) continue;
+                const int32_t row = lane_row[(size_t)b * KL + j];
+                if (row < 0) continue;
                 if (complete) continue;
                 if (eng->opt_force_replay || (masks[b] >> j) & 1ull) jobs.emplace_back(eng->h_attached[row], row);
             }
@@ -2385,6 +2478,7 @@ int shadowtopo_set_attached(shadowtopo_engine* eng, const int32_t* attached, int
     eng->d_self_hops = nullptr;
     eng->d_self_kind = nullptr;
     eng->h_attached.assign(attached, attached + count);
+    eng->key_ready = false;
     eng->A = count;
     const size_t n = (size_t)std::max(count, 1);
     HIP_TRY(hipMalloc((void**)&eng->d_attached, n * sizeof(int32_t)));
@@ -2432,6 +2526,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL)
                 return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
             eng->opt_csr_variant = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SOURCE_ORDER:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "source order must be 0 or 1");
+            eng->opt_source_order = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_PERMILLE:
             if (value < 0 || value > 1000) return fail(SHADOWTOPO_EINVAL, "delta per mille must be in [0, 1000]");
