@@ -82,6 +82,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Morton
                                               order of distances to three attached landmarks), 0 = attach order.
                                               Results are identical; only which sources share a wave changes. */
+#define SHADOWTOPO_OPT_DENSE_SEED 11       /* dense round 0: 1 (default) = one fused pass writing every (vertex,
+                                              source) state once (k_seed_dense_t), 0 = init, source seed and arc seed
+                                              kernels in turn. Results are identical. */
 
 /* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every
  * in-arc of every active vertex; DELTA folds only the in-neighbours whose state changed for

@@ -910,6 +910,74 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
     }
 }
 
+// Dense round 0 in one pass: the state k_init + k_seed + k_seed_dense would leave, with
+// every (v, source) entry written once.  A block owns 64 destinations [v0, v0+64) of one
+// batch; the batch's source rows W[s][v0..v0+63] are loaded coalesced (lane = v), staged in
+// LDS and read back transposed (lane = source), so the state rows [v][64] are written
+// coalesced too.  Pad rows v >= V get the unreached state.
+constexpr int SEED_ST = KL + 1;  // LDS row stride: the transposed reads spread over the banks
+__global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__ W, const int32_t* __restrict__ WI,
+                                                      int32_t Vp, const double* __restrict__ in_r,
+                                                      const double* __restrict__ vfac, Pools pools, int32_t V) {
+    __shared__ double sw[KL * SEED_ST];
+    __shared__ int32_t si[KL * SEED_ST];
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int32_t v0 = blockIdx.x * KL;
+    for (int j = wave; j < KL; j += 4) {
+        const int32_t s = B.srcv[j];
+        double w = dinf();
+        int32_t a = -1;
+        if (s >= 0 && v0 + lane < V) {
+            w = W[(size_t)s * Vp + v0 + lane];
+            a = WI[(size_t)s * Vp + v0 + lane];
+        }
+        sw[j * SEED_ST + lane] = w;
+        si[j * SEED_ST + lane] = a;
+    }
+    __syncthreads();
+    const int32_t sv = B.srcv[lane];
+    const double rs = sv >= 0 ? vfac[sv] : 0.0;  // R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445)
+    for (int x = wave; x < KL; x += 4) {
+        const int32_t v = v0 + x;
+        const double w = sw[lane * SEED_ST + x];
+        const int32_t arc = si[lane * SEED_ST + x];
+        const bool own = (v == sv);
+        const bool seeded = sv >= 0 && !own && v < V && w < dinf();
+        double d = dinf(), r = 0.0, bdu = dinf();
+        uint32_t h = 0;
+        int32_t p = -1;
+        float d32 = __int_as_float(0x7fc00000);  // NaN: unreached, and the source's own row
+        if (own) {
+            d = 0.0;
+            r = rs;
+        } else if (seeded) {
+            d = 0.0 + w;
+            d32 = f32_key(d);
+            h = 1;
+            r = rs * in_r[arc];
+            p = arc;
+            bdu = 0.0;
+        }
+        const size_t idx = (size_t)v * KL + lane;
+        B.D[idx] = d;
+        B.D32[idx] = d32;
+        B.H[idx] = h;
+        B.R[idx] = r;
+        B.P[idx] = p;
+        B.BDU[idx] = bdu;
+        const unsigned long long reach = __ballot(seeded);
+        const unsigned long long srcm = __ballot(own);
+        if (lane == 0) {
+            B.act0[v] = reach != 0;  // k_seed: out-neighbours of the sources
+            B.act1[v] = 0;
+            B.chm0[v] = 0;
+            B.chm1[v] = srcm;        // k_seed: round -1's change mask holds the sources
+        }
+    }
+}
+
 // One candidate (u -> v for source lane s) with c <= d(v): the lexicographic update of
 // k_relax_dense applied incrementally against the recorded state.  The recorded lex key is
 // (D, BDU); the local-tie bit LTIE stays valid while the predecessor's key is unchanged.
@@ -1665,6 +1733,7 @@ struct shadowtopo_engine {
     std::vector<uint64_t> h_key;  // locality key per attached index (OPT_SOURCE_ORDER)
     bool key_ready = false;
     int32_t opt_source_order = 1;
+    int32_t opt_dense_seed = 1;
     int32_t* d_attached = nullptr;
     double* d_self_lat = nullptr;
     double* d_self_rel = nullptr;
@@ -1860,7 +1929,12 @@ hipError_t launch_dense_f(shadowtopo_engine* eng, int32_t nbg, int32_t par, int3
 int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = eng->V;
     const GraphDev& g = eng->g;
-    {
+    const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
+    if (fused_seed) {
+        hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / KL, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
+                           g.in_r, g.vfac, eng->pools, V);
+        HIP_TRY(hipGetLastError());
+    } else {
         const size_t total = (size_t)eng->Vp * KL;
         int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
         hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp);
@@ -1876,9 +1950,11 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     eng->d_prof = eng->opt_profile ? eng->prof_buf : nullptr;
     if (eng->d_prof) HIP_TRY(hipMemsetAsync(eng->d_prof, 0, sizeof(unsigned long long) * 16 * nbg, s));
     if (eng->dense) {
-        hipLaunchKernelGGL(k_seed_dense, dim3(ntb, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp, g.in_r,
-                           eng->pools, V);
-        HIP_TRY(hipGetLastError());
+        if (!fused_seed) {
+            hipLaunchKernelGGL(k_seed_dense, dim3(ntb, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp, g.in_r,
+                               eng->pools, V);
+            HIP_TRY(hipGetLastError());
+        }
         // round 0 consumes the change counts of a virtual round -1: every batch changed
         // everything (full sweep)
         HIP_TRY(hipMemsetAsync(eng->d_cnt + eng->nb_cap, 0x7f, sizeof(int32_t) * nbg, s));
@@ -2530,6 +2606,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_SOURCE_ORDER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "source order must be 0 or 1");
             eng->opt_source_order = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DENSE_SEED:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");
+            eng->opt_dense_seed = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_PERMILLE:
             if (value < 0 || value > 1000) return fail(SHADOWTOPO_EINVAL, "delta per mille must be in [0, 1000]");

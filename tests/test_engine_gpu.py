@@ -229,3 +229,40 @@ def test_dense_delta_same_fixed_point(case):
         assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
     if case == "ties":
         assert (t0 != 0).any()
+
+
+@pytest.mark.parametrize("case", ["sparse", "directed", "ties", "vloss_prefer", "geometric_odd"])
+def test_dense_fused_seed_same_state(case):
+    """OPT_DENSE_SEED: the fused round-0 kernel (k_seed_dense_t) and the init / source seed /
+    arc seed kernels leave the same state, so rows and matrices are bit-identical (and the
+    default, fused, matches the oracle)."""
+    if case == "sparse":
+        g = synth.random_sparse(V=301, avg_deg=5, seed=2)
+    elif case == "directed":
+        g = synth.random_sparse(V=203, avg_deg=4, seed=5, directed=True)
+    elif case == "ties":
+        g = synth.integer_grid(rows=9, cols=11, seed=2)
+    elif case == "vloss_prefer":
+        rng = np.random.default_rng(4)
+        g = synth.random_sparse(V=150, avg_deg=8, seed=6, vloss=rng.uniform(0, 0.1, 150))
+        g.prefer_direct = True
+    else:
+        g = synth.geometric_complete_ish(V=611, A=150)  # V not a multiple of 64, 3 batches
+    srcs = np.arange(0, g.n, 2, dtype=np.int32)
+    rows, mats = [], []
+    for fused in (0, 1):
+        eng = E.Engine.from_synth(g, layout="dense")
+        eng.set_option(E.OPT_DENSE_SEED, fused)
+        rows.append(eng.sssp(srcs))
+        eng.set_attached(g.attached)
+        mats.append(eng.compute_rows(want_kind=True))
+        eng.close()
+    (d0, p0, h0, t0), (d1, p1, h1, t1) = rows
+    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+    assert np.array_equal(t0, t1)
+    ok = t0 == 0
+    assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
+    for x, y in zip(*mats):
+        assert np.array_equal(x.view(np.uint8) if x.dtype == np.float64 else x,
+                              y.view(np.uint8) if y.dtype == np.float64 else y)
+    assert compare(g, layout="dense")["dense"] == 1
