@@ -85,6 +85,12 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DENSE_SEED 11       /* dense round 0: 1 (default) = one fused pass writing every (vertex,
                                               source) state once (k_seed_dense_t), 0 = init, source seed and arc seed
                                               kernels in turn. Results are identical. */
+#define SHADOWTOPO_OPT_DENSE_PRUNE 12      /* f32 dense full sweep: 1 (default) = rows and destinations in a vertex
+                                              locality order (Morton order of distances to three landmarks, built on
+                                              the first computation), sources batched in locality order, and a wave
+                                              skips a 32-row chunk when no lane can pass any of its rows (bound: min
+                                              D32 of the chunk vs max threshold - min W32 of the chunk x tile);
+                                              0 = every chunk filtered, original order. Results are identical. */
 
 /* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every
  * in-arc of every active vertex; DELTA folds only the in-neighbours whose state changed for

@@ -544,12 +544,13 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
                                                const double* bc, const double* bdu, const int32_t* bu, uint32_t tie,
                                                const int32_t* __restrict__ WI, int32_t Vp,
                                                const double* __restrict__ in_r, int32_t parity,
-                                               int32_t* __restrict__ cnt, int32_t b) {
+                                               int32_t* __restrict__ cnt, int32_t b,
+                                               const int32_t* vids = nullptr) {
     unsigned long long* chn = B.chm(parity);
     int32_t nch = 0;
 #pragma unroll
     for (int t = 0; t < TDT; ++t) {
-        const int32_t v = v0 + t;
+        const int32_t v = vids ? vids[t] : v0 + t;  // vids: the pruned sweep's permuted tile
         if (v >= V) break;
         bool ch = false;
         if (bu[t] >= 0 && sv >= 0 && sv != v) {
@@ -654,7 +655,7 @@ __device__ __forceinline__ float f32_thr(double bc) {
 //    minimum and tie flag as a sequential scan.
 constexpr int SRS = 32;  // rows per LDS chunk
 
-template <int TDT, int XR, int TB>
+template <int TDT, int XR, int TB, bool PR>
 __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
@@ -662,7 +663,18 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
                                                        const int32_t* __restrict__ cnt_prev,
                                                        int32_t* __restrict__ cnt,
                                                        unsigned long long* __restrict__ prof,
-                                                       uint32_t* __restrict__ hitlog) {
+                                                       uint32_t* __restrict__ hitlog,
+                                                       const int32_t* __restrict__ perm,
+                                                       const float* __restrict__ minW,
+                                                       const float* __restrict__ minD) {
+    // PR (pruned): rows, columns and W32 are in the locality order `perm` (W32 here is the
+    // permuted copy W32p[i][j] = W32[perm i][perm j]); a wave skips a chunk outright when no
+    // lane can pass any of its rows: min D32 over the chunk's rows (minD, per lane) exceeds
+    // fl32(max_t thr_t - min W32 over the chunk x the wave's columns (minW)).  Every row's
+    // filter bound max_t fl32(thr_t - W32(u, v_t)) is <= that (rounding is monotone), and
+    // D32(u) >= min D32, so the skip is exact; minD is taken before the sweep, which is the
+    // same as having read those rows' pre-sweep values (later changes reach the delta round
+    // through the change masks).
     constexpr int BW = 4 * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
@@ -683,6 +695,9 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int32_t v0 = vb + wave * TDT;
+    int32_t vid[TDT];  // this wave's destinations (vertex ids)
+#pragma unroll
+    for (int t = 0; t < TDT; ++t) vid[t] = PR ? perm[v0 + t] : v0 + t;
     BatchDev B[TB];
     int32_t sv[TB];
     double bc[TB][TDT], bdu[TB][TDT];
@@ -698,7 +713,7 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         tie[k] = 0;
 #pragma unroll
         for (int t = 0; t < TDT; ++t) {
-            const int32_t v = v0 + t;
+            const int32_t v = vid[t];
             const double cd = B[k].D[(size_t)v * KL + lane];  // padding rows are +inf
             const double ws = (sv[k] >= 0 && sv[k] != v) ? W[(size_t)sv[k] * Vp + v] : dinf();
             if (ws < dinf()) {
@@ -722,14 +737,38 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     constexpr int DQ = SRS * KL / 4 / 256;       // float4 of one batch's D32 chunk per thread
     constexpr int WQT = (SRS * WQ + 255) / 256;  // float4 of W32 per thread
     f4 pd[TB][DQ], pw[WQT];
+    // PR: permuted row ids of the chunk being fetched (loaded one fetch ahead), and the
+    // chunk's skip bounds (md: min D32 per lane and batch, mw: min W32 of the wave's tile)
+    int32_t prow[DQ];
+    float mdn[TB], mdc[TB], mwn = 0.f, mwc = 0.f;
+    const int32_t nwt = (V + BW - 1) / BW * 4;  // wave tiles per chunk row of minW
+    if (PR) {
+#pragma unroll
+        for (int i = 0; i < DQ; ++i) prow[i] = perm[vt % nchunks * SRS + (threadIdx.x + i * 256) / (KL / 4)];
+    }
     auto fetch = [&](int32_t u0) {
 #pragma unroll
         for (int k = 0; k < TB; ++k)
 #pragma unroll
             for (int i = 0; i < DQ; ++i) {
                 const int e = threadIdx.x + i * 256;  // float4 index within the chunk
-                pd[k][i] = *(gf4*)(B[k].D32 + (size_t)u0 * KL + (size_t)e * 4);
+                if (PR)
+                    pd[k][i] = *(gf4*)(B[k].D32 + (size_t)prow[i] * KL + (size_t)(e % (KL / 4)) * 4);
+                else
+                    pd[k][i] = *(gf4*)(B[k].D32 + (size_t)u0 * KL + (size_t)e * 4);
             }
+        if (PR) {
+            const int32_t c = u0 / SRS;
+#pragma unroll
+            for (int k = 0; k < TB; ++k)
+                mdn[k] = minD[((size_t)(live[k] ? b0 + k : first) * nchunks + c) * KL + lane];
+            mwn = minW[(size_t)c * nwt + vt * 4 + wave];
+#pragma unroll
+            for (int i = 0; i < DQ; ++i) {
+                const int32_t r = (c + 1 == nchunks ? 0 : c + 1) * SRS + (threadIdx.x + i * 256) / (KL / 4);
+                prow[i] = perm[r];
+            }
+        }
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
             const int e = threadIdx.x + i * 256;
@@ -750,13 +789,39 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
             if (e < SRS * WQ) *(f4*)&sW[buf][e * 4] = pw[i];
         }
     };
-    fetch(0);
+    auto advance = [&]() {
+        if (PR) {
+#pragma unroll
+            for (int k = 0; k < TB; ++k) mdc[k] = mdn[k];
+            mwc = mwn;
+        }
+    };
+    // PR: chunks in the order vt, vt+1, .., wrapping: the block's own tile (its destinations'
+    // nearest rows) first, which gives unreached and arc-less (t, s) pairs a tight threshold
+    // before the far chunks are tested
+    const int32_t c0 = PR ? vt % nchunks : 0;
+    fetch(c0 * SRS);
     stash(0);
+    advance();
     __syncthreads();
-    for (int32_t u0 = 0; u0 < nrows; u0 += SRS) {
-        const int cur = (u0 / SRS) & 1;
-        const bool more = u0 + SRS < nrows;
-        if (more) fetch(u0 + SRS);
+    for (int32_t it = 0; it < nchunks; ++it) {
+        const int32_t c = PR ? (c0 + it) % nchunks : it;
+        const int32_t u0 = c * SRS;
+        const int cur = it & 1;
+        const bool more = it + 1 < nchunks;
+        if (more) fetch((c + 1 == nchunks ? 0 : c + 1) * SRS);
+        bool run = true;
+        if (PR) {
+            bool p = false;
+#pragma unroll
+            for (int k = 0; k < TB; ++k) {
+                float tm = thr[k][0];
+#pragma unroll
+                for (int t = 1; t < TDT; ++t) tm = fmaxf(tm, thr[k][t]);
+                p |= mdc[k] <= tm - mwc;
+            }
+            run = __ballot(p) != 0;
+        }
         // per batch: bit r = row u0 + r passed the filter in some lane.  One broadcast read
         // of the row's TDT weights serves all TB batches.  A passing row tightens the
         // thresholds at once with an f32 upper bound of its candidates -- the exact f64 work
@@ -766,7 +831,7 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
 #pragma unroll
         for (int k = 0; k < TB; ++k) hits[k] = 0;
 #pragma unroll 2
-        for (int r = 0; r < SRS; ++r) {
+        for (int r = 0; r < (run ? SRS : 0); ++r) {
             const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
             f4 w4[TDT / 4];
 #pragma unroll
@@ -815,7 +880,10 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
 #pragma unroll
             for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + (u0 / SRS)] = hits[k];
         }
-        if (more) stash(cur ^ 1);
+        if (more) {
+            stash(cur ^ 1);
+            advance();
+        }
         __syncthreads();
     }
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
@@ -827,6 +895,7 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         if (!live[k]) continue;
         const uint32_t* hl = hitlog + ((size_t)gw * TB + k) * nchunks;
         const gdouble* Dl = B[k].D + lane;
+        const int32_t vl = PR ? perm[v0 + (lane & (TDT - 1))] : v0 + (lane & (TDT - 1));
         for (int32_t c0 = 0; c0 < nchunks; c0 += 64) {
             const uint32_t e = (c0 + lane < nchunks) ? hl[c0 + lane] : 0u;
             unsigned long long cm = __ballot(e != 0u);
@@ -847,12 +916,13 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
                             hrows &= hrows - 1;
                             nr = x + 1;
                         }
+                        if (PR) ur[x] = perm[ur[x]];  // row index -> vertex
                     }
                     double d64[XR], wl[XR];
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
                         d64[x] = Dl[(size_t)ur[x] * KL];
-                        wl[x] = W[(size_t)ur[x] * Vp + v0 + (lane & (TDT - 1))];
+                        wl[x] = W[(size_t)ur[x] * Vp + vl];
                     }
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
@@ -876,8 +946,43 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         for (int k = 0; k < TB; ++k)
             if (live[k])
                 dense_epilogue<TDT>(B[k], lane, sv[k], v0, V, bc[k], bdu[k], bu[k], tie[k], WI, Vp, in_r, parity,
-                                    cnt, b0 + k);
+                                    cnt, b0 + k, vid);
     }
+}
+
+// Pruned full sweep (k_relax_dense_f<.., PR = true>) inputs.
+// W32p[i][j] = W32[perm i][perm j]: the f32 weights in the vertex locality order, one row per block
+__global__ __launch_bounds__(256) void k_permute_w32(const float* __restrict__ W32, const int32_t* __restrict__ perm,
+                                                     int32_t Vp, float* __restrict__ W32p) {
+    const size_t i = blockIdx.x;
+    const gfloat* src = (const gfloat*)W32 + (size_t)perm[i] * Vp;
+    for (int32_t j = threadIdx.x; j < Vp; j += 256) W32p[i * Vp + j] = src[perm[j]];
+}
+
+// minW[c][w] = min of W32p over rows [c*SRS, c*SRS+SRS) x columns [w*tdt, w*tdt+tdt), NaN (no
+// arc) ignored, +inf when the tile has no arc
+__global__ __launch_bounds__(256) void k_min_w32(const float* __restrict__ W32p, int32_t Vp, int32_t nchunks,
+                                                 int32_t nwt, int32_t tdt, float* __restrict__ minW) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)nchunks * nwt) return;
+    const int32_t c = (int32_t)(idx / nwt), w = (int32_t)(idx % nwt);
+    float m = __int_as_float(0x7f800000);
+    for (int r = 0; r < SRS; ++r)
+        for (int t = 0; t < tdt; ++t) m = fminf(m, W32p[(size_t)(c * SRS + r) * Vp + w * tdt + t]);
+    minW[idx] = m;
+}
+
+// minD[b][c][lane] = min of D32 over the rows perm[c*SRS .. c*SRS+SRS) of batch b, NaN
+// (unreached, own source) ignored; one wave per (chunk, batch)
+__global__ __launch_bounds__(256) void k_min_d32(Pools pools, const int32_t* __restrict__ perm, int32_t nchunks,
+                                                 float* __restrict__ minD) {
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
+    float m = __int_as_float(0x7f800000);
+    for (int r = 0; r < SRS; ++r) m = fminf(m, B.D32[(size_t)perm[c * SRS + r] * KL + lane]);
+    minD[((size_t)blockIdx.y * nchunks + c) * KL + lane] = m;
 }
 
 // Dense round 0: every destination's only finite candidate is its source's direct arc
@@ -1716,6 +1821,13 @@ struct shadowtopo_engine {
     const float* d_W32 = nullptr;   // dense mode: [Vp][Vp] arc latency rounded down to f32, NaN if none
     uint32_t* d_hitlog = nullptr;   // dense full sweep: per wave, per batch, per 32-row chunk: rows to settle in f64
     size_t hitlog_n = 0;
+    // pruned full sweep (OPT_DENSE_PRUNE): vertex locality order and its chunk bounds
+    int32_t* d_perm = nullptr;  // [Vp] row/column order (padding maps to itself)
+    float* d_W32p = nullptr;    // [Vp][Vp] W32 in that order
+    float* d_minW = nullptr;    // [nchunks][wave tiles] min W32p
+    float* d_minD = nullptr;    // [nb_cap][nchunks][64] min D32 per chunk and lane
+    size_t minD_n = 0;
+    bool vperm_ready = false;
     int64_t E = 0;
     int64_t n_arcs = 0;
     uint32_t flags = 0;
@@ -1734,6 +1846,7 @@ struct shadowtopo_engine {
     bool key_ready = false;
     int32_t opt_source_order = 1;
     int32_t opt_dense_seed = 1;
+    int32_t opt_dense_prune = 1;
     int32_t* d_attached = nullptr;
     double* d_self_lat = nullptr;
     double* d_self_rel = nullptr;
@@ -1910,9 +2023,27 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
         if (e != hipSuccess) return e;
         eng->hitlog_n = need;
     }
-    hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32, eng->d_W,
-                       eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof, eng->d_hitlog);
+    if (eng->vperm_ready && eng->opt_dense_prune) {
+        const size_t mneed = (size_t)eng->nb_cap * nchunks * KL;
+        if (eng->minD_n < mneed) {
+            if (eng->d_minD) (void)hipFree(eng->d_minD);
+            eng->d_minD = nullptr;
+            eng->minD_n = 0;
+            hipError_t e = hipMalloc((void**)&eng->d_minD, mneed * sizeof(float));
+            if (e != hipSuccess) return e;
+            eng->minD_n = mneed;
+        }
+        hipLaunchKernelGGL(k_min_d32, dim3((uint32_t)((nchunks + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
+                           eng->d_perm, (int32_t)nchunks, eng->d_minD);
+        hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
+                           eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
+                           thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
+                           eng->d_minD);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, false>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32,
+                       eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
+                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -2062,15 +2193,13 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
 // farthest from the landmarks so far), quantised to 21 bits each and bit-interleaved
 // (Morton order), computed once per attached set with the engine's own rounds.  Results do
 // not depend on it: every lane converges to its own source's fixed point.
-int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
-    if (eng->key_ready) return SHADOWTOPO_OK;
+// Morton keys of `cand` (the attached list, or every vertex for the pruned dense sweep's
+// vertex order) from three farthest-point landmarks chosen among `cand`
+int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32_t>& cand,
+                  std::vector<uint64_t>& key) {
     constexpr double HINF = std::numeric_limits<double>::infinity();
-    const int32_t A = eng->A, V = eng->V;
-    eng->h_key.assign((size_t)A, 0);
-    if (A <= KL) {
-        eng->key_ready = true;
-        return SHADOWTOPO_OK;
-    }
+    const int32_t A = (int32_t)cand.size(), V = eng->V;
+    key.assign((size_t)A, 0);
     int rc;
     if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
     const shadowtopo_stats keep = eng->st;
@@ -2078,7 +2207,7 @@ int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
     std::vector<std::vector<double>> dl;
     double* d_dist = nullptr;
     HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V));
-    int32_t land = eng->h_attached[0];
+    int32_t land = cand[0];
     for (int k = 0; k < NL && land >= 0 && rc == 0; ++k) {
         for (int j = 0; j < KL; ++j) {
             eng->h_srcv[j] = j == 0 ? land : -1;
@@ -2106,7 +2235,7 @@ int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
         double best = -1.0;
         land = -1;
         for (int32_t i = 0; i < A; ++i) {
-            const int32_t a = eng->h_attached[i];
+            const int32_t a = cand[i];
             double m = HINF;
             for (const auto& d : dl) m = std::min(m, d[a]);
             if (m < HINF && m > best) best = m, land = a;
@@ -2120,17 +2249,60 @@ int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
     for (size_t k = 0; k < dl.size(); ++k) {
         double lo = HINF, hi = -HINF;
         for (int32_t i = 0; i < A; ++i) {
-            const double d = dl[k][eng->h_attached[i]];
+            const double d = dl[k][cand[i]];
             if (d < HINF) lo = std::min(lo, d), hi = std::max(hi, d);
         }
         const double span = hi > lo ? hi - lo : 1.0;
         for (int32_t i = 0; i < A; ++i) {
-            const double d = dl[k][eng->h_attached[i]];
+            const double d = dl[k][cand[i]];
             const uint64_t q = d < HINF ? std::min<uint64_t>(qmax, (uint64_t)((d - lo) / span * (double)qmax)) : qmax;
-            for (int b = 0; b < QB; ++b) eng->h_key[i] |= ((q >> b) & 1ull) << (b * NL + k);
+            for (int b = 0; b < QB; ++b) key[i] |= ((q >> b) & 1ull) << (b * NL + k);
         }
     }
+    return SHADOWTOPO_OK;
+}
+
+int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
+    if (eng->key_ready) return SHADOWTOPO_OK;
+    if (eng->A <= KL) {
+        eng->h_key.assign((size_t)eng->A, 0);
+        eng->key_ready = true;
+        return SHADOWTOPO_OK;
+    }
+    int rc = locality_keys(eng, s, eng->h_attached, eng->h_key);
+    if (rc) return rc;
     eng->key_ready = true;
+    return SHADOWTOPO_OK;
+}
+
+// Pruned dense sweep: the vertex locality order, W32 permuted into it, and the per-chunk,
+// per-wave-tile W32 minima.  Built once per engine (the landmark rounds run the unpruned
+// sweep); any order gives the same results, a local one lets waves skip chunks.
+int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
+    if (eng->vperm_ready || !eng->dense || !eng->opt_dense_prune || !eng->d_W32) return SHADOWTOPO_OK;
+    const int32_t V = eng->V, Vp = eng->Vp;
+    if (V <= SRS) return SHADOWTOPO_OK;
+    std::vector<int32_t> all((size_t)V);
+    for (int32_t v = 0; v < V; ++v) all[v] = v;
+    std::vector<uint64_t> key;
+    int rc = locality_keys(eng, s, all, key);
+    if (rc) return rc;
+    std::vector<int32_t> perm(all);
+    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    for (int32_t i = V; i < Vp; ++i) perm.push_back(i);
+    constexpr int TDT = 8;  // launch_dense_ft's wave tile
+    const int32_t nchunks = (V + SRS - 1) / SRS;
+    const int32_t nwt = (V + 4 * TDT - 1) / (4 * TDT) * 4;
+    HIP_TRY(hipMalloc((void**)&eng->d_perm, sizeof(int32_t) * (size_t)Vp));
+    HIP_TRY(hipMalloc((void**)&eng->d_W32p, sizeof(float) * (size_t)Vp * Vp));
+    HIP_TRY(hipMalloc((void**)&eng->d_minW, sizeof(float) * (size_t)nchunks * nwt));
+    HIP_TRY(hipMemcpyAsync(eng->d_perm, perm.data(), sizeof(int32_t) * (size_t)Vp, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_permute_w32, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_W32, eng->d_perm, Vp, eng->d_W32p);
+    hipLaunchKernelGGL(k_min_w32, dim3((uint32_t)(((int64_t)nchunks * nwt + 255) / 256)), dim3(256), 0, s,
+                       eng->d_W32p, Vp, nchunks, nwt, TDT, eng->d_minW);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    eng->vperm_ready = true;
     return SHADOWTOPO_OK;
 }
 
@@ -2143,9 +2315,12 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const int32_t nb = default_nb(eng, row_end - row_begin);
     if ((rc = ensure_batches(eng, nb))) return rc;
     const int32_t group = nb * KL;
-    // rows of a group go to batch lanes in locality order (CSR rounds only: the dense sweeps
-    // cost the same for any batch)
-    const bool order = eng->opt_source_order && !eng->dense && !complete && row_end - row_begin > KL;
+    if ((rc = ensure_vperm(eng, s))) return rc;
+    // rows of a group go to batch lanes in locality order (CSR rounds, and the pruned dense
+    // sweep, whose chunk skips need a batch's sources near each other; the unpruned dense
+    // sweeps cost the same for any batch)
+    const bool order = eng->opt_source_order && (!eng->dense || eng->vperm_ready) && !complete &&
+                       row_end - row_begin > KL;
     if (order && (rc = ensure_locality(eng, s))) return rc;
     std::vector<int32_t> lane_row;
     // device destinations (user buffers or staging)
@@ -2530,6 +2705,10 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
     if (eng->stage) (void)hipFree(eng->stage);
     if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
+    if (eng->d_perm) (void)hipFree(eng->d_perm);
+    if (eng->d_W32p) (void)hipFree(eng->d_W32p);
+    if (eng->d_minW) (void)hipFree(eng->d_minW);
+    if (eng->d_minD) (void)hipFree(eng->d_minD);
     if (eng->ev0) (void)hipEventDestroy(eng->ev0);
     if (eng->ev1) (void)hipEventDestroy(eng->ev1);
     if (eng->evm) (void)hipEventDestroy(eng->evm);
@@ -2606,6 +2785,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_SOURCE_ORDER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "source order must be 0 or 1");
             eng->opt_source_order = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DENSE_PRUNE:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense prune must be 0 or 1");
+            eng->opt_dense_prune = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DENSE_SEED:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");

@@ -40,6 +40,7 @@ OPT_CSR_VARIANT = 8
 OPT_DENSE_BATCHES_PER_WAVE = 9
 OPT_SOURCE_ORDER = 10
 OPT_DENSE_SEED = 11
+OPT_DENSE_PRUNE = 12
 CSR_DELTA = 0  # fold changed in-neighbours into the recorded state (cross-check)
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (default)
 

@@ -266,3 +266,43 @@ def test_dense_fused_seed_same_state(case):
         assert np.array_equal(x.view(np.uint8) if x.dtype == np.float64 else x,
                               y.view(np.uint8) if y.dtype == np.float64 else y)
     assert compare(g, layout="dense")["dense"] == 1
+
+
+@pytest.mark.parametrize("case", ["sparse", "directed", "ties", "vloss_prefer", "geometric_odd", "geometric_big"])
+def test_dense_prune_same_results(case):
+    """OPT_DENSE_PRUNE: the pruned full sweep (vertex locality order, chunks skipped on the
+    min-D32 / min-W32 bound, sources batched in locality order) gives bit-identical rows and
+    matrices to the unpruned sweep, and the default (pruned) matches the oracle."""
+    if case == "sparse":
+        g = synth.random_sparse(V=301, avg_deg=5, seed=2)
+    elif case == "directed":
+        g = synth.random_sparse(V=203, avg_deg=4, seed=5, directed=True)
+    elif case == "ties":
+        g = synth.integer_grid(rows=9, cols=11, seed=2)
+    elif case == "vloss_prefer":
+        rng = np.random.default_rng(4)
+        g = synth.random_sparse(V=150, avg_deg=8, seed=6, vloss=rng.uniform(0, 0.1, 150))
+        g.prefer_direct = True
+    elif case == "geometric_odd":
+        g = synth.geometric_complete_ish(V=611, A=150)  # V not a multiple of 64, 3 batches
+    else:
+        g = synth.geometric_complete_ish(V=2500, A=400, drop=0.2)  # 7 batches, many skipped chunks
+    srcs = np.arange(0, g.n, 3, dtype=np.int32)
+    rows, mats = [], []
+    for prune in (0, 1):
+        eng = E.Engine.from_synth(g, layout="dense")
+        eng.set_option(E.OPT_DENSE_PRUNE, prune)
+        eng.set_attached(g.attached)
+        mats.append(eng.compute_rows(want_kind=True))  # builds the vertex order when pruning
+        rows.append(eng.sssp(srcs))  # full rows through the (pruned) sweep
+        eng.close()
+    (d0, p0, h0, t0), (d1, p1, h1, t1) = rows
+    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+    assert np.array_equal(t0, t1)
+    ok = t0 == 0
+    assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
+    for x, y in zip(*mats):
+        assert np.array_equal(x.view(np.uint8) if x.dtype == np.float64 else x,
+                              y.view(np.uint8) if y.dtype == np.float64 else y)
+    if case != "geometric_big":
+        assert compare(g, layout="dense")["dense"] == 1
