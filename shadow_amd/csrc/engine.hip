@@ -725,7 +725,9 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
                 bdu[k][t] = dinf();
                 bu[k][t] = -1;
             }
-            thr[k][t] = live[k] ? f32_thr(cd < bc[k][t] ? cd : bc[k][t]) : __int_as_float(0x7fc00000);
+            // a lane without a source (a partial batch) never passes: NaN, so it cannot hold a
+            // pruned wave's chunk skip back either
+            thr[k][t] = live[k] && sv[k] >= 0 ? f32_thr(cd < bc[k][t] ? cd : bc[k][t]) : __int_as_float(0x7fc00000);
         }
     }
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1828,6 +1830,7 @@ struct shadowtopo_engine {
     float* d_minD = nullptr;    // [nb_cap][nchunks][64] min D32 per chunk and lane
     size_t minD_n = 0;
     bool vperm_ready = false;
+    std::vector<uint64_t> h_vkey;  // [V] locality key of every vertex (the order's sort key)
     int64_t E = 0;
     int64_t n_arcs = 0;
     uint32_t flags = 0;
@@ -2194,16 +2197,18 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
 // (Morton order), computed once per attached set with the engine's own rounds.  Results do
 // not depend on it: every lane converges to its own source's fixed point.
 // Morton keys of `cand` (the attached list, or every vertex for the pruned dense sweep's
-// vertex order) from three farthest-point landmarks chosen among `cand`
+// vertex order) from NL farthest-point landmarks chosen among `cand`.  embed2: instead of
+// interleaving the NL distances, project the centred distance vectors on their top two
+// principal axes (landmark MDS) and interleave those two coordinates: for geographic graphs
+// that recovers a near-planar layout, whose 32-vertex chunks are far more compact.
 int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32_t>& cand,
-                  std::vector<uint64_t>& key) {
+                  std::vector<uint64_t>& key, int NL = 3, bool embed2 = false) {
     constexpr double HINF = std::numeric_limits<double>::infinity();
     const int32_t A = (int32_t)cand.size(), V = eng->V;
     key.assign((size_t)A, 0);
     int rc;
     if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
     const shadowtopo_stats keep = eng->st;
-    constexpr int NL = 3;
     std::vector<std::vector<double>> dl;
     double* d_dist = nullptr;
     HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V));
@@ -2244,9 +2249,66 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
     (void)hipFree(d_dist);
     eng->st = keep;
     if (rc) return rc;
-    constexpr int QB = 21;
+    if (embed2 && dl.size() >= 3) {
+        const int L = (int)dl.size();
+        std::vector<double> mean((size_t)L, 0.0), X((size_t)A * L);
+        for (int k = 0; k < L; ++k) {
+            double sum = 0.0;
+            int64_t n = 0;
+            for (int32_t i = 0; i < A; ++i)
+                if (dl[k][cand[i]] < HINF) sum += dl[k][cand[i]], ++n;
+            const double m = n ? sum / (double)n : 0.0;
+            for (int32_t i = 0; i < A; ++i) X[(size_t)i * L + k] = (dl[k][cand[i]] < HINF ? dl[k][cand[i]] : m) - m;
+        }
+        std::vector<double> C((size_t)L * L, 0.0);
+        for (int32_t i = 0; i < A; ++i)
+            for (int a = 0; a < L; ++a)
+                for (int b = 0; b < L; ++b) C[a * L + b] += X[(size_t)i * L + a] * X[(size_t)i * L + b];
+        std::vector<double> axes[2];
+        for (int e = 0; e < 2; ++e) {  // power iteration with deflation
+            std::vector<double> v((size_t)L), w((size_t)L);
+            for (int a = 0; a < L; ++a) v[a] = 1.0 + 0.1 * a;
+            double lam = 0.0;
+            for (int it = 0; it < 500; ++it) {
+                double nrm = 0.0;
+                for (int a = 0; a < L; ++a) {
+                    w[a] = 0.0;
+                    for (int b = 0; b < L; ++b) w[a] += C[a * L + b] * v[b];
+                    nrm += w[a] * w[a];
+                }
+                nrm = std::sqrt(nrm);
+                if (!(nrm > 0.0)) break;
+                lam = nrm;
+                for (int a = 0; a < L; ++a) v[a] = w[a] / nrm;
+            }
+            axes[e] = v;
+            for (int a = 0; a < L; ++a)
+                for (int b = 0; b < L; ++b) C[a * L + b] -= lam * v[a] * v[b];
+        }
+        std::vector<double> y[2];
+        for (int e = 0; e < 2; ++e) {
+            y[e].resize((size_t)A);
+            double lo = HINF, hi = -HINF;
+            for (int32_t i = 0; i < A; ++i) {
+                double t = 0.0;
+                for (int a = 0; a < L; ++a) t += X[(size_t)i * L + a] * axes[e][a];
+                y[e][i] = t;
+                lo = std::min(lo, t), hi = std::max(hi, t);
+            }
+            const double span = hi > lo ? hi - lo : 1.0;
+            for (int32_t i = 0; i < A; ++i) y[e][i] = (y[e][i] - lo) / span;
+        }
+        constexpr int QB2 = 31;
+        const double qm = (double)((1ull << QB2) - 1);
+        for (int32_t i = 0; i < A; ++i) {
+            const uint64_t q0 = (uint64_t)(y[0][i] * qm), q1 = (uint64_t)(y[1][i] * qm);
+            for (int b = 0; b < QB2; ++b) key[i] |= (((q0 >> b) & 1ull) << (2 * b)) | (((q1 >> b) & 1ull) << (2 * b + 1));
+        }
+        return SHADOWTOPO_OK;
+    }
+    constexpr int QB = 21;  // three 21-bit coordinates per 64-bit key
     const uint64_t qmax = (1ull << QB) - 1;
-    for (size_t k = 0; k < dl.size(); ++k) {
+    for (size_t k = 0; k < std::min<size_t>(dl.size(), 3); ++k) {
         double lo = HINF, hi = -HINF;
         for (int32_t i = 0; i < A; ++i) {
             const double d = dl[k][cand[i]];
@@ -2256,7 +2318,7 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
         for (int32_t i = 0; i < A; ++i) {
             const double d = dl[k][cand[i]];
             const uint64_t q = d < HINF ? std::min<uint64_t>(qmax, (uint64_t)((d - lo) / span * (double)qmax)) : qmax;
-            for (int b = 0; b < QB; ++b) key[i] |= ((q >> b) & 1ull) << (b * NL + k);
+            for (int b = 0; b < QB; ++b) key[i] |= ((q >> b) & 1ull) << (b * 3 + k);
         }
     }
     return SHADOWTOPO_OK;
@@ -2266,6 +2328,12 @@ int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->key_ready) return SHADOWTOPO_OK;
     if (eng->A <= KL) {
         eng->h_key.assign((size_t)eng->A, 0);
+        eng->key_ready = true;
+        return SHADOWTOPO_OK;
+    }
+    if (eng->vperm_ready && !eng->h_vkey.empty()) {  // the pruned sweep's vertex keys
+        eng->h_key.resize((size_t)eng->A);
+        for (int32_t i = 0; i < eng->A; ++i) eng->h_key[i] = eng->h_vkey[eng->h_attached[i]];
         eng->key_ready = true;
         return SHADOWTOPO_OK;
     }
@@ -2284,8 +2352,8 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     if (V <= SRS) return SHADOWTOPO_OK;
     std::vector<int32_t> all((size_t)V);
     for (int32_t v = 0; v < V; ++v) all[v] = v;
-    std::vector<uint64_t> key;
-    int rc = locality_keys(eng, s, all, key);
+    std::vector<uint64_t>& key = eng->h_vkey;
+    int rc = locality_keys(eng, s, all, key, 8, true);
     if (rc) return rc;
     std::vector<int32_t> perm(all);
     std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
