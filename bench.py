@@ -242,7 +242,8 @@ def main():
         roofline["valu"] = {"unit": "candidates/s", "achieved": ach, "peak": F64_VALU_OPS / 2,
                             "frac": ach / (F64_VALU_OPS / 2) if ach else None,
                             "candidates_per_launch": cand,
-                            "note": "peak = f64 add+compare per candidate; the kernel filters in f32"}
+                            "note": "peak = f64 add+compare per candidate of the naive V*V*sources sweep; "
+                                    "the kernel filters in f32 and skips pruned chunks unevaluated"}
     if st["dense"] and st["delta_sweeps"]:
         roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if args.dense_variant == 1 else "k_relax_dense_delta_s",
                                     "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],

@@ -89,7 +89,8 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               locality order (Morton order of distances to three landmarks, built on
                                               the first computation), sources batched in locality order, and a wave
                                               skips a 32-row chunk when no lane can pass any of its rows (bound: min
-                                              D32 of the chunk vs max threshold - min W32 of the chunk x tile);
+                                              D32 of the chunk vs max over its columns of threshold - the
+                                              column's min W32 over the chunk);
                                               0 = every chunk filtered, original order. Results are identical. */
 
 /* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every

@@ -670,8 +670,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     // PR (pruned): rows, columns and W32 are in the locality order `perm` (W32 here is the
     // permuted copy W32p[i][j] = W32[perm i][perm j]); a wave skips a chunk outright when no
     // lane can pass any of its rows: min D32 over the chunk's rows (minD, per lane) exceeds
-    // fl32(max_t thr_t - min W32 over the chunk x the wave's columns (minW)).  Every row's
-    // filter bound max_t fl32(thr_t - W32(u, v_t)) is <= that (rounding is monotone), and
+    // max_t fl32(thr_t - minW_t), minW_t = min W32 over the chunk's rows in column v_t.  Every
+    // row's filter bound max_t fl32(thr_t - W32(u, v_t)) is <= that (rounding is monotone), and
     // D32(u) >= min D32, so the skip is exact; minD is taken before the sweep, which is the
     // same as having read those rows' pre-sweep values (later changes reach the delta round
     // through the change masks).
@@ -742,8 +742,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     // PR: permuted row ids of the chunk being fetched (loaded one fetch ahead), and the
     // chunk's skip bounds (md: min D32 per lane and batch, mw: min W32 of the wave's tile)
     int32_t prow[DQ];
-    float mdn[TB], mdc[TB], mwn = 0.f, mwc = 0.f;
-    const int32_t nwt = (V + BW - 1) / BW * 4;  // wave tiles per chunk row of minW
+    float mdn[TB], mdc[TB], mwn[TDT], mwc[TDT];
+    const int32_t ncol = (V + BW - 1) / BW * BW;  // columns per chunk row of minW
     if (PR) {
 #pragma unroll
         for (int i = 0; i < DQ; ++i) prow[i] = perm[vt % nchunks * SRS + (threadIdx.x + i * 256) / (KL / 4)];
@@ -764,7 +764,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
 #pragma unroll
             for (int k = 0; k < TB; ++k)
                 mdn[k] = minD[((size_t)(live[k] ? b0 + k : first) * nchunks + c) * KL + lane];
-            mwn = minW[(size_t)c * nwt + vt * 4 + wave];
+#pragma unroll
+            for (int t = 0; t < TDT; ++t) mwn[t] = minW[(size_t)c * ncol + v0 + t];
 #pragma unroll
             for (int i = 0; i < DQ; ++i) {
                 const int32_t r = (c + 1 == nchunks ? 0 : c + 1) * SRS + (threadIdx.x + i * 256) / (KL / 4);
@@ -795,7 +796,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
         if (PR) {
 #pragma unroll
             for (int k = 0; k < TB; ++k) mdc[k] = mdn[k];
-            mwc = mwn;
+#pragma unroll
+            for (int t = 0; t < TDT; ++t) mwc[t] = mwn[t];
         }
     };
     // PR: chunks in the order vt, vt+1, .., wrapping: the block's own tile (its destinations'
@@ -817,10 +819,10 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
             bool p = false;
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
-                float tm = thr[k][0];
+                float tm = thr[k][0] - mwc[0];
 #pragma unroll
-                for (int t = 1; t < TDT; ++t) tm = fmaxf(tm, thr[k][t]);
-                p |= mdc[k] <= tm - mwc;
+                for (int t = 1; t < TDT; ++t) tm = fmaxf(tm, thr[k][t] - mwc[t]);
+                p |= mdc[k] <= tm;
             }
             run = __ballot(p) != 0;
         }
@@ -962,7 +964,7 @@ __global__ __launch_bounds__(256) void k_permute_w32(const float* __restrict__ W
 }
 
 // minW[c][w] = min of W32p over rows [c*SRS, c*SRS+SRS) x columns [w*tdt, w*tdt+tdt), NaN (no
-// arc) ignored, +inf when the tile has no arc
+// arc) ignored, +inf when the tile has no arc (the pruned sweep uses tdt = 1: one per column)
 __global__ __launch_bounds__(256) void k_min_w32(const float* __restrict__ W32p, int32_t Vp, int32_t nchunks,
                                                  int32_t nwt, int32_t tdt, float* __restrict__ minW) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1826,7 +1828,7 @@ struct shadowtopo_engine {
     // pruned full sweep (OPT_DENSE_PRUNE): vertex locality order and its chunk bounds
     int32_t* d_perm = nullptr;  // [Vp] row/column order (padding maps to itself)
     float* d_W32p = nullptr;    // [Vp][Vp] W32 in that order
-    float* d_minW = nullptr;    // [nchunks][wave tiles] min W32p
+    float* d_minW = nullptr;    // [nchunks][columns] min W32p over each chunk's rows
     float* d_minD = nullptr;    // [nb_cap][nchunks][64] min D32 per chunk and lane
     size_t minD_n = 0;
     bool vperm_ready = false;
@@ -2360,14 +2362,14 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     for (int32_t i = V; i < Vp; ++i) perm.push_back(i);
     constexpr int TDT = 8;  // launch_dense_ft's wave tile
     const int32_t nchunks = (V + SRS - 1) / SRS;
-    const int32_t nwt = (V + 4 * TDT - 1) / (4 * TDT) * 4;
+    const int32_t nwt = (V + 4 * TDT - 1) / (4 * TDT) * 4 * TDT;  // columns
     HIP_TRY(hipMalloc((void**)&eng->d_perm, sizeof(int32_t) * (size_t)Vp));
     HIP_TRY(hipMalloc((void**)&eng->d_W32p, sizeof(float) * (size_t)Vp * Vp));
     HIP_TRY(hipMalloc((void**)&eng->d_minW, sizeof(float) * (size_t)nchunks * nwt));
     HIP_TRY(hipMemcpyAsync(eng->d_perm, perm.data(), sizeof(int32_t) * (size_t)Vp, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_permute_w32, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_W32, eng->d_perm, Vp, eng->d_W32p);
     hipLaunchKernelGGL(k_min_w32, dim3((uint32_t)(((int64_t)nchunks * nwt + 255) / 256)), dim3(256), 0, s,
-                       eng->d_W32p, Vp, nchunks, nwt, TDT, eng->d_minW);
+                       eng->d_W32p, Vp, nchunks, nwt, 1, eng->d_minW);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     eng->vperm_ready = true;
