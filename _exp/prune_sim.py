@@ -19,6 +19,28 @@ def morton(cols):
         for k, qq in enumerate(q):
             key |= ((qq >> np.uint64(b)) & np.uint64(1)) << np.uint64(b * len(q) + k)
     return key
+def hilbert(x, y, order=16):
+    n = 1 << order
+    x = ((x - x.min()) / (x.max() - x.min()) * (n - 1)).astype(np.int64)
+    y = ((y - y.min()) / (y.max() - y.min()) * (n - 1)).astype(np.int64)
+    d = np.zeros(len(x), np.int64)
+    sh = n // 2
+    while sh > 0:
+        rx = (x & sh) > 0; ry = (y & sh) > 0
+        d += sh * sh * ((3 * rx) ^ ry)
+        # rotate
+        m = ~ry
+        fl = m & rx
+        x = np.where(fl, sh - 1 - x, x); y = np.where(fl, sh - 1 - y, y)
+        x, y = np.where(m, y, x), np.where(m, x, y)
+        sh //= 2
+    return d.astype(np.uint64)
+HIL = mode.endswith("h")
+if HIL: mode = mode[:-1]
+_morton = morton
+def morton(cols):
+    if HIL and len(cols) == 2: return hilbert(np.asarray(cols[0], np.float64), np.asarray(cols[1], np.float64))
+    return _morton(cols)
 if mode == "landmark":
     lm = [0]; 
     for _ in range(2):

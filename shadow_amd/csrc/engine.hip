@@ -2201,8 +2201,9 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
 // Morton keys of `cand` (the attached list, or every vertex for the pruned dense sweep's
 // vertex order) from NL farthest-point landmarks chosen among `cand`.  embed2: instead of
 // interleaving the NL distances, project the centred distance vectors on their top two
-// principal axes (landmark MDS) and interleave those two coordinates: for geographic graphs
-// that recovers a near-planar layout, whose 32-vertex chunks are far more compact.
+// principal axes (landmark MDS) and take the Hilbert index of those two coordinates: for
+// geographic graphs that recovers a near-planar layout, whose 32-vertex chunks are far more
+// compact.
 int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32_t>& cand,
                   std::vector<uint64_t>& key, int NL = 3, bool embed2 = false) {
     constexpr double HINF = std::numeric_limits<double>::infinity();
@@ -2300,11 +2301,21 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
             const double span = hi > lo ? hi - lo : 1.0;
             for (int32_t i = 0; i < A; ++i) y[e][i] = (y[e][i] - lo) / span;
         }
-        constexpr int QB2 = 31;
-        const double qm = (double)((1ull << QB2) - 1);
+        // Hilbert index of the two coordinates (no Z-order jumps: 32 consecutive vertices
+        // stay one compact patch)
+        constexpr int QB2 = 24;
+        const uint64_t n = 1ull << QB2;
         for (int32_t i = 0; i < A; ++i) {
-            const uint64_t q0 = (uint64_t)(y[0][i] * qm), q1 = (uint64_t)(y[1][i] * qm);
-            for (int b = 0; b < QB2; ++b) key[i] |= (((q0 >> b) & 1ull) << (2 * b)) | (((q1 >> b) & 1ull) << (2 * b + 1));
+            uint64_t x = (uint64_t)(y[0][i] * (double)(n - 1)), z = (uint64_t)(y[1][i] * (double)(n - 1)), d = 0;
+            for (uint64_t sh = n >> 1; sh > 0; sh >>= 1) {
+                const uint64_t rx = (x & sh) ? 1 : 0, rz = (z & sh) ? 1 : 0;
+                d += sh * sh * ((3 * rx) ^ rz);
+                if (rz == 0) {
+                    if (rx == 1) x = n - 1 - x, z = n - 1 - z;
+                    std::swap(x, z);
+                }
+            }
+            key[i] = d;
         }
         return SHADOWTOPO_OK;
     }
