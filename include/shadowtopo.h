@@ -79,14 +79,15 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               sweep (default 125; 0 = always full sweeps) */
 #define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default) or _DELTA */
 #define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
-#define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Morton
-                                              order of distances to three attached landmarks), 0 = attach order.
+#define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Hilbert
+                                              order of the top two principal axes of the distances to eight
+                                              attached landmarks), 0 = attach order.
                                               Results are identical; only which sources share a wave changes. */
 #define SHADOWTOPO_OPT_DENSE_SEED 11       /* dense round 0: 1 (default) = one fused pass writing every (vertex,
                                               source) state once (k_seed_dense_t), 0 = init, source seed and arc seed
                                               kernels in turn. Results are identical. */
 #define SHADOWTOPO_OPT_DENSE_PRUNE 12      /* f32 dense full sweep: 1 (default) = rows and destinations in a vertex
-                                              locality order (Morton order of distances to three landmarks, built on
+                                              locality order (the same landmark embedding over all vertices, built on
                                               the first computation), sources batched in locality order, and a wave
                                               skips a 32-row chunk when no lane can pass any of its rows (bound: min
                                               D32 of the chunk vs max over its columns of threshold - the

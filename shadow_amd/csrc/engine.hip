@@ -2194,10 +2194,11 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
 // when ANY of its 64 sources has a changed in-neighbour there, so 64 scattered sources make
 // every vertex busy in almost every round (C3: 24 visits per vertex and batch).  Sources
 // that are near each other improve the same vertices in the same rounds.  The key: distances
-// from three attached landmarks (farthest-point: attached[0], then the attached vertex
-// farthest from the landmarks so far), quantised to 21 bits each and bit-interleaved
-// (Morton order), computed once per attached set with the engine's own rounds.  Results do
-// not depend on it: every lane converges to its own source's fixed point.
+// from eight attached landmarks (farthest-point: attached[0], then the attached vertex
+// farthest from the landmarks so far), projected on their top two principal axes and
+// ordered along a Hilbert curve (locality_keys), computed once per attached set with the
+// engine's own rounds (C3: 13.6 ms with three landmarks in Morton order, 12.3 ms so).
+// Results do not depend on it: every lane converges to its own source's fixed point.
 // Morton keys of `cand` (the attached list, or every vertex for the pruned dense sweep's
 // vertex order) from NL farthest-point landmarks chosen among `cand`.  embed2: instead of
 // interleaving the NL distances, project the centred distance vectors on their top two
@@ -2350,7 +2351,7 @@ int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
         eng->key_ready = true;
         return SHADOWTOPO_OK;
     }
-    int rc = locality_keys(eng, s, eng->h_attached, eng->h_key);
+    int rc = locality_keys(eng, s, eng->h_attached, eng->h_key, 8, true);
     if (rc) return rc;
     eng->key_ready = true;
     return SHADOWTOPO_OK;
