@@ -57,6 +57,20 @@ elif mode.startswith("pca"):
     ev, evec = np.linalg.eigh(X.T @ X)
     Y = X @ evec[:, ::-1][:, :nc]
     vkey = morton([Y[:, i] for i in range(nc)])
+elif mode == "lmds":
+    nl = 8
+    lm = [0]
+    while len(lm) < nl:
+        m = np.min(np.stack([np.where(np.isfinite(W[l]), W[l], 0) for l in lm]), 0); m[lm] = -1; lm.append(int(np.argmax(m)))
+    X = np.stack([np.where(np.isfinite(W[l]), W[l], np.nan).astype(np.float64) for l in lm], 1)
+    X = np.where(np.isnan(X), np.nanmean(X, 0), X) ** 2
+    Dl = X[lm]  # landmark x landmark squared distances
+    Dl = (Dl + Dl.T) / 2
+    H = np.eye(nl) - 1.0 / nl
+    Bm = -0.5 * H @ Dl @ H
+    ev, evec = np.linalg.eigh(Bm)
+    Y = X @ evec[:, ::-1][:, :2]
+    vkey = morton([Y[:, 0], Y[:, 1]])
 else:
     r1 = np.random.default_rng(1); pts = r1.random((V, 2)); vkey = morton([pts[:, 0], pts[:, 1]])
 perm = np.argsort(vkey, kind="stable")
