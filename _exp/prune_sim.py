@@ -47,7 +47,7 @@ if mode == "landmark":
         m = np.min(np.stack([np.where(np.isfinite(W[l]), W[l], 0) for l in lm]), 0); lm.append(int(np.argmax(m)))
     vkey = morton([W[l].astype(np.float64) for l in lm])
 elif mode.startswith("pca"):
-    nl = 8; nc = int(mode[3:] or 2)
+    nl = int(__import__("os").environ.get("NL", 8)); nc = int(mode[3:] or 2)
     lm = [0]
     while len(lm) < nl:
         m = np.min(np.stack([np.where(np.isfinite(W[l]), W[l], 0) for l in lm]), 0); m[lm] = -1; lm.append(int(np.argmax(m)))
