@@ -64,6 +64,21 @@ def test_c2_geometric_full_matrix():
     assert st["dense"] == 1 and st["replayed_sources"] == 0
 
 
+def test_c2_pruned_equals_unpruned_full_matrix():
+    """The whole 1000x1000 bench matrix from the pruned sweep (default) and from the
+    unpruned one, bit for bit: every pair of the headline workload, not a sample."""
+    g = synth.geometric_complete_ish(V=10_000, A=1_000)
+    mats = []
+    for prune in (1, 0):
+        eng = E.Engine.from_synth(g)
+        eng.set_option(E.OPT_DENSE_PRUNE, prune)
+        eng.set_attached(g.attached)
+        mats.append(eng.compute_rows())
+        eng.close()
+    for name, x, y in zip(("latency", "reliability", "hops", "kind"), *mats):
+        assert_bitexact(name, x, y)
+
+
 def test_c2_geometric_f64_kernels():
     g = synth.geometric_complete_ish(V=10_000, A=1_000)
     st = _run(g, 0, 192, sample=[5, 130], dense_variant=E.DENSE_F64)
