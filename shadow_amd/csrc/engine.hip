@@ -654,6 +654,7 @@ __device__ __forceinline__ float f32_thr(double bc) {
 //    exactly in f64 (D and W from global memory) in row order -- the same lexicographic
 //    minimum and tie flag as a sequential scan.
 constexpr int SRS = 32;  // rows per LDS chunk
+constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FTDT; 4 was slower: 4.63 vs 3.8 ms on C2)
 
 template <int TDT, int XR, int TB, bool PR>
 __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
@@ -746,7 +747,7 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     const int32_t ncol = (V + BW - 1) / BW * BW;  // columns per chunk row of minW
     if (PR) {
 #pragma unroll
-        for (int i = 0; i < DQ; ++i) prow[i] = perm[vt % nchunks * SRS + (threadIdx.x + i * 256) / (KL / 4)];
+        for (int i = 0; i < DQ; ++i) prow[i] = perm[(int32_t)((int64_t)vt * BW / SRS % nchunks) * SRS + (threadIdx.x + i * 256) / (KL / 4)];
     }
     auto fetch = [&](int32_t u0) {
 #pragma unroll
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     // PR: chunks in the order vt, vt+1, .., wrapping: the block's own tile (its destinations'
     // nearest rows) first, which gives unreached and arc-less (t, s) pairs a tight threshold
     // before the far chunks are tested
-    const int32_t c0 = PR ? vt % nchunks : 0;
+    const int32_t c0 = PR ? (int32_t)((int64_t)vt * BW / SRS % nchunks) : 0;  // the chunk holding the tile
     fetch(c0 * SRS);
     stash(0);
     advance();
@@ -2014,7 +2015,7 @@ int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
 template <int TB>
 hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
                            const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
-    constexpr int TDT = 8, XR = 2;
+    constexpr int TDT = FTDT, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
     const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
@@ -2372,7 +2373,7 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     std::vector<int32_t> perm(all);
     std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
     for (int32_t i = V; i < Vp; ++i) perm.push_back(i);
-    constexpr int TDT = 8;  // launch_dense_ft's wave tile
+    constexpr int TDT = FTDT;  // launch_dense_ft's wave tile
     const int32_t nchunks = (V + SRS - 1) / SRS;
     const int32_t nwt = (V + 4 * TDT - 1) / (4 * TDT) * 4 * TDT;  // columns
     HIP_TRY(hipMalloc((void**)&eng->d_perm, sizeof(int32_t) * (size_t)Vp));
