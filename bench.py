@@ -58,8 +58,51 @@ def build_workload(config, world, scale):
 
 
 def algorithmic_bytes_per_source(V, n_arcs, A):
-    """B_src = 4(V+1) + 12*E_arc + 12*V + 20*A"""
+    """SURVEY.md 8d's per-source figure: B_src = 4(V+1) + 12*E_arc + 12*V + 20*A (kept for
+    reference; it prices a private CSR sweep per source, which the batched kernels never do)"""
     return 4 * (V + 1) + 12 * n_arcs + 12 * V + 20 * A
+
+
+STATE_BYTES = 36  # per changed (vertex, source): D f64 + D32 f32 + BDU f64 + P i32 + H u32 + R f64
+
+
+def dense_sweep_compulsory(Vp, st):
+    """Compulsory HBM bytes of the f32 dense full sweep (k_relax_dense_f), per launch, for
+    the batched formulation: the W32 table once per launch (every batch of
+    the launch filters against it), and per batch its D32 rows (4 B), the f64 distances the
+    thresholds start from (8 B), the per-chunk D32 minima and the change masks; plus the
+    state of every (vertex, source) pair the sweep changed.  Averaged over the launches."""
+    L = max(1, st["full_sweeps"])
+    nchunks = -(-Vp // 32)
+    per_batch = Vp * 64 * (4 + 8) + nchunks * 64 * 4 + Vp * 8
+    total = L * Vp * Vp * 4 + st["full_batches"] * per_batch + st["full_changes"] * STATE_BYTES
+    return total / L
+
+
+def sparse_step_compulsory(V, n_arcs, sources):
+    """Compulsory HBM bytes of one matrix build on a sparse graph, batched Dijkstra-
+    equivalent: per 64-source batch every in-arc's tail distances once (64 x 8 B), the CSR
+    once (row pointer 8 B, tail 4 B + latency 8 B per arc) and every (vertex, source) state
+    written once."""
+    nb = -(-sources // 64)
+    return nb * (n_arcs * 64 * 8 + (V + 1) * 8 + n_arcs * 12 + V * 64 * STATE_BYTES)
+
+
+VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions/s: 1024 SIMDs, one per 4 cycles at 2.4 GHz
+
+
+def load_counters(key):
+    """this round's rocprofv3 counter summary for the same bench command (scripts/gpu_roofline.sh
+    -> profiles/roofline_counters.json): HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE,
+    separate passes) and wave64 VALU instructions per launch (SQ_INSTS_VALU scaled by the
+    known wave count over SQ_WAVES) of the dominant kernel"""
+    p = os.path.join(ROOT, "profiles", "roofline_counters.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get(key)
+    except Exception:
+        return None
 
 
 def cpu_baseline(g, n_sources, budget_s=20.0, all_cores=16):
@@ -93,17 +136,6 @@ def cpu_baseline(g, n_sources, budget_s=20.0, all_cores=16):
     return out
 
 
-def load_traffic(workload_key):
-    p = os.path.join(ROOT, "profiles", "relax_traffic.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        d = json.load(open(p)).get(workload_key)
-        return d["bytes_per_launch"] if d else None
-    except Exception:
-        return None
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,12 +156,25 @@ def main():
     ap.add_argument("--csr-variant", type=int, default=1, help="1 = full recomputation (default), 0 = delta rounds")
     args = ap.parse_args()
 
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one rank per GPU: start them ourselves (a child launcher, before this process
+        # touches the GPU) and report its exit status
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        log("launching: " + " ".join(cmd))
+        raise SystemExit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to run a different rank count")
+
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -146,7 +191,7 @@ def main():
     A = len(g.attached)
     r0, r1, per = shard.shard_rows(A, world, rank)
     log(f"[rank {rank}] workload {desc}: E={g.m} built in {time.perf_counter() - t:.1f}s; rows [{r0},{r1})")
-    t = time.perf_counter()
+    t_cold = t = time.perf_counter()
     eng = E.Engine.from_synth(g, device=local)
     eng.set_attached(g.attached)
     eng.set_option(E.OPT_TIMING, 1)
@@ -190,8 +235,11 @@ def main():
         for w in works:
             w.wait()
 
-    for _ in range(args.warmup):
+    for i in range(max(1, args.warmup)):
         step()
+        if i == 0:  # engine creation -> first finished matrix rows on the device
+            torch.cuda.synchronize(dev)
+            cold_start_ms = (time.perf_counter() - t_cold) * 1e3
     torch.cuda.synchronize(dev)
     eng.reset_stats()
     if world > 1:
@@ -213,37 +261,43 @@ def main():
     value = total_sources * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel, from live HIP events on its stream: the dense full
-    # sweep (k_relax_dense) on complete-ish graphs, the CSR relax (k_relax) otherwise.  One
-    # launch relaxes every source of the batch group in flight, so its algorithmic bytes are
-    # SURVEY.md 8d's B_src times the sources it covers.
-    B_src = algorithmic_bytes_per_source(g.n, st["n_arcs"], A)
+    # roofline of the dominant kernel, timed with HIP events on the engine's stream around
+    # every launch: the f32 dense full sweep (k_relax_dense_f) on complete-ish graphs, the
+    # CSR relax round (k_relax) otherwise.  achieved = that kernel's compulsory bytes per
+    # launch / its average launch time.
     if st["dense"]:
         kname = "k_relax_dense" if args.dense_variant == 1 else "k_relax_dense_f"
         launches, kms = max(1, st["full_sweeps"]), st["full_ms"]
+        Vp = -(-g.n // 64) * 64
+        bytes_per_launch = dense_sweep_compulsory(Vp, st)
+        batches_per_launch = st["full_batches"] / launches
     else:
         kname, launches, kms = "k_relax", max(1, st["relax_launches"]), st["relax_ms"]
-    bytes_per_launch = rows * args.steps * B_src / launches
+        bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * args.steps / launches
+        batches_per_launch = st["relax_batches"] / launches
     avg_launch_s = kms / launches / 1e3
     achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
-    traffic = load_traffic(f"{args.config}@{args.scale}@{world}")
+    ckey = f"{args.config}@{args.scale}@{world}"
+    cnt = load_counters(ckey)
+    if cnt and (cnt.get("kernel") != kname or abs(cnt.get("batches_per_launch", -1) - batches_per_launch) > 0.5):
+        log(f"counter record {ckey} is for another launch shape ({cnt.get('kernel')}, "
+            f"{cnt.get('batches_per_launch')} batches); not used")
+        cnt = None
+    traffic = cnt["hbm_bytes_per_launch"] if cnt else None
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "kernel": kname, "avg_launch_ms": avg_launch_s * 1e3,
-                "launches_per_step": launches / args.steps,
-                "algorithmic_bytes_per_source": B_src, "algorithmic_bytes_per_launch": bytes_per_launch,
-                "measured_hbm_gbs": (traffic / avg_launch_s / 1e9) if (traffic and avg_launch_s > 0) else None}
-    if st["dense"]:
-        # the dense sweep is VALU-bound, not HBM-bound: price it also against the f64 VALU
-        # roofline of a naive exact kernel (one f64 add + one f64 compare per candidate
-        # (u, v, source); MI355X_MICROARCH.md: 78.6 TF/s f64 vector = 39.3e12 ops/s)
-        cand = float(g.n) * float(g.n) * rows * args.steps / launches
-        ach = cand / avg_launch_s if avg_launch_s > 0 else None
-        roofline["valu"] = {"unit": "candidates/s", "achieved": ach, "peak": F64_VALU_OPS / 2,
-                            "frac": ach / (F64_VALU_OPS / 2) if ach else None,
-                            "candidates_per_launch": cand,
-                            "note": "peak = f64 add+compare per candidate of the naive V*V*sources sweep; "
-                                    "the kernel filters in f32 and skips pruned chunks unevaluated"}
+                "launches_per_step": launches / args.steps, "batches_per_launch": batches_per_launch,
+                "compulsory_bytes_per_launch": bytes_per_launch,
+                "traffic_over_compulsory": (traffic / bytes_per_launch) if traffic else None,
+                "measured_hbm_gbs": (traffic / avg_launch_s / 1e9) if (traffic and avg_launch_s > 0) else None,
+                "counters": (cnt.get("source") if cnt else None)}
+    if cnt and cnt.get("valu_insts_per_launch") and avg_launch_s > 0:
+        ach = cnt["valu_insts_per_launch"] / avg_launch_s
+        roofline["valu"] = {"unit": "wave64 VALU instructions/s", "achieved": ach, "peak": VALU_PEAK,
+                            "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
+                            "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
+                                    "waves / SQ_WAVES; peak = one VALU issue per 4 cycles per SIMD at 2.4 GHz"}
     if st["dense"] and st["delta_sweeps"]:
         roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if args.dense_variant == 1 else "k_relax_dense_delta_s",
                                     "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
@@ -290,7 +344,7 @@ def main():
                        "visits_per_step": st["visits"] / args.steps, "changes_per_step": st["changes"] / args.steps,
                        "full_sweeps_per_step": st["full_sweeps"] / args.steps,
                        "delta_sweeps_per_step": st["delta_sweeps"] / args.steps,
-                       "host_buffers_ms": host_ms,
+                       "host_buffers_ms": host_ms, "cold_start_ms": cold_start_ms,
                        "host_buffers_source_paths_per_s": (rows / host_ms * 1e3) if host_ms else None},
         }
         print(json.dumps(out), flush=True)

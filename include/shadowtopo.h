@@ -94,6 +94,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               column's min W32 over the chunk);
                                               0 = every chunk filtered, original order. Results are identical. */
 
+#define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
+                                              engine may take (default 1000); engines sharing one device split it */
+
 /* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every
  * in-arc of every active vertex; DELTA folds only the in-neighbours whose state changed for
  * the lane's source into the recorded lexicographic state (fewer row bytes, more
@@ -127,6 +130,10 @@ typedef struct shadowtopo_stats {
     int64_t delta_sweeps;    /* dense: change-mask (delta) relax launches */
     double full_ms;          /* OPT_TIMING: HIP-event time of the dense full sweeps (k_relax_dense) */
     double delta_ms;         /* OPT_TIMING: HIP-event time of the delta rounds (k_relax_dense_delta) */
+    /* launch shapes, for the per-launch rooflines (bench.py) */
+    int64_t full_batches;    /* dense: batches swept by full-sweep launches (summed over launches) */
+    int64_t full_changes;    /* dense: (vertex, source) pairs those full sweeps changed */
+    int64_t relax_batches;   /* sparse: batches in flight, summed over relax launches */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

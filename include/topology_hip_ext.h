@@ -30,6 +30,7 @@ typedef struct topology_hip_info {
     double compute_seconds;   /* wall time of the eager attached-pair computation */
     int64_t compute_count;    /* sources computed ("shortest paths with dijkstra") */
     int32_t n_devices;        /* GPUs the attached-pair rows are sharded over */
+    int32_t compute_failed;   /* 1 after a failed computation: queries fail without retrying it */
 } topology_hip_info;
 
 /* HIP device the engine uses (default: $SHADOWTOPO_DEVICE or 0); before the first query */

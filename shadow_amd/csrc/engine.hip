@@ -638,7 +638,9 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 __device__ __forceinline__ float f32_thr(double bc) {
     if (!(bc < dmax())) return __int_as_float(0x7f800000);  // unreached: any finite candidate passes
     const float r = __double2float_ru(bc);
-    if (!(r < __int_as_float(0x7f800000))) return r;
+    // 4 ulps up, saturating at +inf: past FLT_MAX the bit pattern would be a NaN, which
+    // never passes a filter (a lane would silently lose its candidates)
+    if (!(r < __int_as_float(0x7f7ffffc))) return __int_as_float(0x7f800000);
     return __int_as_float(__float_as_int(r) + 4);
 }
 
@@ -1883,6 +1885,7 @@ struct shadowtopo_engine {
     int32_t opt_csr_variant = 1;    // SHADOWTOPO_CSR_FULL (default) or SHADOWTOPO_CSR_DELTA
     int32_t opt_dense_tb = 1;       // batches per wave in the f32-filtered full sweep (1, 2 or 4)
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
+    int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
@@ -1994,7 +1997,8 @@ int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
-    const double budget = std::max(24.0e9, 0.4 * ((double)free_b + held));
+    // engines sharing one device (SHADOWTOPO_DEVICES listing it twice) split the budget
+    const double budget = std::max(24.0e9, 0.4 * ((double)free_b + held)) * eng->opt_hbm_share / 1000.0;
     const double cap = eng->dense ? 16.0 : 256.0;
     const int32_t nb = (int32_t)std::max(1.0, std::min(cap, std::floor(budget / per_batch)));
     return std::min(nb, need);
@@ -2101,6 +2105,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int64_t nblocks_delta = (int64_t)8 * nbg * ((nvc + 7) / 8);
     const int32_t thresh = (int32_t)std::min<int64_t>(
         0x7f7f7f7e, (int64_t)V * KL * eng->opt_delta_permille / 1000);
+    std::vector<uint8_t> full_b;  // dense: batches the full sweep covers this round
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
@@ -2115,8 +2120,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             bool& any_full = round_full;
             bool& any_delta = round_delta;
             any_full = any_delta = false;
+            full_b.assign((size_t)nbg, 0);
             for (int32_t b = 0; b < nbg; ++b) {
-                any_full |= eng->h_cnt[b] > thresh;
+                full_b[b] = eng->h_cnt[b] > thresh;
+                any_full |= full_b[b] != 0;
                 any_delta |= eng->h_cnt[b] > 0 && eng->h_cnt[b] <= thresh;
             }
             const int32_t par = (int32_t)(round & 1);
@@ -2129,6 +2136,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 else
                     HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s));
                 eng->st.full_sweeps++;
+                for (int32_t b = 0; b < nbg; ++b) eng->st.full_batches += full_b[b];
             }
             if (any_full && any_delta && eng->opt_timing) HIP_TRY(hipEventRecord(eng->evm2, s));
             if (any_delta) {
@@ -2143,10 +2151,12 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 eng->st.delta_sweeps++;
             }
         } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FULL) {
+            eng->st.relax_batches += nbg;
             hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
                                g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
                                eng->d_prof);
         } else {
+            eng->st.relax_batches += nbg;
             hipLaunchKernelGGL(k_relax_delta, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
                                eng->d_prof);
@@ -2176,7 +2186,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             }
         }
         int64_t changed = 0;
-        for (int32_t b = 0; b < nbg; ++b) changed += eng->h_cnt[b];
+        for (int32_t b = 0; b < nbg; ++b) {
+            changed += eng->h_cnt[b];
+            if (round_full && full_b[b]) eng->st.full_changes += eng->h_cnt[b];
+        }
         if (eng->dense && eng->opt_profile) eng->st.changes += changed;  // changed (vertex, source) pairs
         if (changed == 0) break;
     }
@@ -2876,6 +2889,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_SEED:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");
             eng->opt_dense_seed = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_HBM_SHARE:
+            if (value < 1 || value > 1000) return fail(SHADOWTOPO_EINVAL, "HBM share must be in [1, 1000] per mille");
+            eng->opt_hbm_share = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_PERMILLE:
             if (value < 0 || value > 1000) return fail(SHADOWTOPO_EINVAL, "delta per mille must be in [0, 1000]");

@@ -141,9 +141,54 @@ typedef struct matrix {
     double* rel;
     uint32_t* hops;
     uint8_t* kind;
-    _Atomic(uint64_t*)* cnt_rows; /* lazily allocated per row, A entries each */
-    struct matrix* next;          /* retired matrices (readers may still hold them) */
+    struct matrix* next; /* retired matrices (readers may still hold them) */
 } matrix;
+
+/* immutable IP -> vertex snapshot for the per-packet lookups: published
+ * with a release store on the first query after an attach / detach, read with no lock */
+typedef struct ip_snap {
+    uint64_t version;
+    iptable t;
+    struct ip_snap* next; /* retired snapshots (readers may still hold them) */
+} ip_snap;
+
+/* ascending vertex list of one attach queue and how many of its vertices carry a usable IP */
+typedef struct {
+    int32_t* v;
+    int32_t n, cap, nips;
+} vlist;
+
+/* string (lowercased) -> vlist */
+typedef struct {
+    char** keys;
+    int32_t* vals;
+    size_t cap, n;
+    vlist* lists;
+    int32_t nlists, caplists;
+} strmap;
+
+/* uint32 -> vlist */
+typedef struct {
+    uint32_t* keys;
+    int32_t* vals; /* list index + 1, 0 = empty */
+    size_t cap, n;
+    vlist* lists;
+    int32_t nlists, caplists;
+} u32map;
+
+/* attach hint indexes, built on the first attach */
+typedef struct {
+    in_addr_t* vip;      /* [V] address_stringToIP of the "ip" value ("" when absent): the LPM key */
+    uint8_t* usable;     /* [V] ip attribute present and not NONE / ANY / LOOPBACK */
+    int32_t nips_all;    /* vertices with a usable IP */
+    strmap city, country, geo, type, city_type, country_type, geo_type;
+    u32map exact;        /* usable IP -> vertices */
+    int32_t (*trie)[2];  /* binary trie over vip[] (bit 31 first); leaves hold the first vertex */
+    int32_t* leaf;
+    int32_t ntrie, captrie;
+} attach_index;
+
+#define CTILE 64 /* packet counters: 64 x 64 tiles, allocated on first touch */
 
 struct _Topology {
     uint32_t magic;
@@ -155,15 +200,25 @@ struct _Topology {
     double* eloss; /* edge packetloss */
     double* vloss; /* vertex packetloss, NaN = absent */
     const gml_attr *a_ip, *a_city, *a_country, *a_geo, *a_type, *a_bwdown, *a_bwup, *a_asn, *a_vloss;
-    pthread_rwlock_t ip_lock;
+    pthread_rwlock_t ip_lock; /* writers: attach / detach; readers: snapshot builds */
     iptable ips;
-    int32_t* att_index; /* [V] attached index or -1 (verticesWithAttachedHosts) */
+    _Atomic uint64_t ip_version; /* bumped by every attach / detach */
+    _Atomic(ip_snap*) snap;
+    ip_snap* snap_retired;
+    pthread_mutex_t snap_lock;
+    _Atomic int32_t* att_index; /* [V] attached index or -1 (verticesWithAttachedHosts) */
     int32_t* attached;
     int32_t n_att, cap_att;
+    pthread_mutex_t idx_lock;
+    attach_index* aidx;
     pthread_mutex_t compute_lock;
     _Atomic(matrix*) mat;
     matrix* retired;
-    pthread_mutex_t cnt_lock;
+    int compute_failed; /* a failed computation is not retried (queries fail fast) */
+    /* per-pair packet counters, keyed by attached indices (stable across late attaches):
+     * crow[i / 64] -> [ctd] tile pointers -> 64 x 64 u64 (count + 1 once touched) */
+    int32_t ctd;
+    _Atomic(_Atomic(uint64_t*)*)* crow;
     shadowtopo_engine* eng;  /* engine on devices[0] */
     int32_t device;
     /* in-process multi-GPU: one engine per device, each computing a
@@ -177,7 +232,6 @@ struct _Topology {
     int64_t compute_count;
     int64_t self_count;
 };
-
 /* ------------------------------------------------------------ attribute helpers
  * _topology_find{Vertex,Edge,Graph}Attribute{String,Double} (topology.c:284-369): a value
  * counts only if the attribute exists (exact name) and is non-empty / not NaN. */
@@ -536,6 +590,12 @@ static int check_edges(Topology* top) {
                 st_warning("required attribute 'latency' on edge %li (from '%s' to '%s') is non-positive", (long)e,
                            from, to);
                 all_ok = 0;
+            } else if (isinf(x)) {
+                /* deviation: the reference accepts +inf here (topology.c:1066-1082); the engine
+                 * needs finite latencies, so the graph fails at load time, not at the first query */
+                st_warning("required attribute 'latency' on edge %li (from '%s' to '%s') is infinite", (long)e, from,
+                           to);
+                all_ok = 0;
             }
         } else {
             st_warning("required attribute 'latency' on edge %li (from '%s' to '%s') is missing or NAN", (long)e,
@@ -593,11 +653,103 @@ static void free_matrix(matrix* m) {
     free(m->rel);
     free(m->hops);
     free(m->kind);
-    if (m->cnt_rows) {
-        for (int32_t i = 0; i < m->A; i++) free(atomic_load(&m->cnt_rows[i]));
-        free((void*)m->cnt_rows);
-    }
     free(m);
+}
+
+static void vl_push(vlist* l, int32_t v, int usable) {
+    if (l->n == l->cap) {
+        l->cap = l->cap ? l->cap * 2 : 8;
+        l->v = realloc(l->v, sizeof(int32_t) * (size_t)l->cap);
+    }
+    l->v[l->n++] = v;
+    if (usable) l->nips++;
+}
+
+static void strmap_free(strmap* m) {
+    for (size_t i = 0; i < m->cap; i++) free(m->keys[i]);
+    free(m->keys);
+    free(m->vals);
+    for (int32_t k = 0; k < m->nlists; k++) free(m->lists[k].v);
+    free(m->lists);
+}
+
+static void free_index(attach_index* x) {
+    if (!x) return;
+    free(x->vip);
+    free(x->usable);
+    strmap* maps[] = {&x->city, &x->country, &x->geo, &x->type, &x->city_type, &x->country_type, &x->geo_type};
+    for (size_t k = 0; k < sizeof maps / sizeof maps[0]; k++) strmap_free(maps[k]);
+    free(x->exact.keys);
+    free(x->exact.vals);
+    for (int32_t k = 0; k < x->exact.nlists; k++) free(x->exact.lists[k].v);
+    free(x->exact.lists);
+    free(x->trie);
+    free(x->leaf);
+    free(x);
+}
+
+static void free_snap(ip_snap* s) {
+    if (!s) return;
+    free(s->t.keys);
+    free(s->t.vals);
+    free(s->t.state);
+    free(s);
+}
+
+/* counter cell of attached pair (i, j): one per cached Path, i.e. per unordered pair in
+ * undirected graphs (the reference stores one direction, topology.c:1312-1318); the
+ * stored value is count + 1 so a touched pair is non-zero (the teardown log lists touched
+ * pairs).  Tiles are allocated on first touch with a compare-and-swap, no lock. */
+static _Atomic uint64_t* counter_slot(Topology* top, int32_t i, int32_t j) {
+    if (!top->directed && j < i) {
+        int32_t t = i;
+        i = j;
+        j = t;
+    }
+    const int32_t ti = i / CTILE, tj = j / CTILE;
+    if (ti >= top->ctd || tj >= top->ctd) return NULL;
+    _Atomic(uint64_t*)* row = atomic_load_explicit(&top->crow[ti], memory_order_acquire);
+    if (!row) {
+        _Atomic(uint64_t*)* fresh = calloc((size_t)top->ctd, sizeof(*fresh));
+        if (!fresh) return NULL;
+        _Atomic(uint64_t*)* expect = NULL;
+        if (atomic_compare_exchange_strong_explicit(&top->crow[ti], &expect, fresh, memory_order_acq_rel,
+                                                    memory_order_acquire))
+            row = fresh;
+        else {
+            free((void*)fresh);
+            row = expect;
+        }
+    }
+    uint64_t* tile = atomic_load_explicit(&row[tj], memory_order_acquire);
+    if (!tile) {
+        uint64_t* fresh = calloc(CTILE * CTILE, sizeof(uint64_t));
+        if (!fresh) return NULL;
+        uint64_t* expect = NULL;
+        if (atomic_compare_exchange_strong_explicit(&row[tj], &expect, fresh, memory_order_acq_rel,
+                                                    memory_order_acquire))
+            tile = fresh;
+        else {
+            free(fresh);
+            tile = expect;
+        }
+    }
+    return (_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)];
+}
+
+static uint64_t counter_peek(const Topology* top, int32_t i, int32_t j) {
+    if (!top->directed && j < i) {
+        int32_t t = i;
+        i = j;
+        j = t;
+    }
+    const int32_t ti = i / CTILE, tj = j / CTILE;
+    if (!top->crow || ti >= top->ctd || tj >= top->ctd) return 0;
+    _Atomic(uint64_t*)* row = atomic_load_explicit(&top->crow[ti], memory_order_acquire);
+    if (!row) return 0;
+    uint64_t* tile = atomic_load_explicit(&row[tj], memory_order_acquire);
+    if (!tile) return 0;
+    return atomic_load_explicit((_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)], memory_order_relaxed);
 }
 
 static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix* m, int32_t i, int32_t j,
@@ -615,17 +767,24 @@ static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix
 void topology_free(Topology* top) {
     if (!top) return;
     matrix* m = atomic_load(&top->mat);
-    if (m && m->cnt_rows && shadowtopo_log_enabled(ST_INFO)) {
-        /* _topology_logAllCachedPaths (topology.c:1929-1967): every pair a query touched */
+    if (m && top->crow && shadowtopo_log_enabled(ST_INFO)) {
+        /* _topology_logAllCachedPaths (topology.c:1929-1967): every pair a query touched,
+         * with every packet counted since the first query (late attaches included) */
         char buf[512];
-        for (int32_t i = 0; i < m->A; i++) {
-            uint64_t* row = atomic_load(&m->cnt_rows[i]);
+        for (int32_t ti = 0; ti < top->ctd; ti++) {
+            _Atomic(uint64_t*)* row = atomic_load(&top->crow[ti]);
             if (!row) continue;
-            for (int32_t j = 0; j < m->A; j++) {
-                if (!row[j]) continue;
-                int32_t s = top->attached[i], t = top->attached[j];
-                st_info("Found path %s%s%s in cache: %s", vid(top, s), top->directed ? "->" : "<->", vid(top, t),
-                        path_string(top, s, t, m, i, j, row[j] - 1, buf, sizeof buf));
+            for (int32_t tj = 0; tj < top->ctd; tj++) {
+                uint64_t* tile = atomic_load(&row[tj]);
+                if (!tile) continue;
+                for (int32_t k = 0; k < CTILE * CTILE; k++) {
+                    if (!tile[k]) continue;
+                    int32_t i = ti * CTILE + k / CTILE, j = tj * CTILE + k % CTILE;
+                    if (i >= m->A || j >= m->A) continue;
+                    int32_t s = top->attached[i], t = top->attached[j];
+                    st_info("Found path %s%s%s in cache: %s", vid(top, s), top->directed ? "->" : "<->",
+                            vid(top, t), path_string(top, s, t, m, i, j, tile[k] - 1, buf, sizeof buf));
+                }
             }
         }
     }
@@ -638,13 +797,29 @@ void topology_free(Topology* top) {
         free_matrix(r);
         r = n;
     }
+    if (top->crow) {
+        for (int32_t ti = 0; ti < top->ctd; ti++) {
+            _Atomic(uint64_t*)* row = atomic_load(&top->crow[ti]);
+            if (!row) continue;
+            for (int32_t tj = 0; tj < top->ctd; tj++) free(atomic_load(&row[tj]));
+            free((void*)row);
+        }
+        free((void*)top->crow);
+    }
+    free_snap(atomic_load(&top->snap));
+    for (ip_snap* r = top->snap_retired; r;) {
+        ip_snap* n = r->next;
+        free_snap(r);
+        r = n;
+    }
+    free_index(top->aidx);
     for (int32_t k = 0; k < top->ndev; k++)
         if (top->engs[k]) shadowtopo_destroy(top->engs[k]);
     top->eng = NULL;
     free(top->ips.keys);
     free(top->ips.vals);
     free(top->ips.state);
-    free(top->att_index);
+    free((void*)top->att_index);
     free(top->attached);
     free(top->elat);
     free(top->eloss);
@@ -652,9 +827,18 @@ void topology_free(Topology* top) {
     gml_free(top->gml);
     pthread_rwlock_destroy(&top->ip_lock);
     pthread_mutex_destroy(&top->compute_lock);
-    pthread_mutex_destroy(&top->cnt_lock);
+    pthread_mutex_destroy(&top->snap_lock);
+    pthread_mutex_destroy(&top->idx_lock);
     top->magic = 0;
     free(top);
+}
+
+/* SHADOWTOPO_DEVICES / topology_hip_set_devices: engines that share a device split its
+ * batch-slot HBM budget (shadowtopo.h SHADOWTOPO_OPT_HBM_SHARE) */
+static int32_t device_sharers(const Topology* top, int32_t k) {
+    int32_t n = 0;
+    for (int32_t j = 0; j < top->ndev; j++) n += top->devices[j] == top->devices[k];
+    return n;
 }
 
 Topology* topology_new(const char* graphPath) {
@@ -664,7 +848,10 @@ Topology* topology_new(const char* graphPath) {
     top->magic = TOPO_MAGIC;
     pthread_rwlock_init(&top->ip_lock, NULL);
     pthread_mutex_init(&top->compute_lock, NULL);
-    pthread_mutex_init(&top->cnt_lock, NULL);
+    pthread_mutex_init(&top->snap_lock, NULL);
+    pthread_mutex_init(&top->idx_lock, NULL);
+    atomic_store(&top->ip_version, 1);
+    atomic_store(&top->snap, NULL);
     const char* dev = getenv("SHADOWTOPO_DEVICE");
     top->device = dev ? atoi(dev) : 0;
     top->ndev = 1;
@@ -721,36 +908,255 @@ Topology* topology_new(const char* graphPath) {
                     "graphml file");
         return NULL;
     }
-    top->att_index = malloc(sizeof(int32_t) * (size_t)(top->V > 0 ? top->V : 1));
-    for (int32_t v = 0; v < top->V; v++) top->att_index[v] = -1;
+    top->att_index = malloc(sizeof(*top->att_index) * (size_t)(top->V > 0 ? top->V : 1));
+    for (int32_t v = 0; v < top->V; v++) atomic_init(&top->att_index[v], -1);
+    top->ctd = (top->V + CTILE - 1) / CTILE;
+    top->crow = calloc((size_t)(top->ctd > 0 ? top->ctd : 1), sizeof(*top->crow));
     return top;
 }
-
-/* ------------------------------------------------------------ attach */
-typedef struct {
-    int32_t* v;
-    int32_t n, cap;
-} ivec;
-
-static void iv_push(ivec* q, int32_t x) {
-    if (q->n == q->cap) {
-        q->cap = q->cap ? q->cap * 2 : 64;
-        q->v = realloc(q->v, sizeof(int32_t) * (size_t)q->cap);
-    }
-    q->v[q->n++] = x;
-}
-
+/* ------------------------------------------------------------ attach
+ * _topology_findAttachmentVertex + its hook (topology.c:2094-2369) scan every vertex per
+ * host with five string compares (5e4 hosts x 1e6 vertices at C5).  Here the same
+ * candidate queues come from indexes built once, on the first attach:
+ * the ASCII-lowercased citycode / countrycode / geocode / type values and the three
+ * (code, type) pairs map to ascending vertex lists with their usable-IP counts, the usable
+ * vertex IPs map to their vertices (the exact-IP rule), and a binary trie over every
+ * vertex's parsed IP answers the longest-prefix rule over the whole vertex set.  Queue
+ * order (ascending vertex index), the usable-IP counts, the ~(a^b) match with its
+ * 'bestMatch == 0' quirk and the round((n-1)*r) pick are the reference's, so the chosen
+ * vertex and the consumed random stream are identical (tests/test_topology_shim.py checks
+ * them against oracle/attach_ref.py, a restatement of the scan). */
 static int usable_ip(in_addr_t ip) { return ip != INADDR_NONE && ip != INADDR_ANY && ip != INADDR_LOOPBACK; }
 
-/* _topology_findAttachmentVertex + its hook, topology.c:2094-2369 */
+static uint64_t fnv1a(const char* s, size_t n) {
+    uint64_t h = 1469598103934665603ULL;
+    for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)s[i]) * 1099511628211ULL;
+    return h;
+}
+
+/* g_ascii_strcasecmp equality == equality of the ASCII-lowercased strings (malloc'd) */
+static char* ascii_lower(const char* s) {
+    const size_t n = strlen(s);
+    char* out = malloc(n + 1);
+    if (!out) return NULL;
+    for (size_t i = 0; i <= n; i++) out[i] = (char)((s[i] >= 'A' && s[i] <= 'Z') ? s[i] + 32 : s[i]);
+    return out;
+}
+
+static vlist* strmap_get(const strmap* m, const char* key, size_t n) {
+    if (!m->cap) return NULL;
+    for (size_t j = fnv1a(key, n) & (m->cap - 1); m->keys[j]; j = (j + 1) & (m->cap - 1))
+        if (!memcmp(m->keys[j], key, n) && m->keys[j][n] == 0) return &m->lists[m->vals[j]];
+    return NULL;
+}
+
+static vlist* strmap_add(strmap* m, const char* key, size_t n) {
+    vlist* l = strmap_get(m, key, n);
+    if (l) return l;
+    if ((m->n + 1) * 2 > m->cap) {
+        size_t ncap = m->cap ? m->cap * 2 : 64;
+        char** nk = calloc(ncap, sizeof(char*));
+        int32_t* nv = calloc(ncap, sizeof(int32_t));
+        for (size_t i = 0; i < m->cap; i++) {
+            if (!m->keys[i]) continue;
+            size_t j = fnv1a(m->keys[i], strlen(m->keys[i])) & (ncap - 1);
+            while (nk[j]) j = (j + 1) & (ncap - 1);
+            nk[j] = m->keys[i];
+            nv[j] = m->vals[i];
+        }
+        free(m->keys);
+        free(m->vals);
+        m->keys = nk;
+        m->vals = nv;
+        m->cap = ncap;
+    }
+    if (m->nlists == m->caplists) {
+        m->caplists = m->caplists ? m->caplists * 2 : 16;
+        m->lists = realloc(m->lists, sizeof(vlist) * (size_t)m->caplists);
+    }
+    size_t j = fnv1a(key, n) & (m->cap - 1);
+    while (m->keys[j]) j = (j + 1) & (m->cap - 1);
+    m->keys[j] = strndup(key, n);
+    m->vals[j] = m->nlists;
+    memset(&m->lists[m->nlists], 0, sizeof(vlist));
+    m->n++;
+    return &m->lists[m->nlists++];
+}
+
+static vlist* u32map_get(const u32map* m, uint32_t k) {
+    if (!m->cap) return NULL;
+    for (size_t j = ip_slot(k, m->cap); m->vals[j]; j = (j + 1) & (m->cap - 1))
+        if (m->keys[j] == k) return &m->lists[m->vals[j] - 1];
+    return NULL;
+}
+
+static vlist* u32map_add(u32map* m, uint32_t k) {
+    vlist* l = u32map_get(m, k);
+    if (l) return l;
+    if ((m->n + 1) * 2 > m->cap) {
+        size_t ncap = m->cap ? m->cap * 2 : 64;
+        uint32_t* nk = calloc(ncap, sizeof(uint32_t));
+        int32_t* nv = calloc(ncap, sizeof(int32_t));
+        for (size_t i = 0; i < m->cap; i++) {
+            if (!m->vals[i]) continue;
+            size_t j = ip_slot(m->keys[i], ncap);
+            while (nv[j]) j = (j + 1) & (ncap - 1);
+            nk[j] = m->keys[i];
+            nv[j] = m->vals[i];
+        }
+        free(m->keys);
+        free(m->vals);
+        m->keys = nk;
+        m->vals = nv;
+        m->cap = ncap;
+    }
+    if (m->nlists == m->caplists) {
+        m->caplists = m->caplists ? m->caplists * 2 : 16;
+        m->lists = realloc(m->lists, sizeof(vlist) * (size_t)m->caplists);
+    }
+    size_t j = ip_slot(k, m->cap);
+    while (m->vals[j]) j = (j + 1) & (m->cap - 1);
+    m->keys[j] = k;
+    m->vals[j] = ++m->nlists;
+    memset(&m->lists[m->nlists - 1], 0, sizeof(vlist));
+    m->n++;
+    return &m->lists[m->nlists - 1];
+}
+
+static int32_t trie_node(attach_index* x) {
+    if (x->ntrie == x->captrie) {
+        x->captrie = x->captrie ? x->captrie * 2 : 1024;
+        x->trie = realloc(x->trie, sizeof(*x->trie) * (size_t)x->captrie);
+        x->leaf = realloc(x->leaf, sizeof(int32_t) * (size_t)x->captrie);
+    }
+    x->trie[x->ntrie][0] = x->trie[x->ntrie][1] = 0;
+    x->leaf[x->ntrie] = -1;
+    return x->ntrie++;
+}
+
+/* key "<len(a)>:<a>|<b>" (unambiguous for any byte values), malloc'd */
+static char* pair_key(const char* a, const char* b) {
+    const size_t n = strlen(a) + strlen(b) + 24;
+    char* k = malloc(n);
+    if (k) snprintf(k, n, "%zu:%s|%s", strlen(a), a, b);
+    return k;
+}
+
+static attach_index* build_index(Topology* top) {
+    attach_index* x = calloc(1, sizeof(attach_index));
+    const int32_t V = top->V;
+    x->vip = malloc(sizeof(in_addr_t) * (size_t)(V ? V : 1));
+    x->usable = calloc((size_t)(V ? V : 1), 1);
+    trie_node(x); /* root */
+    for (int32_t v = 0; v < V; v++) {
+        const char *ipS = NULL, *s[4] = {NULL, NULL, NULL, NULL};
+        int ipF = vstr(top, top->a_ip, v, &ipS);
+        vstr(top, top->a_city, v, &s[0]);
+        vstr(top, top->a_country, v, &s[1]);
+        vstr(top, top->a_geo, v, &s[2]);
+        vstr(top, top->a_type, v, &s[3]);
+        /* LPM key: VAS(graph, "ip", v) parsed, "" (INADDR_NONE) when absent (topology.c:2232-2235) */
+        x->vip[v] = address_stringToIP(top->a_ip ? gml_str(top->a_ip, v) : "");
+        const in_addr_t ip = ipF ? address_stringToIP(ipS) : INADDR_NONE;
+        const int u = ipF && usable_ip(ip);
+        x->usable[v] = (uint8_t)u;
+        x->nips_all += u;
+        if (u) vl_push(u32map_add(&x->exact, ip), v, 1);
+        char* l[4] = {NULL, NULL, NULL, NULL};
+        for (int k = 0; k < 4; k++)
+            if (s[k]) l[k] = ascii_lower(s[k]);
+        strmap* single[3] = {&x->city, &x->country, &x->geo};
+        strmap* paired[3] = {&x->city_type, &x->country_type, &x->geo_type};
+        for (int k = 0; k < 3; k++) {
+            if (!l[k]) continue;
+            vl_push(strmap_add(single[k], l[k], strlen(l[k])), v, u);
+            char* key = l[3] ? pair_key(l[k], l[3]) : NULL;
+            if (key) vl_push(strmap_add(paired[k], key, strlen(key)), v, u);
+            free(key);
+        }
+        if (l[3]) vl_push(strmap_add(&x->type, l[3], strlen(l[3])), v, u);
+        for (int k = 0; k < 4; k++) free(l[k]);
+        /* trie insert, bit 31 first; a leaf keeps its first (lowest) vertex */
+        int32_t node = 0;
+        for (int b = 31; b >= 0; b--) {
+            const int bit = (int)((x->vip[v] >> b) & 1u);
+            if (!x->trie[node][bit]) {
+                int32_t c = trie_node(x);
+                x->trie[node][bit] = c;
+            }
+            node = x->trie[node][bit];
+        }
+        if (x->leaf[node] < 0) x->leaf[node] = v;
+    }
+    return x;
+}
+
+static attach_index* attach_index_of(Topology* top) {
+    pthread_mutex_lock(&top->idx_lock);
+    if (!top->aidx) top->aidx = build_index(top);
+    attach_index* x = top->aidx;
+    pthread_mutex_unlock(&top->idx_lock);
+    return x;
+}
+
+/* a hint's queue (NULL hint or no vertex with that value: empty) */
+static vlist* queue_of(const strmap* m, const char* hint) {
+    if (!hint) return NULL;
+    char* l = ascii_lower(hint);
+    vlist* q = l ? strmap_get(m, l, strlen(l)) : NULL;
+    free(l);
+    return q;
+}
+
+static vlist* pair_queue_of(const strmap* m, const char* a, const char* b) {
+    if (!a || !b) return NULL;
+    char *la = ascii_lower(a), *lb = ascii_lower(b);
+    char* key = (la && lb) ? pair_key(la, lb) : NULL;
+    vlist* q = key ? strmap_get(m, key, strlen(key)) : NULL;
+    free(la);
+    free(lb);
+    free(key);
+    return q;
+}
+
+/* _topology_getLongestPrefixMatch (topology.c:2219-2246) over one queue, in queue order */
+static int32_t lpm_scan(const attach_index* x, const vlist* q, in_addr_t requested) {
+    in_addr_t best_match = 0;
+    int32_t chosen = -1;
+    for (int32_t k = 0; k < q->n; k++) {
+        const in_addr_t match = ~(x->vip[q->v[k]] ^ requested);
+        if (match > best_match || best_match == 0) {
+            best_match = match;
+            chosen = q->v[k];
+        }
+    }
+    return chosen;
+}
+
+/* the same over every vertex: max ~(vip ^ req) == min (vip ^ req), the first vertex with
+ * that value; if even the best match is 0 every vertex replaced the previous one, so the
+ * reference returns the last vertex */
+static int32_t lpm_all(const attach_index* x, int32_t V, in_addr_t requested) {
+    if (V <= 0) return -1;
+    int32_t node = 0;
+    uint32_t xr = 0;
+    for (int b = 31; b >= 0; b--) {
+        const int want = (int)((requested >> b) & 1u);
+        if (x->trie[node][want]) {
+            node = x->trie[node][want];
+        } else {
+            node = x->trie[node][want ^ 1];
+            xr |= 1u << b;
+        }
+    }
+    if ((in_addr_t)~xr == 0) return V - 1;
+    return x->leaf[node];
+}
+
 static int32_t find_attachment_vertex(Topology* top, Random* rnd, const char* ipHint, const char* cityHint,
                                       const char* countryHint, const char* geoHint, const char* typeHint) {
-    enum { CITY_TYPE, CITY, COUNTRY_TYPE, COUNTRY, GEO_TYPE, GEO, TYPE, ALL, NQ };
-    ivec q[NQ];
-    uint32_t nips[NQ];
-    memset(q, 0, sizeof q);
-    memset(nips, 0, sizeof nips);
-    int requested_usable = 0, found_exact = 0;
+    const attach_index* x = attach_index_of(top);
+    int requested_usable = 0;
     in_addr_t requested = 0;
     if (ipHint) {
         in_addr_t ip = address_stringToIP(ipHint);
@@ -759,102 +1165,35 @@ static int32_t find_attachment_vertex(Topology* top, Random* rnd, const char* ip
             requested = ip;
         }
     }
-    for (int32_t v = 0; v < top->V; v++) {
-        const char *ipS = NULL, *cityS = NULL, *countryS = NULL, *geoS = NULL, *typeS = NULL;
-        int ipF = vstr(top, top->a_ip, v, &ipS);
-        int cityF = vstr(top, top->a_city, v, &cityS);
-        int countryF = vstr(top, top->a_country, v, &countryS);
-        int geoF = vstr(top, top->a_geo, v, &geoS);
-        int typeF = vstr(top, top->a_type, v, &typeS);
-        int cityM = cityF && cityHint && !strcasecmp(cityS, cityHint);
-        int countryM = countryF && countryHint && !strcasecmp(countryS, countryHint);
-        int geoM = geoF && geoHint && !strcasecmp(geoS, geoHint);
-        int typeM = typeF && typeHint && !strcasecmp(typeS, typeHint);
-        int vUsable = 0;
-        in_addr_t vip = INADDR_NONE;
-        if (ipF) {
-            in_addr_t ip = address_stringToIP(ipS);
-            if (usable_ip(ip)) {
-                vUsable = 1;
-                vip = ip;
-            }
-        }
-        if (requested_usable && vUsable && vip == requested) {
-            if (!found_exact) /* g_queue_clear of every queue; the IP counters are kept */
-                for (int k = 0; k < NQ; k++) q[k].n = 0;
-            found_exact = 1;
-            iv_push(&q[ALL], v);
-            nips[ALL]++;
-        }
-        if (found_exact) continue;
-        iv_push(&q[ALL], v);
-        if (vUsable) nips[ALL]++;
-        if (cityM && typeM) {
-            iv_push(&q[CITY_TYPE], v);
-            if (vUsable) nips[CITY_TYPE]++;
-        }
-        if (cityM) {
-            iv_push(&q[CITY], v);
-            if (vUsable) nips[CITY]++;
-        }
-        if (countryM && typeM) {
-            iv_push(&q[COUNTRY_TYPE], v);
-            if (vUsable) nips[COUNTRY_TYPE]++;
-        }
-        if (countryM) {
-            iv_push(&q[COUNTRY], v);
-            if (vUsable) nips[COUNTRY]++;
-        }
-        if (geoM && typeM) {
-            iv_push(&q[GEO_TYPE], v);
-            if (vUsable) nips[GEO_TYPE]++;
-        }
-        if (geoM) {
-            iv_push(&q[GEO], v);
-            if (vUsable) nips[GEO]++;
-        }
-        if (typeM) {
-            iv_push(&q[TYPE], v);
-            if (vUsable) nips[TYPE]++;
-        }
-    }
-    int pick = ALL;
+    const vlist* q = NULL;
+    int32_t n = top->V; /* ALL: every vertex, in order */
     int use_lpm = 0;
-    for (int k = CITY_TYPE; k <= TYPE; k++) {
-        if (q[k].n > 0) {
-            pick = k;
-            break;
-        }
-    }
-    if (pick != ALL)
-        use_lpm = requested_usable && nips[pick] > 0;
-    else
-        use_lpm = ipHint && nips[ALL] > 0;
-    int32_t chosen = -1;
-    ivec* c = &q[pick];
-    if (c->n > 0) {
-        if (use_lpm && !found_exact) {
-            /* _topology_getLongestPrefixMatch, topology.c:2219-2246 */
-            in_addr_t best_match = 0;
-            for (int32_t k = 0; k < c->n; k++) {
-                int32_t v = c->v[k];
-                const char* ipS = top->a_ip ? gml_str(top->a_ip, v) : "";
-                in_addr_t vip = address_stringToIP(ipS);
-                in_addr_t match = ~(vip ^ requested);
-                if (match > best_match || best_match == 0) {
-                    best_match = match;
-                    chosen = v;
-                }
-            }
+    const vlist* exact = requested_usable ? u32map_get(&x->exact, requested) : NULL;
+    if (exact && exact->n > 0) {
+        /* exact IP matches: every other queue was cleared, LPM is skipped (topology.c:2138-2160, 2318) */
+        q = exact;
+        n = exact->n;
+    } else {
+        const vlist* cand[7] = {
+            pair_queue_of(&x->city_type, cityHint, typeHint), queue_of(&x->city, cityHint),
+            pair_queue_of(&x->country_type, countryHint, typeHint), queue_of(&x->country, countryHint),
+            pair_queue_of(&x->geo_type, geoHint, typeHint), queue_of(&x->geo, geoHint), queue_of(&x->type, typeHint)};
+        for (int k = 0; k < 7 && !q; k++)
+            if (cand[k] && cand[k]->n > 0) q = cand[k];
+        if (q) {
+            n = q->n;
+            use_lpm = requested_usable && q->nips > 0;
         } else {
-            double r = random_nextDouble(rnd);
-            int index_range = c->n - 1;
-            int chosen_index = (int)round((double)(index_range * r));
-            if (chosen_index >= 0 && chosen_index < c->n) chosen = c->v[chosen_index];
+            use_lpm = ipHint && x->nips_all > 0;
         }
     }
-    for (int k = 0; k < NQ; k++) free(q[k].v);
-    return chosen;
+    if (n <= 0) return -1;
+    if (use_lpm) return q ? lpm_scan(x, q, requested) : lpm_all(x, top->V, requested);
+    double r = random_nextDouble(rnd);
+    int index_range = n - 1;
+    int chosen_index = (int)round((double)(index_range * r));
+    if (chosen_index < 0 || chosen_index >= n) return -1;
+    return q ? q->v[chosen_index] : chosen_index;
 }
 
 void topology_attach(Topology* top, Address* address, Random* randomSourcePool, char* ipHint, char* citycodeHint,
@@ -870,18 +1209,21 @@ void topology_attach(Topology* top, Address* address, Random* randomSourcePool, 
     }
     pthread_rwlock_wrlock(&top->ip_lock);
     ipt_put(&top->ips, node_ip, v);
-    if (top->att_index[v] < 0) {
+    if (atomic_load_explicit(&top->att_index[v], memory_order_relaxed) < 0) {
         if (top->n_att == top->cap_att) {
             top->cap_att = top->cap_att ? top->cap_att * 2 : 256;
             top->attached = realloc(top->attached, sizeof(int32_t) * (size_t)top->cap_att);
         }
-        top->att_index[v] = top->n_att;
-        top->attached[top->n_att++] = v;
+        top->attached[top->n_att] = v;
+        atomic_store_explicit(&top->att_index[v], top->n_att, memory_order_release);
+        top->n_att++;
     }
+    atomic_fetch_add_explicit(&top->ip_version, 1, memory_order_release);
     pthread_rwlock_unlock(&top->ip_lock);
     double x;
     if (bwUpOut) *bwUpOut = vnum(top->a_bwup, v, &x) ? (uint64_t)x : 0;
     if (bwDownOut) *bwDownOut = vnum(top->a_bwdown, v, &x) ? (uint64_t)x : 0;
+    if (!shadowtopo_log_enabled(ST_MESSAGE)) return;
     const char *ipS = NULL, *cityS = NULL, *countryS = NULL, *geoS = NULL, *typeS = NULL;
     vstr(top, top->a_ip, v, &ipS);
     vstr(top, top->a_city, v, &cityS);
@@ -901,9 +1243,9 @@ void topology_detach(Topology* top, Address* address) {
     uint32_t ip = address_toNetworkIP(address);
     pthread_rwlock_wrlock(&top->ip_lock);
     ipt_del(&top->ips, ip);
+    atomic_fetch_add_explicit(&top->ip_version, 1, memory_order_release);
     pthread_rwlock_unlock(&top->ip_lock);
 }
-
 /* ------------------------------------------------------------ eager computation */
 static int ensure_engine(Topology* top) {
     if (top->eng) return 0;
@@ -915,6 +1257,8 @@ static int ensure_engine(Topology* top) {
     for (int32_t k = 0; k < top->ndev; k++) {
         int rc = shadowtopo_create(top->V, top->E, top->gml->src, top->gml->dst, top->elat, top->eloss, top->vloss,
                                    flags, top->devices[k], &top->engs[k]);
+        if (rc == SHADOWTOPO_OK)
+            rc = shadowtopo_set_option(top->engs[k], SHADOWTOPO_OPT_HBM_SHARE, 1000 / device_sharers(top, k));
         if (rc != SHADOWTOPO_OK) {
             st_critical("GPU topology engine unavailable on device %d (%d): %s", (int)top->devices[k], rc,
                         shadowtopo_last_error());
@@ -929,12 +1273,16 @@ static int ensure_engine(Topology* top) {
     return 0;
 }
 
-/* one device's share of the attached-pair matrix: rows [r0, r1) written in place */
+/* one device's share of the rows: source rows [r0, r1) of the attached list, written to
+ * out + (row - r0) * A (host memory) */
 typedef struct {
     shadowtopo_engine* eng;
     const int32_t* attached;
     int32_t A, r0, r1;
-    matrix* m;
+    double* lat;
+    double* rel;
+    uint32_t* hops;
+    uint8_t* kind;
     int rc;
     char err[256];
 } row_block;
@@ -942,48 +1290,36 @@ typedef struct {
 static void* compute_block(void* arg) {
     row_block* w = arg;
     w->rc = shadowtopo_set_attached(w->eng, w->attached, w->A);
-    if (w->rc == SHADOWTOPO_OK && w->r1 > w->r0) {
-        size_t o = (size_t)w->r0 * (size_t)w->A;
-        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->m->lat + o, w->m->rel + o, w->m->hops + o,
-                                        w->m->kind + o, SHADOWTOPO_MEM_HOST, NULL);
-    }
+    if (w->rc == SHADOWTOPO_OK && w->r1 > w->r0)
+        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->lat, w->rel, w->hops, w->kind, SHADOWTOPO_MEM_HOST,
+                                        NULL);
     if (w->rc != SHADOWTOPO_OK) snprintf(w->err, sizeof w->err, "%s", shadowtopo_last_error());
     return NULL;
 }
 
-static matrix* compute_matrix(Topology* top, int32_t A) {
-    if (ensure_engine(top)) return NULL;
-    struct timespec t0, t1;
-    clock_gettime(CLOCK_MONOTONIC, &t0);
-    matrix* m = calloc(1, sizeof(matrix));
-    size_t n = (size_t)A * (size_t)A;
-    m->A = A;
-    m->lat = malloc(sizeof(double) * (n ? n : 1));
-    m->rel = malloc(sizeof(double) * (n ? n : 1));
-    m->hops = malloc(sizeof(uint32_t) * (n ? n : 1));
-    m->kind = malloc(n ? n : 1);
-    m->cnt_rows = calloc((size_t)(A ? A : 1), sizeof(*m->cnt_rows));
-    if (!m->lat || !m->rel || !m->hops || !m->kind || !m->cnt_rows) {
-        st_critical("out of host memory for the %d x %d attached-pair matrix", A, A);
-        free_matrix(m);
-        return NULL;
-    }
-    /* sources shard naturally: device k computes the contiguous row block
-     * k of ceil(A / ndev) rows against all A targets, on its own thread, straight into the
-     * host matrix; no exchange between devices is needed in one process */
+/* rows [r0, r1) of the pair matrix over `attached` (A targets) into m's rows, sharded over
+ * the devices (device k takes the contiguous k-th block, its own thread) */
+static int compute_rows_sharded(Topology* top, const int32_t* attached, int32_t A, int32_t r0, int32_t r1,
+                                matrix* m) {
     int32_t nd = top->ndev;
     row_block blocks[SHADOWTOPO_MAX_DEVICES];
     pthread_t th[SHADOWTOPO_MAX_DEVICES];
-    int32_t per = (A + nd - 1) / nd;
+    const int32_t rows = r1 - r0;
+    const int32_t per = (rows + nd - 1) / nd;
     for (int32_t k = 0; k < nd; k++) {
-        blocks[k].eng = top->engs[k];
-        blocks[k].attached = top->attached;
-        blocks[k].A = A;
-        blocks[k].r0 = k * per < A ? k * per : A;
-        blocks[k].r1 = (k + 1) * per < A ? (k + 1) * per : A;
-        blocks[k].m = m;
-        blocks[k].rc = 0;
-        blocks[k].err[0] = 0;
+        row_block* b = &blocks[k];
+        b->eng = top->engs[k];
+        b->attached = attached;
+        b->A = A;
+        b->r0 = r0 + (k * per < rows ? k * per : rows);
+        b->r1 = r0 + ((k + 1) * per < rows ? (k + 1) * per : rows);
+        const size_t o = (size_t)b->r0 * (size_t)A;
+        b->lat = m->lat + o;
+        b->rel = m->rel + o;
+        b->hops = m->hops + o;
+        b->kind = m->kind + o;
+        b->rc = 0;
+        b->err[0] = 0;
     }
     int spawned[SHADOWTOPO_MAX_DEVICES] = {0};
     for (int32_t k = 1; k < nd; k++) spawned[k] = pthread_create(&th[k], NULL, compute_block, &blocks[k]) == 0;
@@ -998,38 +1334,96 @@ static matrix* compute_matrix(Topology* top, int32_t A) {
         if (blocks[k].rc != SHADOWTOPO_OK) {
             st_critical("attached-pair computation failed on device %d (%d): %s", (int)top->devices[k],
                         blocks[k].rc, blocks[k].err);
-            free_matrix(m);
-            return NULL;
+            return -1;
+        }
+    }
+    return 0;
+}
+
+static matrix* alloc_matrix(int32_t A) {
+    matrix* m = calloc(1, sizeof(matrix));
+    if (!m) return NULL;
+    size_t n = (size_t)A * (size_t)A;
+    m->A = A;
+    m->lat = malloc(sizeof(double) * (n ? n : 1));
+    m->rel = malloc(sizeof(double) * (n ? n : 1));
+    m->hops = malloc(sizeof(uint32_t) * (n ? n : 1));
+    m->kind = malloc(n ? n : 1);
+    if (!m->lat || !m->rel || !m->hops || !m->kind) {
+        st_critical("out of host memory for the %d x %d attached-pair matrix", A, A);
+        free_matrix(m);
+        return NULL;
+    }
+    return m;
+}
+
+/* The matrix for the first A attached vertices (`attached`, a private copy).
+ * Late attach (`old` covers the first old->A of them): in an undirected graph only the new
+ * rows are computed (the new sources against every target); an old source's entry for a
+ * new target takes the new target's own entry for it (the reverse direction), which is
+ * exactly what the reference returns once the new host's paths are cached first
+ * (_topology_getPathEntry tries (t, s) for undirected graphs, topology.c:1987-1990), and
+ * the old block is kept as computed.  Directed graphs recompute every row. */
+static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A, const matrix* old) {
+    if (ensure_engine(top)) return NULL;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    matrix* m = alloc_matrix(A);
+    if (!m) return NULL;
+    const int32_t A0 = (old && !top->directed && old->A < A) ? old->A : 0;
+    if (compute_rows_sharded(top, attached, A, A0, A, m)) {
+        free_matrix(m);
+        return NULL;
+    }
+    for (int32_t i = 0; i < A0; i++) {
+        const size_t src = (size_t)i * (size_t)A0, dst = (size_t)i * (size_t)A;
+        memcpy(m->lat + dst, old->lat + src, sizeof(double) * (size_t)A0);
+        memcpy(m->rel + dst, old->rel + src, sizeof(double) * (size_t)A0);
+        memcpy(m->hops + dst, old->hops + src, sizeof(uint32_t) * (size_t)A0);
+        memcpy(m->kind + dst, old->kind + src, (size_t)A0);
+        for (int32_t j = A0; j < A; j++) {
+            const size_t o = dst + (size_t)j, r = (size_t)j * (size_t)A + (size_t)i;
+            m->lat[o] = m->lat[r];
+            m->rel[o] = m->rel[r];
+            m->hops[o] = m->hops[r];
+            m->kind[o] = m->kind[r];
         }
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
-    top->compute_count += top->complete ? 0 : A;
-    top->self_count += top->complete ? 0 : A;
-    /* _topology_storePathInCache's running minimum (topology.c:1374-1385) over every path
-     * the matrix holds */
+    top->compute_count += top->complete ? 0 : A - A0;
+    top->self_count += top->complete ? 0 : A - A0;
+    /* _topology_storePathInCache's running minimum (topology.c:1374-1385), over every path
+     * the matrix holds (it covers all attached pairs at once; the reference folds in paths
+     * as they are cached, so this window can be smaller, never larger: DESIGN.md 2) */
     double mn = 0;
+    const size_t n = (size_t)A * (size_t)A;
     for (size_t k = 0; k < n; k++)
         if (m->kind[k] != SHADOWTOPO_KIND_NONE && (mn == 0 || m->lat[k] < mn)) mn = m->lat[k];
     if (mn > 0 && (top->min_latency == 0 || mn < top->min_latency)) {
         top->min_latency = mn;
         worker_updateMinTimeJump(top->min_latency);
     }
-    st_info("computed %d x %d attached-pair matrix on %d device(s) (first %d) in %f seconds", A, A, (int)nd,
-            (int)top->device, top->compute_s);
+    st_info("computed %d x %d attached-pair matrix (%d new rows) on %d device(s) (first %d) in %f seconds", A, A,
+            A - A0, (int)top->ndev, (int)top->device, top->compute_s);
     return m;
 }
 
+/* the matrix covering attached index `need`; computed on the first query that needs it */
 static matrix* current_matrix(Topology* top, int32_t need) {
     matrix* m = atomic_load_explicit(&top->mat, memory_order_acquire);
     if (m && m->A > need) return m;
     pthread_mutex_lock(&top->compute_lock);
     m = atomic_load_explicit(&top->mat, memory_order_acquire);
-    if (!m || m->A <= need) {
+    if ((!m || m->A <= need) && !top->compute_failed) {
+        /* a private copy of the attached list: a concurrent attach may grow (realloc) it */
         pthread_rwlock_rdlock(&top->ip_lock);
-        int32_t A = top->n_att;
+        const int32_t A = top->n_att;
+        int32_t* att = malloc(sizeof(int32_t) * (size_t)(A ? A : 1));
+        if (att && A) memcpy(att, top->attached, sizeof(int32_t) * (size_t)A);
         pthread_rwlock_unlock(&top->ip_lock);
-        matrix* nm = A > need ? compute_matrix(top, A) : NULL;
+        matrix* nm = (att && A > need) ? compute_matrix(top, att, A, m) : NULL;
+        free(att);
         if (nm) {
             if (m) {
                 m->next = top->retired;
@@ -1038,19 +1432,61 @@ static matrix* current_matrix(Topology* top, int32_t need) {
             atomic_store_explicit(&top->mat, nm, memory_order_release);
             m = nm;
         } else {
+            /* fail once, loudly: later queries return -1 without retrying the GPU work */
+            if (A > need) {
+                top->compute_failed = 1;
+                st_critical("attached-pair computation failed; every later query fails without a retry");
+            }
             m = NULL;
         }
+    } else if (!m || m->A <= need) {
+        m = NULL;
     }
     pthread_mutex_unlock(&top->compute_lock);
     return m;
 }
 
+/* IP -> vertex snapshot for the per-packet path: rebuilt (under snap_lock) only when an
+ * attach / detach bumped the version since the last one; lookups then take no lock */
+static const ip_snap* query_snap(Topology* top) {
+    ip_snap* s = atomic_load_explicit(&top->snap, memory_order_acquire);
+    if (s && s->version == atomic_load_explicit(&top->ip_version, memory_order_acquire)) return s;
+    pthread_mutex_lock(&top->snap_lock);
+    s = atomic_load_explicit(&top->snap, memory_order_acquire);
+    if (!s || s->version != atomic_load_explicit(&top->ip_version, memory_order_acquire)) {
+        ip_snap* n = calloc(1, sizeof(ip_snap));
+        if (n) {
+            pthread_rwlock_rdlock(&top->ip_lock);
+            n->version = atomic_load_explicit(&top->ip_version, memory_order_acquire);
+            n->t = top->ips;
+            size_t cap = top->ips.cap;
+            n->t.keys = cap ? malloc(sizeof(uint32_t) * cap) : NULL;
+            n->t.vals = cap ? malloc(sizeof(int32_t) * cap) : NULL;
+            n->t.state = cap ? malloc(cap) : NULL;
+            if (cap && n->t.keys && n->t.vals && n->t.state) {
+                memcpy(n->t.keys, top->ips.keys, sizeof(uint32_t) * cap);
+                memcpy(n->t.vals, top->ips.vals, sizeof(int32_t) * cap);
+                memcpy(n->t.state, top->ips.state, cap);
+            } else if (cap) {
+                n->t.cap = 0;
+            }
+            pthread_rwlock_unlock(&top->ip_lock);
+            if (s) {
+                s->next = top->snap_retired;
+                top->snap_retired = s;
+            }
+            atomic_store_explicit(&top->snap, n, memory_order_release);
+            s = n;
+        }
+    }
+    pthread_mutex_unlock(&top->snap_lock);
+    return s;
+}
+
 static int32_t connected_vertex(Topology* top, Address* a) {
-    /* _topology_getConnectedVertexIndex, topology.c:1388-1405 */
-    uint32_t ip = address_toNetworkIP(a);
-    pthread_rwlock_rdlock(&top->ip_lock);
-    int32_t v = ipt_get(&top->ips, ip);
-    pthread_rwlock_unlock(&top->ip_lock);
+    /* _topology_getConnectedVertexIndex, topology.c:1388-1405, on the lock-free snapshot */
+    const ip_snap* s = query_snap(top);
+    int32_t v = s ? ipt_get(&s->t, address_toNetworkIP(a)) : -1;
     if (v < 0) st_warning("address %s is not connected to the topology", address_toHostIPString(a));
     return v;
 }
@@ -1069,8 +1505,9 @@ static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off
                     address_toString(dst));
         return NULL;
     }
-    int32_t i = top->att_index[vs], j = top->att_index[vd];
-    matrix* m = current_matrix(top, i > j ? i : j);
+    int32_t i = atomic_load_explicit(&top->att_index[vs], memory_order_acquire);
+    int32_t j = atomic_load_explicit(&top->att_index[vd], memory_order_acquire);
+    matrix* m = (i >= 0 && j >= 0) ? current_matrix(top, i > j ? i : j) : NULL;
     if (m) {
         size_t o = (size_t)i * (size_t)m->A + (size_t)j;
         if (m->kind[o] != SHADOWTOPO_KIND_NONE) {
@@ -1101,29 +1538,6 @@ int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress)
     return topology_getLatency(top, srcAddress, dstAddress) > -1 ? 1 : 0;
 }
 
-/* counters: one per cached Path, i.e. per unordered pair in undirected graphs (the
- * reference stores one direction, topology.c:1312-1318); stored value = count + 1 so a
- * touched pair is non-zero (the teardown log lists touched pairs) */
-static _Atomic uint64_t* counter_of(Topology* top, matrix* m, int32_t i, int32_t j) {
-    if (!top->directed && j < i) {
-        int32_t t = i;
-        i = j;
-        j = t;
-    }
-    uint64_t* row = atomic_load_explicit(&m->cnt_rows[i], memory_order_acquire);
-    if (!row) {
-        pthread_mutex_lock(&top->cnt_lock);
-        row = atomic_load_explicit(&m->cnt_rows[i], memory_order_acquire);
-        if (!row) {
-            row = calloc((size_t)m->A, sizeof(uint64_t));
-            atomic_store_explicit(&m->cnt_rows[i], row, memory_order_release);
-        }
-        pthread_mutex_unlock(&top->cnt_lock);
-    }
-    if (!row) return NULL;
-    return (_Atomic uint64_t*)&row[j];
-}
-
 void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Address* dstAddress) {
     size_t o;
     int32_t i, j;
@@ -1133,7 +1547,7 @@ void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Add
                  address_toString(dstAddress));
         return;
     }
-    _Atomic uint64_t* c = counter_of(top, m, i, j);
+    _Atomic uint64_t* c = counter_slot(top, i, j);
     if (!c) return;
     uint64_t expect = atomic_load_explicit(c, memory_order_relaxed);
     if (expect == 0) {
@@ -1142,7 +1556,6 @@ void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Add
     }
     atomic_fetch_add_explicit(c, 1, memory_order_relaxed);
 }
-
 /* ------------------------------------------------------------ extensions */
 int topology_hip_set_device(Topology* top, int32_t device) {
     if (!top || top->eng) return -1;
@@ -1190,6 +1603,7 @@ int topology_hip_get_info(Topology* top, topology_hip_info* out) {
     out->min_path_latency = top->min_latency;
     out->compute_seconds = top->compute_s;
     out->compute_count = top->compute_count;
+    out->compute_failed = top->compute_failed;
     return 0;
 }
 
@@ -1217,17 +1631,10 @@ int32_t topology_hip_vertex_of_id(Topology* top, const char* id) {
 
 uint64_t topology_hip_packet_count(Topology* top, int32_t src_vertex, int32_t dst_vertex) {
     if (!top || src_vertex < 0 || dst_vertex < 0 || src_vertex >= top->V || dst_vertex >= top->V) return 0;
-    int32_t i = top->att_index[src_vertex], j = top->att_index[dst_vertex];
-    matrix* m = atomic_load(&top->mat);
-    if (!m || i < 0 || j < 0 || i >= m->A || j >= m->A) return 0;
-    if (!top->directed && j < i) {
-        int32_t t = i;
-        i = j;
-        j = t;
-    }
-    uint64_t* row = atomic_load(&m->cnt_rows[i]);
-    if (!row || !row[j]) return 0;
-    return row[j] - 1;
+    int32_t i = atomic_load(&top->att_index[src_vertex]), j = atomic_load(&top->att_index[dst_vertex]);
+    if (i < 0 || j < 0) return 0;
+    uint64_t c = counter_peek(top, i, j);
+    return c ? c - 1 : 0;
 }
 
 int topology_hip_edges(Topology* top, const int32_t** src, const int32_t** dst, const double** latency,

@@ -41,6 +41,7 @@ OPT_DENSE_BATCHES_PER_WAVE = 9
 OPT_SOURCE_ORDER = 10
 OPT_DENSE_SEED = 11
 OPT_DENSE_PRUNE = 12
+OPT_HBM_SHARE = 13
 CSR_DELTA = 0  # fold changed in-neighbours into the recorded state (cross-check)
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (default)
 
@@ -67,6 +68,7 @@ class Stats(ctypes.Structure):
         ("visits", ctypes.c_int64), ("changes", ctypes.c_int64),
         ("full_sweeps", ctypes.c_int64), ("delta_sweeps", ctypes.c_int64),
         ("full_ms", ctypes.c_double), ("delta_ms", ctypes.c_double),
+        ("full_batches", ctypes.c_int64), ("full_changes", ctypes.c_int64), ("relax_batches", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -34,7 +34,7 @@ class Info(ctypes.Structure):
         ("is_complete", ctypes.c_int32), ("is_connected", ctypes.c_int32), ("cluster_count", ctypes.c_int32),
         ("prefers_direct_paths", ctypes.c_int32), ("n_attached", ctypes.c_int32), ("computed_for", ctypes.c_int32),
         ("device", ctypes.c_int32), ("min_path_latency", ctypes.c_double), ("compute_seconds", ctypes.c_double),
-        ("compute_count", ctypes.c_int64), ("n_devices", ctypes.c_int32),
+        ("compute_count", ctypes.c_int64), ("n_devices", ctypes.c_int32), ("compute_failed", ctypes.c_int32),
     ]
 
     def as_dict(self):

@@ -134,18 +134,68 @@ def test_reference_test_topologies(tmp_path):
         top.free()
 
 
-def test_late_attach_recomputes(tmp_path):
-    g = synth.random_sparse(V=80, avg_deg=4, seed=45, A=20)
+def _subset(g, k):
+    import copy
+    h = copy.copy(g)
+    h.attached = g.attached[:k]
+    return h
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_late_attach_keeps_counters_and_values(tmp_path, directed):
+    """hosts attached after the first query: an undirected graph computes only the new rows
+    (an old source's entry for a new target is the new target's entry for it, the value the
+    reference returns once the new host's paths are cached first, topology.c:1987-1990), a
+    directed graph recomputes every row; packet counters survive both late attaches"""
+    g = synth.random_sparse(V=90, avg_deg=4, seed=45, A=30, directed=directed)
     va, ips = with_vertex_ips(g)
     top = T.Topology.new(write(tmp_path, "l.xml", synth.to_graphml(g, extra_vattr=va)))
     hosts = attach_all(top, ips, g.attached[:10])
+    vx = [top.vertex_of_ip(h.ip) for h in hosts]
     l01 = top.getLatency(hosts[0], hosts[1])
+    for _ in range(3):
+        top.incrementPathPacketCounter(hosts[0], hosts[1])
+    top.incrementPathPacketCounter(hosts[2], hosts[5])
     assert top.info()["computed_for"] == 10
-    more = attach_all(top, ips, g.attached[10:12], base=100)
+    more = attach_all(top, ips, g.attached[10:20], base=100)
     assert top.getLatency(hosts[0], more[1]) > 0
-    assert top.info()["computed_for"] == 12
+    assert top.info()["computed_for"] == 20
     assert top.getLatency(hosts[0], hosts[1]) == l01
+    top.incrementPathPacketCounter(hosts[0], hosts[1])
+    top.incrementPathPacketCounter(more[0], hosts[3])
+    assert top.packet_count(vx[0], vx[1]) == 4
+    assert top.packet_count(vx[2], vx[5]) == 1
+    even_more = attach_all(top, ips, g.attached[20:26], base=200)
+    top.incrementPathPacketCounter(even_more[0], hosts[0])
+    assert top.info()["computed_for"] == 26
+    assert top.packet_count(vx[0], vx[1]) == 4
+    assert top.packet_count(top.vertex_of_ip(more[0].ip), vx[3]) == 1
+    assert top.packet_count(top.vertex_of_ip(even_more[0].ip), vx[0]) == 1
+    # values: rows from each source's own computation, late columns of older rows from the
+    # reverse direction (undirected) or recomputed (directed)
+    all_hosts = hosts + more + even_more
+    lat_o, rel_o, _, _, _ = oracle_matrix(_subset(g, 26))
+    for i, a in enumerate(all_hosts):
+        for j, b in enumerate(all_hosts):
+            first = 0 if max(i, j) < 10 else (10 if max(i, j) < 20 else 20)  # attach wave that made (i, j) known
+            si, sj = (i, j)
+            if not directed and i < first and j >= first:
+                si, sj = j, i  # the new target's own entry
+            assert top.getLatency(a, b) == lat_o[si, sj], (i, j)
+            assert top.getReliability(a, b) == rel_o[si, sj], (i, j)
     top.free()
+
+
+def test_c_harness_lookups_under_threads(tmp_path):
+    """the C caller (tests/c/topo_harness.c): attach, one-shot compute, then 8 worker
+    threads doing the per-packet call sequence of worker.c:267-279 lock-free"""
+    from test_topology_shim import build_harness, run_harness
+    g = synth.random_sparse(V=400, avg_deg=4, seed=47, A=None)
+    va, _ = with_vertex_ips(g)
+    path = write(tmp_path, "h.xml", synth.to_graphml(g, extra_vattr=va))
+    res = run_harness(build_harness(tmp_path), path, 300, 8, 20000, 0)
+    assert res["compute_failed"] == 0 and res["routable"] > 0
+    assert res["ns_per_call_per_thread"] > 0
 
 
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])

@@ -185,44 +185,56 @@ def test_preferdirectpaths_boolean_type_rejected(tmp_path):
     assert top is None  # the reference requires a STRING (topology.c:601-603)
 
 
-def attach_graph(n=40, seed=3):
+def attach_graph(n=40, seed=3, with_ip=True, dup_ips=False):
     rng = np.random.default_rng(seed)
     g = synth.random_sparse(V=n, seed=seed)
     countries = ["US", "DE", "FR", "BR"]
     types = ["relay", "client", "server"]
     cities = ["a", "b", "c", "d", "e", "f"]
-    ips = [f"10.{rng.integers(0, 4)}.{rng.integers(0, 255)}.{rng.integers(1, 255)}" if rng.random() < 0.6
-           else ("0.0.0.0" if rng.random() < 0.5 else None) for _ in range(n)]
+    pool = [f"10.{rng.integers(0, 4)}.{rng.integers(0, 255)}.{rng.integers(1, 255)}" for _ in range(8)]
+    ips = [(pool[rng.integers(0, 8)] if dup_ips else f"10.{rng.integers(0, 4)}.{rng.integers(0, 255)}.{rng.integers(1, 255)}")
+           if rng.random() < 0.6 else ("0.0.0.0" if rng.random() < 0.5 else None) for _ in range(n)]
     va = {
-        "ip": ("d1", "string", ips),
         "countrycode": ("d2", "string", [countries[rng.integers(0, 4)] for _ in range(n)]),
         "citycode": ("d5", "string", [cities[rng.integers(0, 6)] if rng.random() < 0.5 else None for _ in range(n)]),
         "type": ("d6", "string", [types[rng.integers(0, 3)] for _ in range(n)]),
         "geocode": ("d8", "string", [countries[rng.integers(0, 4)] if rng.random() < 0.3 else None for _ in range(n)]),
     }
+    if with_ip:
+        va["ip"] = ("d1", "string", ips)
     vattr = {k: [(x or "") for x in v[2]] for k, v in va.items()}
     return g, synth.to_graphml(g, extra_vattr=va), vattr
 
 
-def test_attach_matches_reference_algorithm(tmp_path):
-    g, text, vattr = attach_graph()
+def random_hints(rng, vattr, k):
+    ip = [None, "10.1.2.3", "10.0.0.1", "192.168.1.1", "0.0.0.0", "127.0.0.1", "garbage", "255.255.255.255",
+          "0.0.0.1"][rng.integers(0, 9)]
+    if rng.random() < 0.2 and "ip" in vattr:
+        cand = [x for x in vattr["ip"] if x and x != "0.0.0.0"]
+        if cand:
+            ip = cand[rng.integers(0, len(cand))]
+    if k % 5 == 0:  # IP hint alone: the longest-prefix rule over the whole vertex set
+        return dict(ipHint=ip)
+    return dict(ipHint=ip,
+                citycodeHint=[None, "a", "B", "zz", ""][rng.integers(0, 5)],
+                countrycodeHint=[None, "us", "DE", "XX"][rng.integers(0, 4)],
+                geocodeHint=[None, "FR", "br"][rng.integers(0, 3)],
+                typeHint=[None, "relay", "CLIENT", "nope"][rng.integers(0, 4)])
+
+
+@pytest.mark.parametrize("n,seed,with_ip,dup_ips", [(40, 3, True, False), (300, 8, True, False),
+                                                   (120, 9, True, True), (60, 10, False, False)])
+def test_attach_matches_reference_algorithm(tmp_path, n, seed, with_ip, dup_ips):
+    """the indexed attach (hint indexes + LPM trie) picks the vertex the reference's O(V)
+    scan picks, with the same random stream, for every hint combination"""
+    g, text, vattr = attach_graph(n=n, seed=seed, with_ip=with_ip, dup_ips=dup_ips)
     top = T.Topology.new(write(tmp_path, "att.xml", text))
     assert top is not None
-    ref_rng = attach_ref.RandR(12345)
-    rnd = T.Random(12345)
-    rng = np.random.default_rng(0)
-    hints = []
-    for k in range(200):
-        ip = [None, "10.1.2.3", "10.0.0.1", "192.168.1.1", "0.0.0.0", "127.0.0.1", "garbage"][rng.integers(0, 7)]
-        if rng.random() < 0.2:
-            cand = [x for x in vattr["ip"] if x and x != "0.0.0.0"]
-            ip = cand[rng.integers(0, len(cand))]
-        h = dict(ipHint=ip,
-                 citycodeHint=[None, "a", "B", "zz"][rng.integers(0, 4)],
-                 countrycodeHint=[None, "us", "DE", "XX"][rng.integers(0, 4)],
-                 geocodeHint=[None, "FR", "br"][rng.integers(0, 3)],
-                 typeHint=[None, "relay", "CLIENT", "nope"][rng.integers(0, 4)])
-        hints.append(h)
+    ref_rng = attach_ref.RandR(12345 + seed)
+    rnd = T.Random(12345 + seed)
+    rng = np.random.default_rng(seed)
+    for k in range(300):
+        h = random_hints(rng, vattr, k)
         addr = T.Address(f"11.0.{k // 250}.{k % 250 + 1}")
         down, up = top.attach(addr, rnd, **h)
         want = attach_ref.find_attachment_vertex(vattr, g.n, ref_rng, **h)
@@ -232,6 +244,29 @@ def test_attach_matches_reference_algorithm(tmp_path):
     att = top.attached()
     assert len(set(att.tolist())) == len(att)
     top.free()
+
+
+def test_failed_computation_is_not_retried(tmp_path):
+    """a failed attached-pair computation is remembered: later queries return -1 at once
+    instead of re-running the GPU work under the compute lock"""
+    g, text, _ = attach_graph(n=20, seed=11)
+    top = T.Topology.new(write(tmp_path, "f.xml", text))
+    a, b = T.Address("11.1.1.1"), T.Address("11.1.1.2")
+    r = T.Random(2)
+    top.attach(a, r)
+    top.attach(b, r)
+    top.set_device(1000)  # no such device: engine creation fails
+    assert top.getLatency(a, b) == -1.0
+    assert top.info()["compute_failed"] == 1
+    assert top.getReliability(a, b) == -1.0 and not top.isRoutable(a, b)
+    assert top.info()["compute_failed"] == 1
+    top.free()
+
+
+def test_infinite_latency_rejected_at_load(tmp_path):
+    g = synth.random_sparse(V=10, seed=12)
+    g.latency[3] = np.inf
+    assert T.Topology.new(write(tmp_path, "inf.xml", synth.to_graphml(g))) is None
 
 
 def test_detach_keeps_attached_vertex(tmp_path):
@@ -268,3 +303,34 @@ def test_unattached_address_is_unroutable(tmp_path):
     top.attach(a, T.Random(3))
     assert top.getLatency(a, b) == -1.0  # topology.c:1979-1984 -> -1 (topology.c:2073)
     top.free()
+
+
+HARNESS = os.path.join(os.path.dirname(__file__), "c", "topo_harness.c")
+
+
+def build_harness(tmp_path):
+    """compile the C caller against the in-tree library, as Shadow links it"""
+    import subprocess
+    lib_dir = os.path.dirname(E.LIB_PATH)
+    exe = str(tmp_path / "topo_harness")
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-pthread", "-I", INCLUDE, HARNESS, "-o", exe, "-L", lib_dir,
+                    "-lshadowtopo_hip", f"-Wl,-rpath,{lib_dir}"], check=True)
+    return exe
+
+
+def run_harness(exe, *args):
+    import json
+    import subprocess
+    out = subprocess.run([exe] + [str(a) for a in args], check=True, capture_output=True, text=True, timeout=300)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_c_harness_ingest_and_attach(tmp_path, mode):
+    """a C program linked against libshadowtopo_hip drives topology_new + topology_attach
+    (no queries: no GPU needed)"""
+    g, text, _ = attach_graph(n=300, seed=13)
+    path = write(tmp_path, "h.xml", text)
+    res = run_harness(build_harness(tmp_path), path, 500, 1, 0, mode)
+    assert res["vertices"] == 300 and res["hosts"] == 500
+    assert 0 < res["attached"] <= 300
