@@ -77,7 +77,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
                                               (vertex, source) pairs gets a change-mask delta round instead of a full
                                               sweep (default 125; 0 = always full sweeps) */
-#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default) or _DELTA */
+#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default), _FILTERED or _DELTA */
 #define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
 #define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Hilbert
                                               order of the top two principal axes of the distances to eight
@@ -94,15 +94,22 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               column's min W32 over the chunk);
                                               0 = every chunk filtered, original order. Results are identical. */
 
+#define SHADOWTOPO_OPT_WORKLIST 14         /* CSR FULL rounds: 1 (default) = over compacted frontier worklists (one
+                                              wave per active (vertex, batch) pair), 0 = one wave per pair of the grid */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
                                               engine may take (default 1000); engines sharing one device split it */
 
-/* sparse (CSR) relaxation rounds (both exact): FULL recomputes the minimum over every
- * in-arc of every active vertex; DELTA folds only the in-neighbours whose state changed for
- * the lane's source into the recorded lexicographic state (fewer row bytes, more
- * instructions and dependent loads: slower on the C3/C4 graphs, kept as a cross-check) */
+/* sparse (CSR) relaxation rounds (all exact, same fixed point):
+ *   FULL (default): recompute every active vertex's minimum over all its in-arcs' 512-byte
+ *     distance rows (k_relax; rounds with few active pairs run over frontier worklists);
+ *   FILTERED: fold only the in-neighbours whose state changed, found through round stamps
+ *     in 256-byte f32 key rows, settling the f32-filter survivors in f64 (k_relax_st);
+ *   DELTA: fold only changed in-neighbours, found through 64-bit change masks, in f64.
+ * FILTERED and DELTA read fewer bytes but issue more instructions and dependent loads:
+ * slower than FULL on the C3/C4/C5 graphs; kept as cross-checks. */
 #define SHADOWTOPO_CSR_DELTA 0
 #define SHADOWTOPO_CSR_FULL 1
+#define SHADOWTOPO_CSR_FILTERED 2
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;
@@ -134,6 +141,8 @@ typedef struct shadowtopo_stats {
     int64_t full_batches;    /* dense: batches swept by full-sweep launches (summed over launches) */
     int64_t full_changes;    /* dense: (vertex, source) pairs those full sweeps changed */
     int64_t relax_batches;   /* sparse: batches in flight, summed over relax launches */
+    int64_t wl_launches;     /* sparse: relax launches over frontier worklists (k_relax_wl), included above */
+    double wl_ms;            /* OPT_TIMING: their HIP-event time, included in relax_ms */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -75,6 +75,7 @@ struct GraphDev {
     const int64_t* in_ptr;   // [V+1] relaxation in-CSR (no loops, parallel edges merged)
     const int32_t* in_src;   // [arcs] tail u, ascending within a row
     const double* in_w;      // [arcs] min latency over the merged parallel edges
+    const float* in_w32;     // [arcs] in_w rounded toward -inf (the f32 filter key; padding arcs +inf)
     const double* in_r;      // [arcs] 1 - packetloss of the get_eid edge
     const int32_t* in_eid;   // [arcs] get_eid edge (lowest edge id)
     const int64_t* out_ptr;  // [V+1] out-neighbours (== in-CSR for undirected graphs)
@@ -108,7 +109,7 @@ struct Pools {
     unsigned long long* mask;  // [slot] lanes whose rows need the heap-exact replay
     double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
     unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
-    float* D32;         // dense mode: [slot][Vp][64] distance rounded down to f32 (NaN = unreached), filter key
+    float* D32;         // [slot][Vp][64] f32 filter key (dense: distance rounded down; CSR: stamped, see stamp_key)
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -162,7 +163,7 @@ struct ReplayDev {
     int32_t row[REPLAY_SLOTS];
 };
 
-constexpr int CSR_PAD = 8;  // in_src / in_w carry 8 padding arcs (u = 0, w = +inf) so chunk loads never clamp
+constexpr int CSR_PAD = 16;  // in_src / in_w carry 16 padding arcs (u = 0, w = +inf) so chunk loads never clamp
 
 __device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000000000000LL); }
 __device__ __forceinline__ double dmax() { return __longlong_as_double(0x7fefffffffffffffLL); }
@@ -183,6 +184,17 @@ __device__ __forceinline__ bool xcd_tile(int32_t L, int32_t ngroups, int32_t nti
 // f32 filter key of a distance: rounded toward -inf, NaN when unreached (see k_relax_dense_f)
 __device__ __forceinline__ float f32_key(double d) {
     return d < dinf() ? __double2float_rd(d) : __int_as_float(0x7fc00000);
+}
+
+// conservative f32 threshold of a running best bc: rounded up plus 4 ulps (+inf when
+// unreached); fl32(D32 + W32) <= it whenever fl64(d + w) <= bc (see k_relax_dense_f)
+__device__ __forceinline__ float f32_thr(double bc) {
+    if (!(bc < dmax())) return __int_as_float(0x7f800000);  // unreached: any finite candidate passes
+    const float r = __double2float_ru(bc);
+    // 4 ulps up, saturating at +inf: past FLT_MAX the bit pattern would be a NaN, which
+    // never passes a filter (a lane would silently lose its candidates)
+    if (!(r < __int_as_float(0x7f7ffffc))) return __int_as_float(0x7f800000);
+    return __int_as_float(__float_as_int(r) + 4);
 }
 
 __device__ __forceinline__ double readlane_d(double x, int l) {
@@ -245,7 +257,7 @@ __global__ void k_init(Pools pools, int32_t V) {
 }
 
 // sources: d(s) = 0, R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445); activate out-neighbours
-__global__ void k_seed(GraphDev g, Pools pools) {
+__global__ void k_seed(GraphDev g, Pools pools, int32_t src_key_zero) {
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int j = blockIdx.x;
     const int32_t s = B.srcv[j];
@@ -256,9 +268,11 @@ __global__ void k_seed(GraphDev g, Pools pools) {
         B.H[idx] = 0;
         B.R[idx] = g.vfac[s];
         B.P[idx] = -1;
-        // f32 filter key NaN: the source's own row never passes a dense filter (its seed
-        // candidate starts every lexicographic state, k_relax_dense_f)
-        if (B.D32) B.D32[idx] = __int_as_float(0x7fc00000);
+        // f32 filter key: NaN for the dense sweeps (the source's own row never passes a
+        // dense filter: its seed candidate starts every lexicographic state,
+        // k_relax_dense_f); 0 for the CSR filtered rounds, where the source's row is the
+        // first candidate its out-neighbours see (k_relax_st)
+        if (B.D32) B.D32[idx] = src_key_zero ? 0.0f : __int_as_float(0x7fc00000);
         // round 0 of the CSR delta rounds reads the change masks of a virtual round -1
         if (B.chm1) atomicOr(&B.chm1[s], 1ull << j);
     }
@@ -313,24 +327,13 @@ __device__ __forceinline__ void relax_arc(double du, double w, int32_t e, int32_
 // and 8 row loads, all in flight before the first compare.
 // Grid: 1-D, remapped so that all blocks sharing an XCD (blockIdx % 8) work on the same
 // batch (its [V][64] state then stays in that XCD's L2).  Placement is a speed hint only.
-__global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
-                                               const double* __restrict__ in_w, const double* __restrict__ in_r,
-                                               const int64_t* __restrict__ out_ptr,
-                                               const int32_t* __restrict__ out_dst, Pools pools,
-                                               int32_t V, int32_t nb, int32_t nvb, int32_t parity,
-                                               int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
-    int32_t b, vt;
-    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
-    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int32_t v = vt * 4 + wave;
-    if (v >= V) return;
-    const int lane = threadIdx.x & 63;
-    const BatchDev B = batch_view(pools, b);
+// one visit of destination v in batch b (the body of k_relax / k_relax_wl)
+__device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                            const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                            const int64_t* __restrict__ out_ptr, const int32_t* __restrict__ out_dst,
+                                            const BatchDev& B, int32_t b, int32_t v, int lane, int32_t parity,
+                                            int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
     const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
-    gbyte* act_cur = B.act(parity);
-    if (act_cur[v] == 0) return;
-    if (lane == 0) act_cur[v] = 0;
-
     const int32_t sv = B.srcv[lane];
     const size_t idx = (size_t)v * KL + lane;
     const double curD = B.D[idx];
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (e + k >= end) w[k] = dinf();
-            du[k] = Dl[(size_t)u[k] * KL];
+            du[k] = e + k < end ? Dl[(size_t)u[k] * KL] : 0.0;  // no row loads past the list
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) relax_arc(du[k], w[k], e + k, u[k], bc, bdu, be, bu, tie);
@@ -369,6 +372,102 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
         if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
     }
     if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
+}
+
+// one wave per (destination, batch) of the whole grid; inactive pairs exit after their flag
+__global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                               const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                               const int64_t* __restrict__ out_ptr,
+                                               const int32_t* __restrict__ out_dst, Pools pools,
+                                               int32_t V, int32_t nb, int32_t nvb, int32_t parity,
+                                               int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
+    int32_t b, vt;
+    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v = vt * 4 + wave;
+    if (v >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    gbyte* act_cur = B.act(parity);
+    if (act_cur[v] == 0) return;
+    if (lane == 0) act_cur[v] = 0;
+    relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+}
+
+// Frontier worklists (default for sparse graphs): the active destinations of each batch for
+// the next round, compacted from the activity flags into one list per batch.  Without them
+// every round launches a wave for every (vertex, batch) pair -- 1.6e7 on C4 -- and each
+// inactive one still pays a flag load; rounds where most pairs are active use the grid.
+constexpr int WL_SPAN = 4096;  // vertices per compaction block: 16 flags per thread, one atomic per block
+__global__ __launch_bounds__(256) void k_compact(Pools pools, int32_t V, int32_t parity, int32_t* __restrict__ wl,
+                                                 uint32_t* __restrict__ wlcnt) {
+    __shared__ uint32_t sc[256];
+    __shared__ uint32_t sbase;
+    const int32_t b = blockIdx.y;
+    const int32_t v0 = blockIdx.x * WL_SPAN + threadIdx.x * 16;
+    const BatchDev B = batch_view(pools, b);
+    // 16 flags in one 16-byte load (the flag arrays are 64-aligned and padded to Vp, zero past V)
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (v0 < V) {
+        const uint4 f = *(const uint4*)((const uint8_t*)B.act(parity) + v0);
+        w[0] = f.x;
+        w[1] = f.y;
+        w[2] = f.z;
+        w[3] = f.w;
+    }
+    uint32_t bits = 0;  // bit i: vertex v0 + i active
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bits |= ((w[q] >> (8 * i)) & 0xFFu) ? 1u << (4 * q + i) : 0u;
+    const uint32_t n = (uint32_t)__popc(bits);
+    // block inclusive scan of the counts (Hillis-Steele in LDS)
+    sc[threadIdx.x] = n;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const uint32_t add = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0u;
+        __syncthreads();
+        sc[threadIdx.x] += add;
+        __syncthreads();
+    }
+    const uint32_t incl = sc[threadIdx.x];
+    if (threadIdx.x == 255) sbase = incl ? atomicAdd(&wlcnt[b], incl) : 0u;
+    __syncthreads();
+    uint32_t pos = sbase + incl - n;
+    int32_t* out = wl + (size_t)b * pools.Vp;
+    while (bits) {
+        const int i = __builtin_ctz(bits);
+        bits &= bits - 1;
+        out[pos++] = v0 + i;
+    }
+}
+
+// one wave per listed (vertex, batch): the T items of all batches in batch-major order
+// (prefix[b] = items before batch b), XCD x (block % 8) takes the contiguous slice
+// [x*S, (x+1)*S) -- a batch's state stays in one XCD's L2, as with xcd_tile
+__global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                  const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                                  const int64_t* __restrict__ out_ptr,
+                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t parity,
+                                                  const int32_t* __restrict__ wl, const int64_t* __restrict__ prefix,
+                                                  int32_t nb, int64_t S, int32_t* __restrict__ cnt,
+                                                  unsigned long long* __restrict__ prof) {
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i = (int64_t)(blockIdx.x & 7) * S + (int64_t)(blockIdx.x >> 3) * 4 + wave;
+    const int64_t T = prefix[nb];
+    if ((int64_t)(blockIdx.x >> 3) * 4 + wave >= S || i >= T) return;
+    int32_t lo = 0, hi = nb;  // last batch with prefix <= i
+    while (hi - lo > 1) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (prefix[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const int32_t b = lo;
+    const int32_t v = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])];
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    if (lane == 0) B.act(parity)[v] = 0;
+    relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
 }
 
 // CSR delta round (default for sparse graphs).  Same pull schedule as k_relax (one wave per
@@ -489,6 +588,180 @@ __global__ __launch_bounds__(256) void k_relax_delta(const int64_t* __restrict__
     const unsigned long long mask = __ballot(ch);
     if (lane == 0) B.chm(parity)[v] = mask;
     if (mask) {
+        gbyte* act_nxt = B.act(parity ^ 1);
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
+    }
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
+}
+
+
+// Round-stamped f32 keys for the CSR rounds (k_relax_st).  The key of a (vertex, source)
+// state is its distance rounded toward -inf in f32, lowered by at least 256 ulps and with
+// the low byte replaced by the round (mod 256) in which the state last changed:
+//   key <= round_down_f32(d) - 1 ulp <= d        (so the f32 filter stays exact)
+//   key >= round_down_f32(d) - 511 ulps           (so thr_of_key below bounds d from above)
+// 0 for d below 512 float ulps (the source itself: always eligible), NaN when unreached.
+// One coalesced 256-byte row load then tells every lane both whether the tail changed
+// recently (no separate change-mask loads) and a lower bound of its candidate.
+constexpr uint32_t KEY_NAN = 0x7fc00000u;
+__device__ __forceinline__ uint32_t stamp_key(double d, int32_t round) {
+    if (!(d < dinf())) return KEY_NAN;
+    const uint32_t kb = __float_as_uint(__double2float_rd(d));
+    if (kb < 512u) return 0u;
+    return ((kb - 256u) & ~0xFFu) | ((uint32_t)round & 0xFFu);
+}
+// an f32 upper bound of round_up(d) + 4 ulps from the key alone (the f32_thr of d or more)
+__device__ __forceinline__ float thr_of_key(uint32_t k) {
+    if (k == KEY_NAN) return __int_as_float(0x7f800000);
+    return k + 516u <= 0x7f7fffffu ? __uint_as_float(k + 516u) : __int_as_float(0x7f800000);
+}
+
+// Lexicographic state of one (destination, source) in the changed-tail CSR rounds
+// (k_relax_st): the recorded state (D0, B0, P0, H0, loaded lazily), the running one
+// (d, bdu = d(pred), pa / pu = predecessor arc / vertex, lt = local tie) and the threshold.
+struct MGState {
+    double D0, B0, d, bdu;
+    int32_t P0, pa, pu;
+    uint32_t H0;
+    float thr;
+    bool have, touched, lt;
+};
+
+__device__ __forceinline__ void mg_fold(MGState& S, double c, double du, int32_t e, int32_t u) {
+    if (!(c < dinf())) return;  // a key seen before its distance (same round): next round
+    if (c < S.d) {
+        S.d = c;
+        S.bdu = du;
+        S.pa = e;
+        S.pu = u;
+        S.lt = du == c;  // degenerate d(u) == d(v): heap-order dependent
+        S.touched = true;
+    } else if (c == S.d) {
+        if (S.pu == u) {  // the recorded predecessor refreshed
+            S.lt = (du == S.bdu && S.lt) || du == c;
+            S.bdu = du;
+            S.touched = true;
+        } else if (du < S.bdu) {
+            S.bdu = du;
+            S.pa = e;
+            S.pu = u;
+            S.lt = du == c;
+            S.touched = true;
+        } else if (du == S.bdu) {
+            S.lt = true;  // two predecessors at the same d(u): heap pop order decides
+            S.touched = true;
+        }
+    }
+}
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+
+// CSR round, changed tails only, stamped f32 keys (SHADOWTOPO_CSR_FILTERED).  One wave =
+// one destination v of one batch (lane = source).  Per chunk of 8 in-arcs: the tails' key
+// rows (256 B, coalesced: half of k_relax's f64 rows, and a working set the Infinity Cache
+// holds for the batches in flight) tell each lane whether the tail changed in the previous
+// or this round (key stamp) and give the f32 filter fl32(key + W32) <= thr(v) (thr_of_key:
+// an upper bound of v's running best, so the filter is exact); only passing lanes read the
+// exact f64 d(u) and fold (fl(d(u)+w), d(u)) into v's recorded lexicographic state with the
+// rules of k_relax_delta (mg_fold) -- that state is loaded lazily, for lanes with a passing
+// candidate only.  Unchanged tails were folded in when they last changed (every change
+// activates all out-neighbours for the next round, which sees its stamp), so the recorded
+// state plus the changed candidates is the full minimum: the same fixed point as k_relax,
+// bit for bit.  A stale stamp (256 rounds back) only re-offers an unchanged candidate,
+// which the rules leave as it is.
+__global__ __launch_bounds__(256) void k_relax_st(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                  const double* __restrict__ in_w, const float* __restrict__ in_w32,
+                                                  const double* __restrict__ in_r, const int64_t* __restrict__ out_ptr,
+                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t V,
+                                                  int32_t nb, int32_t nvb, int32_t parity, int32_t round,
+                                                  int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
+    int32_t b, vt;
+    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v = vt * 4 + wave;
+    if (v >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    gbyte* act_cur = B.act(parity);
+    if (act_cur[v] == 0) return;
+    if (lane == 0) act_cur[v] = 0;
+    const uint32_t kp = (uint32_t)(round - 1) & 0xFFu;
+    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
+    const int32_t sv = B.srcv[lane];
+    const size_t idx = (size_t)v * KL + lane;
+    const gu32* K = (const gu32*)B.D32;
+    const gu32* Kl = K + lane;
+    const gdouble* Dl = B.D + lane;
+    const bool live = sv >= 0 && sv != v;
+    // a dead lane gets a NaN threshold: nothing passes
+    const float thr = live ? thr_of_key(K[idx]) : __int_as_float(0x7fc00000);
+    MGState S;
+    S.have = S.touched = S.lt = false;
+    S.D0 = S.B0 = S.d = S.bdu = dinf();
+    S.P0 = S.pa = S.pu = -1;
+    S.H0 = 0;
+    for (int32_t e = beg; e < end; e += 8) {
+        int32_t u[8];
+        float w32[8];
+        uint32_t kk[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u[k] = in_src[e + k];
+            w32[k] = in_w32[e + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) kk[k] = e + k < end ? Kl[(size_t)u[k] * KL] : KEY_NAN;  // uniform guard
+        bool pass[8];
+        bool anyl = false;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            // changed in the previous round or this one; keys below 256 (the source) always
+            const bool elig = kk[k] < 256u || ((kk[k] - kp) & 0xFFu) <= 1u;
+            pass[k] = elig && __uint_as_float(kk[k]) + w32[k] <= thr;  // NaN never passes
+            anyl |= pass[k];
+        }
+        if (!__ballot(anyl)) continue;
+        if (anyl && !S.have) {  // the recorded state, only for lanes that have a candidate
+            S.D0 = B.D[idx];
+            S.B0 = B.BDU[idx];
+            S.P0 = B.P[idx];
+            S.H0 = B.H[idx];
+            S.d = S.D0;
+            S.bdu = S.B0;
+            S.pa = S.P0;
+            S.pu = S.P0 >= 0 ? in_src[S.P0] : -1;
+            S.lt = (S.H0 & LTIE) != 0;
+            S.have = true;
+        }
+        double du[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) du[k] = pass[k] ? Dl[(size_t)u[k] * KL] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (pass[k]) mg_fold(S, du[k] + in_w[e + k], du[k], e + k, u[k]);  // altdist = mindist + weight
+    }
+    bool ch = false;
+    if (S.touched) {
+        const size_t uidx = (size_t)S.pu * KL + lane;
+        const uint32_t hu = B.H[uidx];
+        const double ru = B.R[uidx];
+        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (S.lt ? (TAINT | LTIE) : 0u);
+        const double r = ru * in_r[S.pa];
+        const double R0 = B.R[idx];
+        ch = S.d != S.D0 || h != S.H0 || r != R0 || S.pa != S.P0;
+        if (ch) {
+            B.D[idx] = S.d;
+            B.H[idx] = h;
+            B.R[idx] = r;
+            B.P[idx] = S.pa;
+            ((gu32*)B.D32)[idx] = stamp_key(S.d, round);
+        }
+        if (S.bdu != S.B0) B.BDU[idx] = S.bdu;
+    }
+    if (__ballot(ch)) {
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
         if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
@@ -635,14 +908,6 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 // best and the lane can skip it; rows where any lane passes redo the exact f64
 // lexicographic update.  The f32 stream costs half the VALU cycles of f64 add + compare and
 // half the bytes per row.
-__device__ __forceinline__ float f32_thr(double bc) {
-    if (!(bc < dmax())) return __int_as_float(0x7f800000);  // unreached: any finite candidate passes
-    const float r = __double2float_ru(bc);
-    // 4 ulps up, saturating at +inf: past FLT_MAX the bit pattern would be a NaN, which
-    // never passes a filter (a lane would silently lose its candidates)
-    if (!(r < __int_as_float(0x7f7ffffc))) return __int_as_float(0x7f800000);
-    return __int_as_float(__float_as_int(r) + 4);
-}
 
 // One full sweep, f32-filtered and LDS-staged.  A 256-thread block owns 4*TDT consecutive
 // destinations (wave w: TDT of them) of one batch; the rows u stream through LDS in chunks
@@ -1868,6 +2133,12 @@ struct shadowtopo_engine {
     std::vector<void*> batch_allocs;
     int32_t* d_cnt = nullptr;
     int32_t* h_cnt = nullptr;  // pinned
+    // CSR frontier worklists (k_compact / k_relax_wl): [nb][Vp] active vertices, per-batch counts
+    int32_t* d_wl = nullptr;
+    uint32_t* d_wlcnt = nullptr;
+    uint32_t* h_wlcnt = nullptr;  // pinned [nb]
+    int64_t* d_wlpre = nullptr;   // [nb + 1] item prefix, uploaded per round
+    int64_t* h_wlpre = nullptr;   // pinned
     // staging for host outputs
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -1882,10 +2153,11 @@ struct shadowtopo_engine {
     int32_t opt_force_replay = 0;
     int32_t opt_profile = 0;
     int32_t opt_dense_variant = 0;  // SHADOWTOPO_DENSE_F32 (default) or SHADOWTOPO_DENSE_F64
-    int32_t opt_csr_variant = 1;    // SHADOWTOPO_CSR_FULL (default) or SHADOWTOPO_CSR_DELTA
+    int32_t opt_csr_variant = 1;    // SHADOWTOPO_CSR_FULL (default), _FILTERED, _DELTA (see shadowtopo.h)
     int32_t opt_dense_tb = 1;       // batches per wave in the f32-filtered full sweep (1, 2 or 4)
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
+    int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
@@ -1937,6 +2209,13 @@ void free_batches(shadowtopo_engine* eng) {
     eng->d_cnt = nullptr;
     if (eng->h_cnt) (void)hipHostFree(eng->h_cnt);
     eng->h_cnt = nullptr;
+    if (eng->h_wlcnt) (void)hipHostFree(eng->h_wlcnt);
+    if (eng->h_wlpre) (void)hipHostFree(eng->h_wlpre);
+    eng->h_wlcnt = nullptr;
+    eng->h_wlpre = nullptr;
+    eng->d_wl = nullptr;
+    eng->d_wlcnt = nullptr;
+    eng->d_wlpre = nullptr;
     eng->h_srcv.clear();
     eng->h_row.clear();
     eng->nb_cap = 0;
@@ -1962,11 +2241,19 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double))) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb)))
         return rc;
-    if (eng->dense && (rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))) return rc;
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))) return rc;
     eng->h_srcv.assign((size_t)KL * nb, -1);
     eng->h_row.assign((size_t)KL * nb, -1);
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
     HIP_TRY(hipHostMalloc((void**)&eng->h_cnt, sizeof(int32_t) * nb, hipHostMallocDefault));
+    if (!eng->dense) {
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wl, sizeof(int32_t) * VK / KL * nb)) ||
+            (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlcnt, sizeof(uint32_t) * nb)) ||
+            (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlpre, sizeof(int64_t) * (nb + 1))))
+            return rc;
+        HIP_TRY(hipHostMalloc((void**)&eng->h_wlcnt, sizeof(uint32_t) * nb, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&eng->h_wlpre, sizeof(int64_t) * (nb + 1), hipHostMallocDefault));
+    }
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->prof_buf, sizeof(unsigned long long) * 16 * nb))) return rc;
     eng->nb_cap = nb;
     return SHADOWTOPO_OK;
@@ -1993,7 +2280,7 @@ int ensure_replay(shadowtopo_engine* eng) {
 int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
-    const double per_batch = (double)eng->Vp * KL * (eng->dense ? 36.0 : 32.0) + 18.0 * eng->Vp;
+    const double per_batch = (double)eng->Vp * KL * 36.0 + 18.0 * eng->Vp;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
@@ -2079,7 +2366,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         const size_t total = (size_t)eng->Vp * KL;
         int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
         hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp);
-        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools);
+        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools, eng->dense ? 0 : 1);
         HIP_TRY(hipGetLastError());
     }
     const int32_t nvb = (V + 3) / 4;
@@ -2106,9 +2393,31 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t thresh = (int32_t)std::min<int64_t>(
         0x7f7f7f7e, (int64_t)V * KL * eng->opt_delta_permille / 1000);
     std::vector<uint8_t> full_b;  // dense: batches the full sweep covers this round
+    // sparse FULL rounds over compacted frontier worklists (k_compact / k_relax_wl)
+    const bool use_wl = !eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL && eng->opt_worklist && eng->d_wl;
+    const int32_t ncb = (V + WL_SPAN - 1) / WL_SPAN;
+    if (use_wl) {
+        HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
+        hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, 0, eng->d_wl,
+                           eng->d_wlcnt);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
+        int64_t wl_total = 0;
+        if (use_wl) {
+            eng->h_wlpre[0] = 0;
+            for (int32_t b = 0; b < nbg; ++b) eng->h_wlpre[b + 1] = eng->h_wlpre[b] + eng->h_wlcnt[b];
+            wl_total = eng->h_wlpre[nbg];
+            if (wl_total == 0) break;  // nothing active: converged
+        }
+        // worklist only where it pays: a mostly-active round runs the plain grid
+        const bool round_wl = use_wl && wl_total * 2 < (int64_t)nbg * V;
+        if (round_wl)
+            HIP_TRY(hipMemcpyAsync(eng->d_wlpre, eng->h_wlpre, sizeof(int64_t) * (nbg + 1), hipMemcpyHostToDevice, s));
         int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
         int32_t* cnt_prev = eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
         HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
@@ -2150,6 +2459,18 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur);
                 eng->st.delta_sweeps++;
             }
+        } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED) {
+            eng->st.relax_batches += nbg;
+            hipLaunchKernelGGL(k_relax_st, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                               g.in_w32, g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1),
+                               (int32_t)(round & 0x7fffffff), cnt_cur, eng->d_prof);
+        } else if (round_wl) {
+            eng->st.relax_batches += nbg;
+            eng->st.wl_launches++;
+            const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
+            hipLaunchKernelGGL(k_relax_wl, dim3((uint32_t)(8 * (S / 4))), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                               g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
+                               eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FULL) {
             eng->st.relax_batches += nbg;
             hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
@@ -2163,6 +2484,13 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         }
         HIP_TRY(hipGetLastError());
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev1, s));
+        if (use_wl) {  // the next round's worklists, from the flags this round set
+            HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
+            hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
+                               (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
+        }
         HIP_TRY(hipMemcpyAsync(eng->h_cnt, cnt_cur, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         eng->st.relax_launches++;
@@ -2171,6 +2499,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
             eng->st.relax_ms += ms;
+            if (round_wl) eng->st.wl_ms += ms;
             if (eng->dense) {
                 if (round_full && round_delta) {
                     float a = 0, b = 0;
@@ -2731,9 +3060,11 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     g.V = V;
     g.flags = flags;
     g.multigraph = multigraph;
+    std::vector<float> in_w32(in_w.size());
+    for (size_t x = 0; x < in_w.size(); ++x) in_w32[x] = f32_round_down(in_w[x]);
     int rc = 0;
     if ((rc = upload(eng, in_ptr, &g.in_ptr)) || (rc = upload(eng, in_src, &g.in_src)) ||
-        (rc = upload(eng, in_w, &g.in_w)) || (rc = upload(eng, in_r, &g.in_r)) ||
+        (rc = upload(eng, in_w, &g.in_w)) || (rc = upload(eng, in_w32, &g.in_w32)) || (rc = upload(eng, in_r, &g.in_r)) ||
         (rc = upload(eng, in_eid, &g.in_eid)) || (rc = upload(eng, inc_ptr, &g.inc_ptr)) ||
         (rc = upload(eng, inc_eid, &g.inc_eid)) || (rc = upload(eng, efrom, &g.efrom)) ||
         (rc = upload(eng, eto, &g.eto)) || (rc = upload(eng, elat, &g.elat)) || (rc = upload(eng, erel, &g.erel)) ||
@@ -2874,7 +3205,7 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_dense_tb = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_CSR_VARIANT:
-            if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL)
+            if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL && value != SHADOWTOPO_CSR_FILTERED)
                 return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
             eng->opt_csr_variant = (int32_t)value;
             return SHADOWTOPO_OK;
@@ -2889,6 +3220,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_SEED:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");
             eng->opt_dense_seed = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_WORKLIST:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "worklist must be 0 or 1");
+            eng->opt_worklist = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_HBM_SHARE:
             if (value < 1 || value > 1000) return fail(SHADOWTOPO_EINVAL, "HBM share must be in [1, 1000] per mille");

@@ -42,8 +42,10 @@ OPT_SOURCE_ORDER = 10
 OPT_DENSE_SEED = 11
 OPT_DENSE_PRUNE = 12
 OPT_HBM_SHARE = 13
-CSR_DELTA = 0  # fold changed in-neighbours into the recorded state (cross-check)
-CSR_FULL = 1  # recompute every active vertex over all in-arcs (default)
+OPT_WORKLIST = 14
+CSR_DELTA = 0  # fold changed in-neighbours into the recorded state, f64 (cross-check)
+CSR_FULL = 1  # recompute every active vertex over all in-arcs (cross-check)
+CSR_FILTERED = 2  # changed tails only: round-stamped f32 keys, f64 settle (k_relax_st)
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (
@@ -69,6 +71,7 @@ class Stats(ctypes.Structure):
         ("full_sweeps", ctypes.c_int64), ("delta_sweeps", ctypes.c_int64),
         ("full_ms", ctypes.c_double), ("delta_ms", ctypes.c_double),
         ("full_batches", ctypes.c_int64), ("full_changes", ctypes.c_int64), ("relax_batches", ctypes.c_int64),
+        ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

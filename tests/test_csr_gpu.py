@@ -1,6 +1,7 @@
-"""CSR relaxation variants (k_relax_delta, the default, and k_relax) against the oracle and
-against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops, kind and
-reliability; the delta rounds and the full recomputation must reach the same fixed point."""
+"""CSR relaxation variants (k_relax, the default: full recomputation, over frontier
+worklists in sparse rounds; k_relax_st: changed tails only, round-stamped f32 keys;
+k_relax_delta: changed tails, f64) against the oracle and against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops, kind and
+reliability; every variant must reach the same fixed point."""
 import numpy as np
 import pytest
 
@@ -40,7 +41,7 @@ def _case(case):
 CASES = ["sparse", "directed", "ties", "int_random", "vloss_prefer", "no_loops", "multigraph"]
 
 
-@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL])
+@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL, E.CSR_FILTERED])
 @pytest.mark.parametrize("case", CASES)
 def test_csr_variants(case, variant):
     g = _case(case)
@@ -48,9 +49,19 @@ def test_csr_variants(case, variant):
     assert st["dense"] == 0
 
 
-def test_csr_delta_several_groups():
+@pytest.mark.parametrize("case", CASES)
+def test_csr_full_grid_without_worklists(case):
+    """the default FULL rounds run over compacted frontier worklists; the one-wave-per-pair
+    grid must give the same matrices"""
+    g = _case(case)
+    compare(g, layout="csr", csr_variant=E.CSR_FULL, worklist=0)
+    compare(g, layout="csr", csr_variant=E.CSR_FULL, worklist=1, batches_in_flight=2)
+
+
+@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FILTERED])
+def test_csr_delta_several_groups(variant):
     g = synth.random_sparse(V=500, avg_deg=4, seed=37)
-    compare(g, layout="csr", batches_in_flight=3)  # 500 sources -> 8 batches -> 3 groups
+    compare(g, layout="csr", batches_in_flight=3, csr_variant=variant)  # 500 sources -> 8 batches -> 3 groups
 
 
 @pytest.mark.parametrize("case", ["ties", "sparse", "int_random", "directed"])
@@ -60,16 +71,17 @@ def test_csr_delta_same_fixed_point(case):
     g = _case(case)
     srcs = np.arange(0, g.n, 2, dtype=np.int32)
     outs = []
-    for variant in (E.CSR_FULL, E.CSR_DELTA):
+    for variant in (E.CSR_FULL, E.CSR_DELTA, E.CSR_FILTERED):
         eng = E.Engine.from_synth(g, layout="csr")
         eng.set_option(E.OPT_CSR_VARIANT, variant)
         outs.append(eng.sssp(srcs))
         eng.close()
-    (d0, p0, h0, t0), (d1, p1, h1, t1) = outs
-    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
-    assert np.array_equal(t0, t1)
-    ok = t0 == 0
-    assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
+    d0, p0, h0, t0 = outs[0]
+    for d1, p1, h1, t1 in outs[1:]:
+        assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
+        assert np.array_equal(t0, t1)
+        ok = t0 == 0
+        assert np.array_equal(p0[ok], p1[ok]) and np.array_equal(h0[ok], h1[ok])
     if case in ("ties", "int_random"):
         assert (t0 != 0).any()
 
