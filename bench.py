@@ -155,7 +155,8 @@ def main():
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists (1, default) or the full grid (0)")
     ap.add_argument("--csr-variant", type=int, default=1,
-                    help="1 = full recomputation (default), 2 = changed tails with stamped f32 keys, 0 = f64 delta rounds")
+                    help="3 = changed (tail, source) pairs over worklists, 1 = full recomputation, "
+                         "2 = changed tails with stamped f32 keys, 0 = f64 delta rounds")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -277,11 +278,12 @@ def main():
     else:
         # the grid rounds (k_relax): the worklist rounds (k_relax_wl, sparse frontiers) are the
         # minority of the time and are reported beside it
-        kname = {0: "k_relax_delta", 1: "k_relax", 2: "k_relax_st"}[args.csr_variant]
-        all_l = max(1, st["relax_launches"])
-        launches, kms = max(1, st["relax_launches"] - st["wl_launches"]), st["relax_ms"] - st["wl_ms"]
-        bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * args.steps / all_l
-        batches_per_launch = st["relax_batches"] / all_l
+        # every relax round of the step (grid and worklist launches alike): achieved = the
+        # step's compulsory bytes / the relax kernels' time in the step
+        kname = {0: "k_relax_delta", 1: "k_relax", 2: "k_relax_st", 3: "k_relax_cm"}[args.csr_variant]
+        launches, kms = max(1, st["relax_launches"]), st["relax_ms"]
+        bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * args.steps / launches
+        batches_per_launch = st["relax_batches"] / launches
     avg_launch_s = kms / launches / 1e3
     achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
     ckey = f"{args.config}@{args.scale}@{world}"
@@ -305,7 +307,7 @@ def main():
                             "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
                             "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
                                     "waves / SQ_WAVES; peak = one VALU issue per 4 cycles per SIMD at 2.4 GHz"}
-    if not st["dense"] and st["wl_launches"]:
+    if not st["dense"] and st["wl_launches"] and args.csr_variant == 1:
         roofline["worklist_kernel"] = {"kernel": "k_relax_wl", "avg_launch_ms": st["wl_ms"] / st["wl_launches"],
                                        "launches_per_step": st["wl_launches"] / args.steps}
     if st["dense"] and st["delta_sweeps"]:

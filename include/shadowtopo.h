@@ -100,16 +100,22 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               engine may take (default 1000); engines sharing one device split it */
 
 /* sparse (CSR) relaxation rounds (all exact, same fixed point):
- *   FULL (default): recompute every active vertex's minimum over all its in-arcs' 512-byte
+ *   MASKED (default): over frontier worklists, fold only the (in-neighbour, source) pairs
+ *     whose state changed, found through per-vertex round-stamped change records; the wave
+ *     compacts the changed in-arcs with a ballot and loads their distance rows masked to
+ *     the changed lanes; the vertex's own state is read only for lanes with a candidate
+ *     (k_relax_cm);
+ *   FULL: recompute every active vertex's minimum over all its in-arcs' 512-byte
  *     distance rows (k_relax; rounds with few active pairs run over frontier worklists);
  *   FILTERED: fold only the in-neighbours whose state changed, found through round stamps
  *     in 256-byte f32 key rows, settling the f32-filter survivors in f64 (k_relax_st);
- *   DELTA: fold only changed in-neighbours, found through 64-bit change masks, in f64.
- * FILTERED and DELTA read fewer bytes but issue more instructions and dependent loads:
- * slower than FULL on the C3/C4/C5 graphs; kept as cross-checks. */
+ *   DELTA: fold only changed in-neighbours, found through 64-bit change masks, in f64,
+ *     over the whole grid.
+ * FULL, FILTERED and DELTA are kept as cross-checks. */
 #define SHADOWTOPO_CSR_DELTA 0
 #define SHADOWTOPO_CSR_FULL 1
 #define SHADOWTOPO_CSR_FILTERED 2
+#define SHADOWTOPO_CSR_MASKED 3
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;

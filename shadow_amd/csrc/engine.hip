@@ -98,6 +98,16 @@ typedef __attribute__((address_space(1))) uint32_t guint;
 typedef __attribute__((address_space(1))) int32_t gint;
 typedef __attribute__((address_space(1))) uint8_t gbyte;
 
+// Change record of one vertex in one batch, for the CSR masked rounds (k_relax_cm): the
+// lanes (sources) whose state changed in round rd[p], one record per round parity p.  A
+// reader in round r takes the records stamped r - 1 or r; a record from an older round is
+// stale and ignored, so nothing is ever cleared between rounds.
+struct alignas(32) CMask {
+    unsigned long long m[2];
+    uint32_t rd[2];
+    uint32_t pad_[2];
+};
+
 struct Pools {
     double* D;          // [slot][Vp][64] distance
     uint32_t* H;        // [slot][Vp][64] hops | TAINT
@@ -110,6 +120,7 @@ struct Pools {
     double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
     unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
     float* D32;         // [slot][Vp][64] f32 filter key (dense: distance rounded down; CSR: stamped, see stamp_key)
+    CMask* cm;          // CSR masked rounds: [slot][Vp] change records
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -129,6 +140,7 @@ struct BatchDev {
     unsigned long long* chm0;
     unsigned long long* chm1;
     gfloat* D32;
+    CMask* cm;
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
     __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
@@ -149,6 +161,7 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.chm0 = p.chm ? p.chm + (size_t)b * 2 * p.Vp : nullptr;
     B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
     B.D32 = p.D32 ? (gfloat*)(p.D32 + o) : nullptr;
+    B.cm = p.cm ? p.cm + (size_t)b * p.Vp : nullptr;
     return B;
 }
 
@@ -275,6 +288,10 @@ __global__ void k_seed(GraphDev g, Pools pools, int32_t src_key_zero) {
         if (B.D32) B.D32[idx] = src_key_zero ? 0.0f : __int_as_float(0x7fc00000);
         // round 0 of the CSR delta rounds reads the change masks of a virtual round -1
         if (B.chm1) atomicOr(&B.chm1[s], 1ull << j);
+        if (B.cm) {  // the masked rounds: the same, as a record stamped round -1
+            atomicOr(&B.cm[s].m[1], 1ull << j);
+            B.cm[s].rd[1] = 0xffffffffu;
+        }
     }
     for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act0[g.out_dst[x]] = 1;
 }
@@ -399,8 +416,8 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
 // every round launches a wave for every (vertex, batch) pair -- 1.6e7 on C4 -- and each
 // inactive one still pays a flag load; rounds where most pairs are active use the grid.
 constexpr int WL_SPAN = 4096;  // vertices per compaction block: 16 flags per thread, one atomic per block
-__global__ __launch_bounds__(256) void k_compact(Pools pools, int32_t V, int32_t parity, int32_t* __restrict__ wl,
-                                                 uint32_t* __restrict__ wlcnt) {
+__global__ __launch_bounds__(256) void k_compact(Pools pools, int32_t V, int32_t parity, int4* __restrict__ wl,
+                                                 uint32_t* __restrict__ wlcnt, const int64_t* __restrict__ in_ptr) {
     __shared__ uint32_t sc[256];
     __shared__ uint32_t sbase;
     const int32_t b = blockIdx.y;
@@ -434,12 +451,27 @@ __global__ __launch_bounds__(256) void k_compact(Pools pools, int32_t V, int32_t
     if (threadIdx.x == 255) sbase = incl ? atomicAdd(&wlcnt[b], incl) : 0u;
     __syncthreads();
     uint32_t pos = sbase + incl - n;
-    int32_t* out = wl + (size_t)b * pools.Vp;
+    int4* out = wl + (size_t)b * pools.Vp;
+    // an entry carries the vertex's in-arc range too: the relax wave starts its arc loads
+    // from the entry instead of a dependent in_ptr load
     while (bits) {
         const int i = __builtin_ctz(bits);
         bits &= bits - 1;
-        out[pos++] = v0 + i;
+        const int32_t v = v0 + i;
+        out[pos++] = make_int4(v, (int32_t)in_ptr[v], (int32_t)in_ptr[v + 1], 0);
     }
+}
+
+// batch of worklist item i: the last b with prefix[b] <= i (prefix non-decreasing) -- one
+// coalesced load of the prefix per 64 batches and a wave ballot, instead of a binary search
+// of dependent loads
+__device__ __forceinline__ int32_t wl_batch(const int64_t* __restrict__ prefix, int32_t nb, int64_t i, int lane) {
+    int32_t c = 0;
+    for (int32_t q = 0; q < nb; q += 64) {
+        const int32_t j = q + lane;
+        c += __popcll(__ballot(j < nb && prefix[j] <= i));
+    }
+    return c - 1;
 }
 
 // one wave per listed (vertex, batch): the T items of all batches in batch-major order
@@ -449,22 +481,16 @@ __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in
                                                   const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                   const int64_t* __restrict__ out_ptr,
                                                   const int32_t* __restrict__ out_dst, Pools pools, int32_t parity,
-                                                  const int32_t* __restrict__ wl, const int64_t* __restrict__ prefix,
+                                                  const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
                                                   int32_t nb, int64_t S, int32_t* __restrict__ cnt,
                                                   unsigned long long* __restrict__ prof) {
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t i = (int64_t)(blockIdx.x & 7) * S + (int64_t)(blockIdx.x >> 3) * 4 + wave;
     const int64_t T = prefix[nb];
     if ((int64_t)(blockIdx.x >> 3) * 4 + wave >= S || i >= T) return;
-    int32_t lo = 0, hi = nb;  // last batch with prefix <= i
-    while (hi - lo > 1) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (prefix[mid] <= i) lo = mid;
-        else hi = mid;
-    }
-    const int32_t b = lo;
-    const int32_t v = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])];
     const int lane = threadIdx.x & 63;
+    const int32_t b = wl_batch(prefix, nb, i, lane);
+    const int32_t v = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x;
     const BatchDev B = batch_view(pools, b);
     if (lane == 0) B.act(parity)[v] = 0;
     relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
@@ -658,6 +684,37 @@ __device__ __forceinline__ void mg_fold(MGState& S, double c, double du, int32_t
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
 
+// mg_fold with the recorded predecessor identified by its in-arc (one arc per tail in the
+// merged in-CSR), so the recorded state needs no tail lookup; S.pu is set whenever a
+// candidate is taken or refreshes the recorded predecessor
+__device__ __forceinline__ void mg_fold_arc(MGState& S, double c, double du, int32_t e, int32_t u) {
+    if (!(c < dinf())) return;  // a record seen before its distance (same round): next round
+    if (c < S.d) {
+        S.d = c;
+        S.bdu = du;
+        S.pa = e;
+        S.pu = u;
+        S.lt = du == c;  // degenerate d(u) == d(v): heap-order dependent
+        S.touched = true;
+    } else if (c == S.d) {
+        if (S.pa == e) {  // the recorded predecessor refreshed
+            S.lt = (du == S.bdu && S.lt) || du == c;
+            S.bdu = du;
+            S.pu = u;
+            S.touched = true;
+        } else if (du < S.bdu) {
+            S.bdu = du;
+            S.pa = e;
+            S.pu = u;
+            S.lt = du == c;
+            S.touched = true;
+        } else if (du == S.bdu) {
+            S.lt = true;  // two predecessors at the same d(u): heap pop order decides
+            S.touched = true;
+        }
+    }
+}
+
 
 // CSR round, changed tails only, stamped f32 keys (SHADOWTOPO_CSR_FILTERED).  One wave =
 // one destination v of one batch (lane = source).  Per chunk of 8 in-arcs: the tails' key
@@ -764,6 +821,151 @@ __global__ __launch_bounds__(256) void k_relax_st(const int64_t* __restrict__ in
     if (__ballot(ch)) {
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
+    }
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
+}
+
+// CSR masked round (SHADOWTOPO_CSR_MASKED, default for sparse graphs).  One wave = one
+// listed (vertex v, batch) of the round's frontier worklist (lane = source); v folds only the
+// (in-neighbour, source) pairs whose state changed in the previous round or this one.
+//  * The in-arcs are read 64 at a time, one per lane (coalesced tails and weights), and each
+//    lane gathers its tail's change record (32 B); a wave ballot compacts the arcs with a
+//    changed lane, and the wave walks only those, 8 at a time (uniform tail, weight and
+//    lane mask by readlane): 8 d(u) row loads in flight, each masked to the lanes whose
+//    source changed at u -- a row with one changed source costs one 64-byte line.  A hub
+//    whose in-list holds thousands of arcs but few changed tails costs a few vector loads,
+//    not a walk of every row.
+//  * v's own recorded state (D, BDU, P, H) is loaded only for lanes that receive a
+//    candidate, and the candidates fold into it with the rules of mg_fold: the unchanged
+//    pairs were folded when they last changed, so the recorded state plus the changed
+//    candidates is the full lexicographic minimum (the k_relax_delta argument).
+//  * A lane whose D, predecessor, hop count, reliability or taint changed is recorded in
+//    v's change record for this round, and v's out-neighbours go on the next worklist.
+//    A predecessor whose tree state changed at the same distance re-offers its candidate,
+//    which mg_fold sees as "the recorded predecessor refreshed" (hops / reliability are
+//    recomputed from it).
+// The fixed point is k_relax's, bit for bit (tests/test_csr_gpu.py).
+__global__ __launch_bounds__(256) void k_relax_cm(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                  const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                                  const int64_t* __restrict__ out_ptr,
+                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t round,
+                                                  const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
+                                                  int32_t nb, int64_t S_, int32_t* __restrict__ cnt,
+                                                  unsigned long long* __restrict__ prof) {
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i = (int64_t)(blockIdx.x & 7) * S_ + (int64_t)(blockIdx.x >> 3) * 4 + wave;
+    const int64_t T = prefix[nb];
+    if ((int64_t)(blockIdx.x >> 3) * 4 + wave >= S_ || i >= T) return;
+    const int lane = threadIdx.x & 63;
+    const int32_t b = wl_batch(prefix, nb, i, lane);
+    const int4 item = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])];
+    const int32_t v = __builtin_amdgcn_readfirstlane(item.x);
+    const int32_t beg = __builtin_amdgcn_readfirstlane(item.y), end = __builtin_amdgcn_readfirstlane(item.z);
+    const int32_t parity = round & 1;
+    const BatchDev B = batch_view(pools, b);
+    if (lane == 0) B.act(parity)[v] = 0;
+    const uint32_t rc = (uint32_t)round, rp = rc - 1u;
+    const CMask* cm = B.cm;
+    const int32_t sv = B.srcv[lane];
+    const bool live = sv >= 0 && sv != v;
+    const size_t idx = (size_t)v * KL + lane;
+    const gdouble* Dl = B.D + lane;
+    MGState S;
+    S.have = S.touched = S.lt = false;
+    S.D0 = S.B0 = S.d = S.bdu = dinf();
+    S.P0 = S.pa = S.pu = -1;
+    S.H0 = 0;
+    int32_t u_first = 0;  // the first 64 tails (the out-neighbours too, undirected)
+    for (int32_t base = beg; base < end; base += 64) {
+        const int32_t e = base + lane;
+        int32_t u = 0;
+        double w = 0.0;
+        unsigned long long m = 0ull;
+        if (e < end) {
+            u = in_src[e];
+            if (base == beg) u_first = u;
+            w = in_w[e];
+            const CMask c = cm[u];
+            m = ((c.rd[0] == rp || c.rd[0] == rc) ? c.m[0] : 0ull) | ((c.rd[1] == rp || c.rd[1] == rc) ? c.m[1] : 0ull);
+        }
+        unsigned long long arcs = __ballot(m != 0ull);
+        while (arcs) {
+            int32_t uk[8], ek[8];
+            double wk[8], du[8];
+            bool on[8];
+            bool anyl = false;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                on[j] = false;
+                uk[j] = 0;
+                ek[j] = 0;
+                wk[j] = 0.0;
+                if (arcs) {
+                    const int k = __builtin_ctzll(arcs);
+                    arcs &= arcs - 1ull;
+                    uk[j] = __builtin_amdgcn_readlane(u, k);
+                    wk[j] = readlane_d(w, k);
+                    ek[j] = base + k;
+                    on[j] = live && ((readlane_u64(m, k) >> lane) & 1ull);
+                    anyl |= on[j];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) du[j] = on[j] ? Dl[(size_t)uk[j] * KL] : 0.0;
+            if (anyl && !S.have) {  // the recorded state, only for lanes that receive a candidate
+                S.D0 = B.D[idx];
+                S.B0 = B.BDU[idx];
+                S.P0 = B.P[idx];
+                S.H0 = B.H[idx];
+                S.d = S.D0;
+                S.bdu = S.B0;
+                S.pa = S.P0;
+                S.pu = -1;  // the recorded predecessor's vertex, looked up only if the finish needs it
+                S.lt = (S.H0 & LTIE) != 0;
+                S.have = true;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (on[j]) mg_fold_arc(S, du[j] + wk[j], du[j], ek[j], uk[j]);  // altdist = mindist + weight
+        }
+    }
+    bool ch = false;
+    if (S.touched) {
+        if (S.pu < 0) S.pu = in_src[S.pa];  // a tie at the recorded predecessor: its vertex
+        const size_t uidx = (size_t)S.pu * KL + lane;
+        const uint32_t hu = B.H[uidx];
+        const double ru = B.R[uidx];
+        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (S.lt ? (TAINT | LTIE) : 0u);
+        const double r = ru * in_r[S.pa];
+        if (S.d != S.D0) {
+            ch = true;
+        } else {
+            const double R0 = B.R[idx];
+            ch = h != S.H0 || r != R0 || S.pa != S.P0;
+        }
+        if (ch) {
+            B.D[idx] = S.d;
+            B.H[idx] = h;
+            B.R[idx] = r;
+            B.P[idx] = S.pa;
+        }
+        if (S.bdu != S.B0) B.BDU[idx] = S.bdu;
+    }
+    const unsigned long long mask = __ballot(ch);
+    if (mask) {
+        if (lane == 0) {
+            CMask* c = B.cm + v;
+            c->m[parity] = mask;
+            c->rd[parity] = rc;
+        }
+        gbyte* act_nxt = B.act(parity ^ 1);
+        if (out_ptr == in_ptr && end - beg <= 64) {  // undirected: the out-neighbours are the tails in hand
+            if (beg + lane < end) act_nxt[u_first] = 1;
+        } else {
+            for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        }
         if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
         if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
     }
@@ -2134,7 +2336,7 @@ struct shadowtopo_engine {
     int32_t* d_cnt = nullptr;
     int32_t* h_cnt = nullptr;  // pinned
     // CSR frontier worklists (k_compact / k_relax_wl): [nb][Vp] active vertices, per-batch counts
-    int32_t* d_wl = nullptr;
+    int4* d_wl = nullptr;  // entries {v, in_ptr[v], in_ptr[v + 1], 0}
     uint32_t* d_wlcnt = nullptr;
     uint32_t* h_wlcnt = nullptr;  // pinned [nb]
     int64_t* d_wlpre = nullptr;   // [nb + 1] item prefix, uploaded per round
@@ -2247,10 +2449,11 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
     HIP_TRY(hipHostMalloc((void**)&eng->h_cnt, sizeof(int32_t) * nb, hipHostMallocDefault));
     if (!eng->dense) {
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wl, sizeof(int32_t) * VK / KL * nb)) ||
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wl, sizeof(int4) * VK / KL * nb)) ||
             (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlcnt, sizeof(uint32_t) * nb)) ||
             (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlpre, sizeof(int64_t) * (nb + 1))))
             return rc;
+        if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.cm, sizeof(CMask) * (size_t)eng->Vp * nb))) return rc;
         HIP_TRY(hipHostMalloc((void**)&eng->h_wlcnt, sizeof(uint32_t) * nb, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&eng->h_wlpre, sizeof(int64_t) * (nb + 1), hipHostMallocDefault));
     }
@@ -2280,7 +2483,7 @@ int ensure_replay(shadowtopo_engine* eng) {
 int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
-    const double per_batch = (double)eng->Vp * KL * 36.0 + 18.0 * eng->Vp;
+    const double per_batch = (double)eng->Vp * KL * 36.0 + 18.0 * eng->Vp + (eng->dense ? 0.0 : 36.0 * eng->Vp);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
@@ -2366,6 +2569,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         const size_t total = (size_t)eng->Vp * KL;
         int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
         hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp);
+        if (eng->pools.cm) HIP_TRY(hipMemsetAsync(eng->pools.cm, 0, sizeof(CMask) * (size_t)eng->Vp * nbg, s));
         hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools, eng->dense ? 0 : 1);
         HIP_TRY(hipGetLastError());
     }
@@ -2394,12 +2598,13 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         0x7f7f7f7e, (int64_t)V * KL * eng->opt_delta_permille / 1000);
     std::vector<uint8_t> full_b;  // dense: batches the full sweep covers this round
     // sparse FULL rounds over compacted frontier worklists (k_compact / k_relax_wl)
-    const bool use_wl = !eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL && eng->opt_worklist && eng->d_wl;
+    const bool masked = !eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_MASKED && eng->pools.cm && eng->d_wl;
+    const bool use_wl = masked || (!eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL && eng->opt_worklist && eng->d_wl);
     const int32_t ncb = (V + WL_SPAN - 1) / WL_SPAN;
     if (use_wl) {
         HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
         hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, 0, eng->d_wl,
-                           eng->d_wlcnt);
+                           eng->d_wlcnt, g.in_ptr);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -2415,7 +2620,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             if (wl_total == 0) break;  // nothing active: converged
         }
         // worklist only where it pays: a mostly-active round runs the plain grid
-        const bool round_wl = use_wl && wl_total * 2 < (int64_t)nbg * V;
+        const bool round_wl = use_wl && (masked || wl_total * 2 < (int64_t)nbg * V);
         if (round_wl)
             HIP_TRY(hipMemcpyAsync(eng->d_wlpre, eng->h_wlpre, sizeof(int64_t) * (nbg + 1), hipMemcpyHostToDevice, s));
         int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
@@ -2464,6 +2669,13 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             hipLaunchKernelGGL(k_relax_st, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_w32, g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1),
                                (int32_t)(round & 0x7fffffff), cnt_cur, eng->d_prof);
+        } else if (masked) {
+            eng->st.relax_batches += nbg;
+            eng->st.wl_launches++;
+            const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
+            hipLaunchKernelGGL(k_relax_cm, dim3((uint32_t)(8 * (S / 4))), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                               g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 0x7fffffff), eng->d_wl,
+                               eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else if (round_wl) {
             eng->st.relax_batches += nbg;
             eng->st.wl_launches++;
@@ -2487,7 +2699,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         if (use_wl) {  // the next round's worklists, from the flags this round set
             HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
             hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
-                               (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt);
+                               (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
         }
@@ -3205,7 +3417,8 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_dense_tb = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_CSR_VARIANT:
-            if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL && value != SHADOWTOPO_CSR_FILTERED)
+            if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL && value != SHADOWTOPO_CSR_FILTERED &&
+                value != SHADOWTOPO_CSR_MASKED)
                 return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
             eng->opt_csr_variant = (int32_t)value;
             return SHADOWTOPO_OK;

@@ -1,6 +1,7 @@
-"""CSR relaxation variants (k_relax, the default: full recomputation, over frontier
-worklists in sparse rounds; k_relax_st: changed tails only, round-stamped f32 keys;
-k_relax_delta: changed tails, f64) against the oracle and against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops, kind and
+"""CSR relaxation variants (k_relax_cm: changed (tail, source) pairs over frontier
+worklists; k_relax: full recomputation, over frontier worklists in sparse rounds;
+k_relax_st: changed tails only, round-stamped f32 keys; k_relax_delta: changed tails, f64,
+whole grid) against the oracle and against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops, kind and
 reliability; every variant must reach the same fixed point."""
 import numpy as np
 import pytest
@@ -41,7 +42,7 @@ def _case(case):
 CASES = ["sparse", "directed", "ties", "int_random", "vloss_prefer", "no_loops", "multigraph"]
 
 
-@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL, E.CSR_FILTERED])
+@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL, E.CSR_FILTERED, E.CSR_MASKED])
 @pytest.mark.parametrize("case", CASES)
 def test_csr_variants(case, variant):
     g = _case(case)
@@ -58,7 +59,7 @@ def test_csr_full_grid_without_worklists(case):
     compare(g, layout="csr", csr_variant=E.CSR_FULL, worklist=1, batches_in_flight=2)
 
 
-@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FILTERED])
+@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FILTERED, E.CSR_MASKED])
 def test_csr_delta_several_groups(variant):
     g = synth.random_sparse(V=500, avg_deg=4, seed=37)
     compare(g, layout="csr", batches_in_flight=3, csr_variant=variant)  # 500 sources -> 8 batches -> 3 groups
@@ -71,7 +72,7 @@ def test_csr_delta_same_fixed_point(case):
     g = _case(case)
     srcs = np.arange(0, g.n, 2, dtype=np.int32)
     outs = []
-    for variant in (E.CSR_FULL, E.CSR_DELTA, E.CSR_FILTERED):
+    for variant in (E.CSR_FULL, E.CSR_DELTA, E.CSR_FILTERED, E.CSR_MASKED):
         eng = E.Engine.from_synth(g, layout="csr")
         eng.set_option(E.OPT_CSR_VARIANT, variant)
         outs.append(eng.sssp(srcs))
