@@ -167,3 +167,42 @@ def test_tie_detector_flags_integer_grid():
     og2 = og_of(g2)
     d2, _ = og2.dijkstra(0)
     assert og2.tie_vertices(0, d2).sum() == 0
+
+
+@pytest.mark.parametrize("case", ["grid", "grid_big", "int_random", "int_directed", "ties_fixture"])
+def test_tie_break_second_restatement(case):
+    """The parity-unpinned branch has no reference fixture (igraph is absent), so the
+    tie-broken predecessors of topo_oracle.c are cross-checked against a second, independent
+    restatement of igraph's heap Dijkstra in pure Python (oracle/igraph_heap_ref.py), on
+    integer-latency graphs where heap-order ties are everywhere: parent edges, distances and
+    the pair rows must agree exactly."""
+    from oracle.igraph_heap_ref import RefGraph
+    if case == "grid":
+        g = synth.integer_grid(rows=8, cols=9, seed=3)
+    elif case == "grid_big":
+        g = synth.integer_grid(rows=14, cols=14, seed=11, max_lat=2)
+    elif case == "int_random":
+        g = synth.random_sparse(V=150, avg_deg=5, seed=33, int_lat=True)
+    elif case == "int_directed":
+        g = synth.random_sparse(V=120, avg_deg=4, seed=34, int_lat=True, directed=True)
+    else:
+        d = np.load(os.path.join(GOLD, "synthetic_ties.npz"))
+        g = synth.SynthGraph("ties", int(d["n"]), d["src"], d["dst"], d["latency"], d["packetloss"], d["vloss"],
+                             d["attached"], directed=bool(d["directed"]))
+    og = og_of(g)
+    rg = RefGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss, directed=g.directed)
+    att = np.asarray(g.attached)
+    lat, rel, hops, kind, _ = og.pair_rows(og.flags(), att)
+    ties = 0
+    for i, s in enumerate(att[: min(len(att), 24)]):
+        d_c, p_c = og.dijkstra(int(s), targets=att)
+        d_p, p_p = rg.dijkstra(int(s), att)
+        assert np.array_equal(np.asarray(d_p), d_c)
+        assert np.array_equal(np.asarray(p_p), p_c), f"source {s}: parent edges differ"
+        ties += int(og.tie_vertices(int(s), d_c).sum())
+        for j, t in enumerate(att):
+            if kind[i, j] != O.KIND_DIJKSTRA:
+                continue
+            pl, pr, ph = rg.pair(int(s), int(t), p_p)
+            assert (pl, pr, ph) == (lat[i, j], rel[i, j], hops[i, j]), (s, t)
+    assert ties > 0  # the fixtures do exercise heap-order ties
