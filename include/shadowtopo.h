@@ -21,6 +21,7 @@
 #ifndef SHADOWTOPO_H
 #define SHADOWTOPO_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -77,7 +78,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
                                               (vertex, source) pairs gets a change-mask delta round instead of a full
                                               sweep (default 125; 0 = always full sweeps) */
-#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default), _FILTERED or _DELTA */
+#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default), _MASKED, _FILTERED or _DELTA */
 #define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
 #define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Hilbert
                                               order of the top two principal axes of the distances to eight
@@ -100,18 +101,19 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               engine may take (default 1000); engines sharing one device split it */
 
 /* sparse (CSR) relaxation rounds (all exact, same fixed point):
- *   MASKED (default): over frontier worklists, fold only the (in-neighbour, source) pairs
- *     whose state changed, found through per-vertex round-stamped change records; the wave
- *     compacts the changed in-arcs with a ballot and loads their distance rows masked to
- *     the changed lanes; the vertex's own state is read only for lanes with a candidate
- *     (k_relax_cm);
- *   FULL: recompute every active vertex's minimum over all its in-arcs' 512-byte
+ *   FULL (default): recompute every active vertex's minimum over all its in-arcs' 512-byte
  *     distance rows (k_relax; rounds with few active pairs run over frontier worklists);
+ *   MASKED: over frontier worklists, fold only the (in-neighbour, source) pairs whose state
+ *     changed, found through per-vertex round-stamped change records; the wave compacts the
+ *     changed in-arcs with a ballot and loads their distance rows masked to the changed
+ *     lanes; the vertex's own state is read only for lanes with a candidate (k_relax_cm);
  *   FILTERED: fold only the in-neighbours whose state changed, found through round stamps
  *     in 256-byte f32 key rows, settling the f32-filter survivors in f64 (k_relax_st);
  *   DELTA: fold only changed in-neighbours, found through 64-bit change masks, in f64,
  *     over the whole grid.
- * FULL, FILTERED and DELTA are kept as cross-checks. */
+ * MASKED, FILTERED and DELTA read fewer rows but issue more instructions: on C4 MASKED
+ * fetches 12 % fewer bytes at 2.2x the VALU instructions and runs 1.3x longer than FULL
+ * (DESIGN.md 4); they are kept as cross-checks. */
 #define SHADOWTOPO_CSR_DELTA 0
 #define SHADOWTOPO_CSR_FULL 1
 #define SHADOWTOPO_CSR_FILTERED 2
@@ -182,13 +184,20 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value);
 
 /*
  * Attached-pair rows [row_begin, row_end) x count: lat (ms), rel, hops, kind.
- * Buffers are row-major with leading dimension `count`; kind may be NULL.
+ * Buffers are row-major with leading dimension `count`; hops and kind may be NULL.
  * mem = SHADOWTOPO_MEM_DEVICE: device pointers on the engine's device, written on
  * `stream` (a hipStream_t, NULL = the engine's own stream); the call returns after the
- * stream work is complete.  mem = SHADOWTOPO_MEM_HOST: host pointers.
+ * stream work is complete.  mem = SHADOWTOPO_MEM_HOST: host pointers; when they are all
+ * page-locked (shadowtopo_host_alloc) the rows are copied at full PCIe rate and a batch
+ * group's copy overlaps the next group's computation.
  */
 int shadowtopo_compute_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
                             uint32_t* hops, uint8_t* kind, int32_t mem, void* stream);
+
+/* Page-locked host memory that compute_rows copies into directly (from any device of the
+ * process); free with shadowtopo_host_free.  NULL-safe free. */
+int shadowtopo_host_alloc(size_t bytes, void** out);
+void shadowtopo_host_free(void* p);
 
 /*
  * Parity tooling: full single-source results for arbitrary source vertices (row-major

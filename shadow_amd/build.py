@@ -14,7 +14,7 @@ OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libshadowtopo_hip.so")
 ARCH = os.environ.get("SHADOWTOPO_ARCH", "gfx950")
 
-HIP_SOURCES = ["engine.hip"]
+HIP_SOURCES = ["engine.hip", "graph_build.hip"]
 C_SOURCES = ["graphml.c", "topology_hip.c", "shadow_hooks.c"]  # C host shim
 
 

@@ -34,9 +34,11 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
 #include <vector>
 
+#include "graph_build.h"
 #include "shadowtopo.h"
 
 namespace {
@@ -2086,7 +2088,7 @@ __global__ __launch_bounds__(256) void k_compose(GraphDev g, Pools pools,
         const int j = k >> 6, tl = k & 63;
         const int32_t r = B.row[j], ti = t0 + tl;
         if (r >= 0 && ti < A) {
-            out_hops[(size_t)(r - row_base) * A + ti] = su[j * 65 + tl];
+            if (out_hops) out_hops[(size_t)(r - row_base) * A + ti] = su[j * 65 + tl];
             if (out_kind) out_kind[(size_t)(r - row_base) * A + ti] = (uint8_t)su[64 * 65 + j * 65 + tl];
         }
     }
@@ -2256,7 +2258,7 @@ __global__ void k_compose_replay(GraphDev g, ReplayDev rp, const int32_t* __rest
     const size_t w = (size_t)(rp.row[slot] - row_base) * A + ti;
     out_lat[w] = o.lat;
     out_rel[w] = o.rel;
-    out_hops[w] = o.hops;
+    if (out_hops) out_hops[w] = o.hops;
     if (out_kind) out_kind[w] = o.kind;
 }
 
@@ -2310,7 +2312,9 @@ struct shadowtopo_engine {
     int32_t device = 0;
     GraphDev g{};
     std::vector<void*> graph_allocs;
-    // host mirrors for get_eid
+    // host mirrors for shadowtopo_get_eid, copied from the device on its first call
+    std::once_flag mirrors_once;
+    int mirrors_rc = 0;
     std::vector<int64_t> h_in_ptr;
     std::vector<int32_t> h_in_src, h_in_eid, h_loop_eid;
     hipStream_t own_stream = nullptr;
@@ -2344,6 +2348,10 @@ struct shadowtopo_engine {
     // staging for host outputs
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // pinned host destinations: group g's rows leave through staging slot g & 1 on the copy
+    // stream while group g + 1 relaxes
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_comp[2] = {nullptr, nullptr}, ev_copy[2] = {nullptr, nullptr};
     // replay scratch
     ReplayDev rp{};
     bool rp_ready = false;
@@ -2943,6 +2951,16 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     return SHADOWTOPO_OK;
 }
 
+// page-locked host memory (hipHostMalloc / shadowtopo_host_alloc / hipHostRegister)
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not an error for the caller
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
                       uint32_t* hops, uint8_t* kind, int32_t mem, hipStream_t s) {
     const int32_t A = eng->A;
@@ -2964,28 +2982,48 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     double *dl = lat, *dr = rel;
     uint32_t* dh = hops;
     uint8_t* dk = kind;
+    // host destinations: rows are composed into device staging and copied out per group;
+    // into pinned (page-locked) host memory -- shadowtopo_host_alloc, as the topology shim
+    // allocates its matrix -- the copy of group g runs on the copy stream behind group
+    // g + 1's relaxation (two staging slots), into pageable memory it is a synchronous copy
+    const bool pinned_out = mem == SHADOWTOPO_MEM_HOST && is_pinned(lat) && is_pinned(rel) &&
+                            (!hops || is_pinned(hops)) && (!kind || is_pinned(kind));
+    const int nslots = pinned_out && row_end - row_begin > group ? 2 : 1;
+    const size_t slot_bytes = ((size_t)group * A * (8 + 8 + (hops ? 4 : 0) + (kind ? 1 : 0)) + 255) & ~(size_t)255;
     if (mem == SHADOWTOPO_MEM_HOST) {
-        const size_t need = (size_t)group * A * (8 + 8 + 4 + 1) + 64;
+        const size_t need = slot_bytes * nslots + 64;
         if (eng->stage_bytes < need) {
+            if (eng->copy_stream) HIP_TRY(hipStreamSynchronize(eng->copy_stream));
             if (eng->stage) (void)hipFree(eng->stage);
             eng->stage = nullptr;
             eng->stage_bytes = 0;
             HIP_TRY(hipMalloc(&eng->stage, need));
             eng->stage_bytes = need;
         }
+        if (pinned_out && !eng->copy_stream) {
+            HIP_TRY(hipStreamCreateWithFlags(&eng->copy_stream, hipStreamNonBlocking));
+            for (int k = 0; k < 2; ++k) {
+                HIP_TRY(hipEventCreateWithFlags(&eng->ev_comp[k], hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&eng->ev_copy[k], hipEventDisableTiming));
+            }
+        }
     }
-    for (int32_t r0 = row_begin; r0 < row_end; r0 += group) {
+    int64_t gidx = 0;
+    for (int32_t r0 = row_begin; r0 < row_end; r0 += group, ++gidx) {
         const int32_t r1 = std::min(row_end, r0 + group);
         const int32_t nbg = (r1 - r0 + KL - 1) / KL;
+        const int slot = (int)(gidx % nslots);
         int32_t row_base = row_begin;
         if (mem == SHADOWTOPO_MEM_HOST) {
-            char* p = static_cast<char*>(eng->stage);
+            char* p = static_cast<char*>(eng->stage) + slot * slot_bytes;
             const size_t n = (size_t)group * A;
             dl = reinterpret_cast<double*>(p);
             dr = reinterpret_cast<double*>(p + n * 8);
-            dh = reinterpret_cast<uint32_t*>(p + n * 16);
-            dk = kind ? reinterpret_cast<uint8_t*>(p + n * 20) : nullptr;
+            dh = hops ? reinterpret_cast<uint32_t*>(p + n * 16) : nullptr;
+            dk = kind ? reinterpret_cast<uint8_t*>(p + n * (hops ? 20 : 16)) : nullptr;
             row_base = r0;
+            // the slot's previous rows (group g - 2) must have left before compose rewrites it
+            if (pinned_out && gidx >= nslots) HIP_TRY(hipStreamWaitEvent(s, eng->ev_copy[slot], 0));
         }
         lane_row.resize((size_t)nbg * KL);
         for (size_t i = 0; i < lane_row.size(); ++i) lane_row[i] = r0 + (int32_t)i < r1 ? r0 + (int32_t)i : -1;
@@ -3052,16 +3090,42 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         if (mem == SHADOWTOPO_MEM_HOST) {
             const size_t n = (size_t)(r1 - r0) * A;
             const size_t o = (size_t)(r0 - row_begin) * A;
-            HIP_TRY(hipMemcpyAsync(lat + o, dl, n * 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(rel + o, dr, n * 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(hops + o, dh, n * 4, hipMemcpyDeviceToHost, s));
-            if (kind) HIP_TRY(hipMemcpyAsync(kind + o, dk, n, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
+            hipStream_t cs = pinned_out ? eng->copy_stream : s;
+            if (pinned_out) {
+                HIP_TRY(hipEventRecord(eng->ev_comp[slot], s));
+                HIP_TRY(hipStreamWaitEvent(cs, eng->ev_comp[slot], 0));
+            }
+            HIP_TRY(hipMemcpyAsync(lat + o, dl, n * 8, hipMemcpyDeviceToHost, cs));
+            HIP_TRY(hipMemcpyAsync(rel + o, dr, n * 8, hipMemcpyDeviceToHost, cs));
+            if (hops) HIP_TRY(hipMemcpyAsync(hops + o, dh, n * 4, hipMemcpyDeviceToHost, cs));
+            if (kind) HIP_TRY(hipMemcpyAsync(kind + o, dk, n, hipMemcpyDeviceToHost, cs));
+            if (pinned_out)
+                HIP_TRY(hipEventRecord(eng->ev_copy[slot], cs));
+            else
+                HIP_TRY(hipStreamSynchronize(s));
         }
         eng->st.sources += r1 - r0;
         eng->st.batches += nbg;
     }
+    if (pinned_out) HIP_TRY(hipStreamSynchronize(eng->copy_stream));
     return SHADOWTOPO_OK;
+}
+
+int ensure_mirrors(shadowtopo_engine* eng) {
+    std::call_once(eng->mirrors_once, [eng] {
+        const size_t V = (size_t)eng->V, M = (size_t)eng->n_arcs;
+        eng->h_in_ptr.resize(V + 1);
+        eng->h_in_src.resize(M);
+        eng->h_in_eid.resize(M);
+        eng->h_loop_eid.resize(V);
+        const bool ok = hipSetDevice(eng->device) == hipSuccess &&
+                        hipMemcpy(eng->h_in_ptr.data(), eng->g.in_ptr, 8 * (V + 1), hipMemcpyDeviceToHost) == hipSuccess &&
+                        (M == 0 || hipMemcpy(eng->h_in_src.data(), eng->g.in_src, 4 * M, hipMemcpyDeviceToHost) == hipSuccess) &&
+                        (M == 0 || hipMemcpy(eng->h_in_eid.data(), eng->g.in_eid, 4 * M, hipMemcpyDeviceToHost) == hipSuccess) &&
+                        hipMemcpy(eng->h_loop_eid.data(), eng->g.loop_eid, 4 * V, hipMemcpyDeviceToHost) == hipSuccess;
+        eng->mirrors_rc = ok ? 0 : fail(SHADOWTOPO_EDEVICE, "get_eid host mirrors");
+    });
+    return eng->mirrors_rc;
 }
 
 }  // namespace
@@ -3087,7 +3151,9 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         return fail(SHADOWTOPO_EINVAL, "NULL edge array");
     const int32_t V = n_vertices;
     const bool directed = flags & SHADOWTOPO_F_DIRECTED;
+    int64_t n_loops = 0;
     for (int64_t e = 0; e < n_edges; ++e) {
+        n_loops += edge_source[e] == edge_target[e];
         if (edge_source[e] < 0 || edge_source[e] >= V || edge_target[e] < 0 || edge_target[e] >= V)
             return fail(SHADOWTOPO_EINVAL, "edge %lld endpoint out of range", (long long)e);
         if (!(edge_latency[e] > 0.0) || std::isinf(edge_latency[e]))
@@ -3106,156 +3172,52 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->E = n_edges;
     eng->device = device;
 
-    // igraph storage of the edges
-    std::vector<int32_t> efrom(n_edges), eto(n_edges);
-    std::vector<double> elat(edge_latency, edge_latency + n_edges), erel(n_edges);
-    for (int64_t e = 0; e < n_edges; ++e) {
-        int32_t a = edge_source[e], b = edge_target[e];
-        if (directed || a > b) {
-            efrom[e] = a;
-            eto[e] = b;
-        } else {
-            efrom[e] = b;
-            eto[e] = a;
-        }
-        erel[e] = 1.0 - edge_packetloss[e];
-    }
+    // The edge list goes to the device once; every derived table is built there
+    // (graph_build.hip: stable radix sorts + segment kernels), so engine creation costs an
+    // upload and a few sorts instead of host counting sorts over every arc.
     std::vector<double> vfac(V, 1.0);
     if (vertex_packetloss)
         for (int32_t v = 0; v < V; ++v)
             if (!std::isnan(vertex_packetloss[v])) vfac[v] = 1.0 - vertex_packetloss[v];
-    std::vector<int32_t> loop_eid(V, -1);
-    for (int64_t e = n_edges - 1; e >= 0; --e)
-        if (efrom[e] == eto[e]) loop_eid[efrom[e]] = (int32_t)e;
-
-    // relaxation in-CSR: arcs (u -> v) sorted by (v, u, eid), parallel arcs merged
-    std::vector<int32_t> au, av;
-    std::vector<int32_t> ae;
-    au.reserve((size_t)n_edges * (directed ? 1 : 2));
-    for (int64_t e = 0; e < n_edges; ++e) {
-        if (efrom[e] == eto[e]) continue;
-        au.push_back(efrom[e]);
-        av.push_back(eto[e]);
-        ae.push_back((int32_t)e);
-        if (!directed) {
-            au.push_back(eto[e]);
-            av.push_back(efrom[e]);
-            ae.push_back((int32_t)e);
-        }
-    }
-    if (au.size() >= 0x7fffffffULL) {
-        delete eng;
-        return fail(SHADOWTOPO_EINVAL, "too many arcs");
-    }
-    // arcs were generated in eid order: stable sort by u, then by v
+    int rc = 0;
+    graph_build::Built gb;
     {
-        std::vector<int64_t> idx(au.size()), tmp;
-        for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int64_t)i;
-        counting_sort(au, V, idx, tmp);
-        counting_sort(av, V, idx, tmp);
-        std::vector<int32_t> su(idx.size()), sv(idx.size()), se(idx.size());
-        for (size_t i = 0; i < idx.size(); ++i) {
-            su[i] = au[idx[i]];
-            sv[i] = av[idx[i]];
-            se[i] = ae[idx[i]];
+        int32_t *d_src = nullptr, *d_dst = nullptr;
+        double *d_lat = nullptr, *d_loss = nullptr;
+        const size_t ne = (size_t)std::max<int64_t>(n_edges, 1);
+        hipError_t e = hipMalloc((void**)&d_src, ne * 4);
+        if (e == hipSuccess) e = hipMalloc((void**)&d_dst, ne * 4);
+        if (e == hipSuccess) e = hipMalloc((void**)&d_lat, ne * 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&d_loss, ne * 8);
+        if (e == hipSuccess && n_edges > 0) {
+            e = hipMemcpy(d_src, edge_source, (size_t)n_edges * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(d_dst, edge_target, (size_t)n_edges * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(d_lat, edge_latency, (size_t)n_edges * 8, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(d_loss, edge_packetloss, (size_t)n_edges * 8, hipMemcpyHostToDevice);
         }
-        au.swap(su);
-        av.swap(sv);
-        ae.swap(se);
-    }
-    std::vector<int64_t> in_ptr(V + 1, 0);
-    std::vector<int32_t> in_src;
-    std::vector<double> in_w, in_r;
-    std::vector<int32_t> in_eid;
-    in_src.reserve(au.size());
-    in_w.reserve(au.size());
-    in_r.reserve(au.size());
-    in_eid.reserve(au.size());
-    int32_t multigraph = 0;
-    for (size_t i = 0; i < au.size();) {
-        size_t j = i;
-        double w = elat[ae[i]];
-        while (j + 1 < au.size() && av[j + 1] == av[i] && au[j + 1] == au[i]) {
-            ++j;
-            w = std::min(w, elat[ae[j]]);
-        }
-        const int32_t low = ae[i];  // lowest eid of the run (stable order)
-        if (w != elat[low]) multigraph = 1;
-        in_src.push_back(au[i]);
-        in_w.push_back(w);
-        in_r.push_back(erel[low]);
-        in_eid.push_back(low);
-        in_ptr[(size_t)av[i] + 1]++;
-        i = j + 1;
-    }
-    for (int32_t v = 0; v < V; ++v) in_ptr[(size_t)v + 1] += in_ptr[v];
-    for (int k = 0; k < CSR_PAD; ++k) {  // padding arcs for the unclamped chunk loads
-        in_src.push_back(0);
-        in_w.push_back(std::numeric_limits<double>::infinity());
-        in_r.push_back(0.0);
-        in_eid.push_back(-1);
-    }
-    std::vector<int64_t> out_ptr;
-    std::vector<int32_t> out_dst;
-    if (directed) {
-        out_ptr.assign((size_t)V + 1, 0);
-        for (int32_t v = 0; v < V; ++v)
-            for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) out_ptr[(size_t)in_src[x] + 1]++;
-        for (int32_t v = 0; v < V; ++v) out_ptr[(size_t)v + 1] += out_ptr[v];
-        out_dst.resize(in_src.size());
-        std::vector<int64_t> fill(out_ptr.begin(), out_ptr.end() - 1);
-        for (int32_t v = 0; v < V; ++v)
-            for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) out_dst[(size_t)fill[in_src[x]]++] = v;
-    }
-    // igraph_incident(OUT) order: edges with from==v by (to, eid), then (undirected) edges
-    // with to==v by (from, eid)
-    std::vector<int64_t> inc_ptr(V + 1, 0);
-    std::vector<int32_t> inc_eid;
-    {
-        std::vector<int64_t> oi(n_edges), ii, tmp;
-        for (int64_t e = 0; e < n_edges; ++e) oi[e] = e;
-        ii = oi;
-        counting_sort(eto, V, oi, tmp);
-        counting_sort(efrom, V, oi, tmp);
-        if (!directed) {
-            counting_sort(efrom, V, ii, tmp);
-            counting_sort(eto, V, ii, tmp);
-        }
-        std::vector<int64_t> os(V + 1, 0), is(V + 1, 0);
-        for (int64_t e = 0; e < n_edges; ++e) {
-            os[(size_t)efrom[e] + 1]++;
-            is[(size_t)eto[e] + 1]++;
-        }
-        for (int32_t v = 0; v < V; ++v) {
-            os[(size_t)v + 1] += os[v];
-            is[(size_t)v + 1] += is[v];
-        }
-        for (int32_t v = 0; v < V; ++v) {
-            int64_t d = os[(size_t)v + 1] - os[v];
-            if (!directed) d += is[(size_t)v + 1] - is[v];
-            inc_ptr[(size_t)v + 1] = inc_ptr[v] + d;
-        }
-        inc_eid.resize((size_t)inc_ptr[V]);
-        for (int32_t v = 0; v < V; ++v) {
-            int64_t k = inc_ptr[v];
-            for (int64_t x = os[v]; x < os[(size_t)v + 1]; ++x) inc_eid[(size_t)k++] = (int32_t)oi[x];
-            if (!directed)
-                for (int64_t x = is[v]; x < is[(size_t)v + 1]; ++x) inc_eid[(size_t)k++] = (int32_t)ii[x];
+        hipStream_t bs = nullptr;
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
+        if (e == hipSuccess)
+            e = graph_build::build(V, n_edges, n_loops, directed, CSR_PAD, d_src, d_dst, d_lat, d_loss, bs, gb,
+                                   eng->graph_allocs);
+        if (bs) (void)hipStreamDestroy(bs);
+        (void)hipFree(d_src);
+        (void)hipFree(d_dst);
+        (void)hipFree(d_lat);
+        (void)hipFree(d_loss);
+        if (e != hipSuccess) {
+            shadowtopo_destroy(eng);
+            return fail(e == hipErrorOutOfMemory ? SHADOWTOPO_ENOMEM : SHADOWTOPO_EDEVICE, "graph build: %s",
+                        hipGetErrorString(e));
         }
     }
+    const int32_t multigraph = gb.multigraph;
     // completeness, topology.c:450-552
-    if (flags & SHADOWTOPO_F_AUTO_COMPLETE) {
-        bool complete = true;
-        for (int32_t v = 0; v < V && complete; ++v) {
-            int64_t ecount = inc_ptr[(size_t)v + 1] - inc_ptr[v];
-            if (!directed && loop_eid[v] >= 0) ecount -= 1;
-            if (ecount < V) complete = false;
-        }
-        flags = (flags & ~SHADOWTOPO_F_COMPLETE) | (complete ? SHADOWTOPO_F_COMPLETE : 0u);
-    }
+    if (flags & SHADOWTOPO_F_AUTO_COMPLETE)
+        flags = (flags & ~SHADOWTOPO_F_COMPLETE) | (gb.complete ? SHADOWTOPO_F_COMPLETE : 0u);
     eng->flags = flags;
     eng->multigraph = multigraph;
-    eng->n_arcs = (int64_t)in_src.size() - CSR_PAD;
+    eng->n_arcs = gb.n_arcs;
     eng->Vp = (V + 63) / 64 * 64;  // dense tiles of 64 destinations, 32-row LDS chunks
     {
         const double VV = (double)V * (double)V;
@@ -3272,48 +3234,59 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     g.V = V;
     g.flags = flags;
     g.multigraph = multigraph;
-    std::vector<float> in_w32(in_w.size());
-    for (size_t x = 0; x < in_w.size(); ++x) in_w32[x] = f32_round_down(in_w[x]);
-    int rc = 0;
-    if ((rc = upload(eng, in_ptr, &g.in_ptr)) || (rc = upload(eng, in_src, &g.in_src)) ||
-        (rc = upload(eng, in_w, &g.in_w)) || (rc = upload(eng, in_w32, &g.in_w32)) || (rc = upload(eng, in_r, &g.in_r)) ||
-        (rc = upload(eng, in_eid, &g.in_eid)) || (rc = upload(eng, inc_ptr, &g.inc_ptr)) ||
-        (rc = upload(eng, inc_eid, &g.inc_eid)) || (rc = upload(eng, efrom, &g.efrom)) ||
-        (rc = upload(eng, eto, &g.eto)) || (rc = upload(eng, elat, &g.elat)) || (rc = upload(eng, erel, &g.erel)) ||
-        (rc = upload(eng, vfac, &g.vfac)) || (rc = upload(eng, loop_eid, &g.loop_eid))) {
+    g.in_ptr = gb.in_ptr;
+    g.in_src = gb.in_src;
+    g.in_w = gb.in_w;
+    g.in_w32 = gb.in_w32;
+    g.in_r = gb.in_r;
+    g.in_eid = gb.in_eid;
+    g.inc_ptr = gb.inc_ptr;
+    g.inc_eid = gb.inc_eid;
+    g.efrom = gb.efrom;
+    g.eto = gb.eto;
+    g.elat = gb.elat;
+    g.erel = gb.erel;
+    g.loop_eid = gb.loop_eid;
+    if ((rc = upload(eng, vfac, &g.vfac))) {
         shadowtopo_destroy(eng);
         return rc;
     }
     if (eng->dense) {
         const size_t Vp = (size_t)eng->Vp;
-        std::vector<double> W(Vp * Vp, std::numeric_limits<double>::infinity());
-        std::vector<int32_t> WI(Vp * Vp, -1);
-        std::vector<float> W32(Vp * Vp, std::numeric_limits<float>::quiet_NaN());
-        for (int32_t v = 0; v < V; ++v)
-            for (int64_t x = in_ptr[v]; x < in_ptr[(size_t)v + 1]; ++x) {
-                W[(size_t)in_src[x] * Vp + v] = in_w[x];
-                WI[(size_t)in_src[x] * Vp + v] = (int32_t)x;
-                W32[(size_t)in_src[x] * Vp + v] = f32_round_down(in_w[x]);
-            }
-        if ((rc = upload(eng, W, &eng->d_W)) || (rc = upload(eng, WI, &eng->d_WI)) ||
-            (rc = upload(eng, W32, &eng->d_W32))) {
+        double* W = nullptr;
+        int32_t* WI = nullptr;
+        float* W32 = nullptr;
+        if ((rc = dev_alloc(eng->graph_allocs, (void**)&W, Vp * Vp * sizeof(double))) ||
+            (rc = dev_alloc(eng->graph_allocs, (void**)&WI, Vp * Vp * sizeof(int32_t))) ||
+            (rc = dev_alloc(eng->graph_allocs, (void**)&W32, Vp * Vp * sizeof(float)))) {
             shadowtopo_destroy(eng);
             return rc;
         }
+        hipStream_t bs = nullptr;
+        hipError_t e = hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
+        if (e == hipSuccess) e = graph_build::build_dense(eng->Vp, gb, W, WI, W32, bs);
+        if (bs) (void)hipStreamDestroy(bs);
+        if (e != hipSuccess) {
+            shadowtopo_destroy(eng);
+            return fail(SHADOWTOPO_EDEVICE, "dense tables: %s", hipGetErrorString(e));
+        }
+        eng->d_W = W;
+        eng->d_WI = WI;
+        eng->d_W32 = W32;
     }
-    if (directed) {
-        if ((rc = upload(eng, out_ptr, &g.out_ptr)) || (rc = upload(eng, out_dst, &g.out_dst))) {
-            shadowtopo_destroy(eng);
-            return rc;
+    // the arc heads were needed only for the dense tables
+    for (auto& p : eng->graph_allocs)
+        if (p == (void*)gb.arc_v) {
+            (void)hipFree(p);
+            p = nullptr;
         }
+    if (directed) {
+        g.out_ptr = gb.out_ptr;
+        g.out_dst = gb.out_dst;
     } else {
         g.out_ptr = g.in_ptr;
         g.out_dst = g.in_src;
     }
-    eng->h_in_ptr.swap(in_ptr);
-    eng->h_in_src.swap(in_src);
-    eng->h_in_eid.swap(in_eid);
-    eng->h_loop_eid.swap(loop_eid);
     if (hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess ||
         hipEventCreate(&eng->evm) != hipSuccess || hipEventCreate(&eng->evm2) != hipSuccess) {
@@ -3352,6 +3325,12 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->ev1) (void)hipEventDestroy(eng->ev1);
     if (eng->evm) (void)hipEventDestroy(eng->evm);
     if (eng->evm2) (void)hipEventDestroy(eng->evm2);
+    if (eng->copy_stream) (void)hipStreamSynchronize(eng->copy_stream);
+    for (int k = 0; k < 2; ++k) {
+        if (eng->ev_comp[k]) (void)hipEventDestroy(eng->ev_comp[k]);
+        if (eng->ev_copy[k]) (void)hipEventDestroy(eng->ev_copy[k]);
+    }
+    if (eng->copy_stream) (void)hipStreamDestroy(eng->copy_stream);
     if (eng->own_stream) (void)hipStreamDestroy(eng->own_stream);
     delete eng;
 }
@@ -3457,7 +3436,7 @@ int shadowtopo_compute_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t r
     if (!eng->d_attached) return fail(SHADOWTOPO_ESTATE, "shadowtopo_set_attached not called");
     if (row_begin < 0 || row_end > eng->A || row_begin > row_end) return fail(SHADOWTOPO_EINVAL, "bad row range");
     if (row_begin == row_end) return SHADOWTOPO_OK;
-    if (!lat || !rel || !hops) return fail(SHADOWTOPO_EINVAL, "NULL output");
+    if (!lat || !rel) return fail(SHADOWTOPO_EINVAL, "NULL output");
     if (mem != SHADOWTOPO_MEM_HOST && mem != SHADOWTOPO_MEM_DEVICE) return fail(SHADOWTOPO_EINVAL, "bad mem kind");
     HIP_TRY(hipSetDevice(eng->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
@@ -3516,6 +3495,22 @@ int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_so
     return rc;
 }
 
+int shadowtopo_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(SHADOWTOPO_EINVAL, "NULL argument");
+    *out = nullptr;
+    // portable: any device of the process (the shim's SHADOWTOPO_DEVICES engines) copies into it
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocPortable);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(SHADOWTOPO_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    }
+    return SHADOWTOPO_OK;
+}
+
+void shadowtopo_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out) {
     if (!eng || !out) return fail(SHADOWTOPO_EINVAL, "NULL argument");
     *out = eng->st;
@@ -3541,6 +3536,7 @@ int shadowtopo_is_complete(const shadowtopo_engine* eng) {
 
 int64_t shadowtopo_get_eid(const shadowtopo_engine* eng, int32_t from, int32_t to) {
     if (!eng || from < 0 || to < 0 || from >= eng->V || to >= eng->V) return -1;
+    if (ensure_mirrors(const_cast<shadowtopo_engine*>(eng))) return -1;
     if (from == to) return eng->h_loop_eid[from];
     const int64_t b = eng->h_in_ptr[to], e = eng->h_in_ptr[(size_t)to + 1];
     auto it = std::lower_bound(eng->h_in_src.begin() + b, eng->h_in_src.begin() + e, from);

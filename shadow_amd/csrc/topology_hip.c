@@ -135,11 +135,15 @@ static void ipt_del(iptable* t, uint32_t ip) {
 }
 
 /* ------------------------------------------------------------ state */
+/* the attached-pair matrix: latency, reliability and pair kind (the API never exposes hop
+ * counts, so they are not copied out); page-locked when the engine can provide it, so the
+ * device rows arrive at full PCIe rate, a batch group's copy behind the next group's
+ * computation (shadowtopo_host_alloc) */
 typedef struct matrix {
     int32_t A;
+    int pinned;
     double* lat;
     double* rel;
-    uint32_t* hops;
     uint8_t* kind;
     struct matrix* next; /* retired matrices (readers may still hold them) */
 } matrix;
@@ -647,12 +651,18 @@ static int extract(Topology* top) {
 }
 
 /* ------------------------------------------------------------ lifecycle */
+static void mat_free(const matrix* m, void* p) {
+    if (m->pinned)
+        shadowtopo_host_free(p);
+    else
+        free(p);
+}
+
 static void free_matrix(matrix* m) {
     if (!m) return;
-    free(m->lat);
-    free(m->rel);
-    free(m->hops);
-    free(m->kind);
+    mat_free(m, m->lat);
+    mat_free(m, m->rel);
+    mat_free(m, m->kind);
     free(m);
 }
 
@@ -1281,7 +1291,6 @@ typedef struct {
     int32_t A, r0, r1;
     double* lat;
     double* rel;
-    uint32_t* hops;
     uint8_t* kind;
     int rc;
     char err[256];
@@ -1291,7 +1300,7 @@ static void* compute_block(void* arg) {
     row_block* w = arg;
     w->rc = shadowtopo_set_attached(w->eng, w->attached, w->A);
     if (w->rc == SHADOWTOPO_OK && w->r1 > w->r0)
-        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->lat, w->rel, w->hops, w->kind, SHADOWTOPO_MEM_HOST,
+        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->lat, w->rel, NULL, w->kind, SHADOWTOPO_MEM_HOST,
                                         NULL);
     if (w->rc != SHADOWTOPO_OK) snprintf(w->err, sizeof w->err, "%s", shadowtopo_last_error());
     return NULL;
@@ -1316,7 +1325,6 @@ static int compute_rows_sharded(Topology* top, const int32_t* attached, int32_t 
         const size_t o = (size_t)b->r0 * (size_t)A;
         b->lat = m->lat + o;
         b->rel = m->rel + o;
-        b->hops = m->hops + o;
         b->kind = m->kind + o;
         b->rc = 0;
         b->err[0] = 0;
@@ -1345,11 +1353,25 @@ static matrix* alloc_matrix(int32_t A) {
     if (!m) return NULL;
     size_t n = (size_t)A * (size_t)A;
     m->A = A;
-    m->lat = malloc(sizeof(double) * (n ? n : 1));
-    m->rel = malloc(sizeof(double) * (n ? n : 1));
-    m->hops = malloc(sizeof(uint32_t) * (n ? n : 1));
-    m->kind = malloc(n ? n : 1);
-    if (!m->lat || !m->rel || !m->hops || !m->kind) {
+    /* page-locked first; plain malloc when the driver refuses (the copy is then slower) */
+    void *pl = NULL, *pr = NULL, *pk = NULL;
+    if (shadowtopo_host_alloc(sizeof(double) * (n ? n : 1), &pl) == SHADOWTOPO_OK &&
+        shadowtopo_host_alloc(sizeof(double) * (n ? n : 1), &pr) == SHADOWTOPO_OK &&
+        shadowtopo_host_alloc(n ? n : 1, &pk) == SHADOWTOPO_OK) {
+        m->pinned = 1;
+        m->lat = pl;
+        m->rel = pr;
+        m->kind = pk;
+    } else {
+        shadowtopo_host_free(pl);
+        shadowtopo_host_free(pr);
+        shadowtopo_host_free(pk);
+        m->pinned = 0;
+        m->lat = malloc(sizeof(double) * (n ? n : 1));
+        m->rel = malloc(sizeof(double) * (n ? n : 1));
+        m->kind = malloc(n ? n : 1);
+    }
+    if (!m->lat || !m->rel || !m->kind) {
         st_critical("out of host memory for the %d x %d attached-pair matrix", A, A);
         free_matrix(m);
         return NULL;
@@ -1379,13 +1401,11 @@ static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A,
         const size_t src = (size_t)i * (size_t)A0, dst = (size_t)i * (size_t)A;
         memcpy(m->lat + dst, old->lat + src, sizeof(double) * (size_t)A0);
         memcpy(m->rel + dst, old->rel + src, sizeof(double) * (size_t)A0);
-        memcpy(m->hops + dst, old->hops + src, sizeof(uint32_t) * (size_t)A0);
         memcpy(m->kind + dst, old->kind + src, (size_t)A0);
         for (int32_t j = A0; j < A; j++) {
             const size_t o = dst + (size_t)j, r = (size_t)j * (size_t)A + (size_t)i;
             m->lat[o] = m->lat[r];
             m->rel[o] = m->rel[r];
-            m->hops[o] = m->hops[r];
             m->kind[o] = m->kind[r];
         }
     }

@@ -53,6 +53,7 @@ ENGINE_SYMBOLS = (
     "shadowtopo_device_count", "shadowtopo_last_error", "shadowtopo_create", "shadowtopo_destroy",
     "shadowtopo_set_attached", "shadowtopo_set_option", "shadowtopo_compute_rows", "shadowtopo_sssp",
     "shadowtopo_get_stats", "shadowtopo_reset_stats", "shadowtopo_is_complete", "shadowtopo_get_eid",
+    "shadowtopo_host_alloc", "shadowtopo_host_free",
 )
 
 
@@ -108,6 +109,9 @@ def lib():
         L.shadowtopo_is_complete.argtypes = [vp]
         L.shadowtopo_get_eid.restype = ctypes.c_int64
         L.shadowtopo_get_eid.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+        L.shadowtopo_host_alloc.restype = ctypes.c_int
+        L.shadowtopo_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+        L.shadowtopo_host_free.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -120,6 +124,31 @@ def _check(rc):
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class _Pinned:
+    """page-locked host allocation (shadowtopo_host_alloc), freed with the last array view"""
+
+    def __init__(self, nbytes):
+        self.p = ctypes.c_void_p()
+        _check(lib().shadowtopo_host_alloc(max(1, int(nbytes)), ctypes.byref(self.p)))
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        if self.p:
+            lib().shadowtopo_host_free(self.p)
+            self.p = None
+
+
+def pinned_empty(shape, dtype):
+    """numpy array in page-locked host memory (what the topology shim allocates its matrix
+    in): compute_rows copies into it at full PCIe rate"""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    buf = _Pinned(n)
+    raw = (ctypes.c_uint8 * max(1, n)).from_address(buf.p.value)
+    raw._owner = buf  # the allocation lives as long as any view of it
+    return np.frombuffer(raw, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
 
 
 def device_count():
@@ -193,18 +222,28 @@ class Engine:
     def set_option(self, key, value):
         _check(lib().shadowtopo_set_option(self._h, int(key), int(value)))
 
-    def compute_rows(self, row_begin=0, row_end=None, want_kind=True):
-        """host numpy outputs: lat, rel, hops, kind for rows [row_begin, row_end)"""
+    def compute_rows(self, row_begin=0, row_end=None, want_kind=True, want_hops=True, pinned=False):
+        """host numpy outputs: lat, rel, hops, kind for rows [row_begin, row_end); pinned=True
+        puts them in page-locked memory (the shim's layout and copy path); hops / kind are
+        None when not wanted"""
         if row_end is None:
             row_end = self.A
         R = row_end - row_begin
-        lat = np.empty((R, self.A), np.float64)
-        rel = np.empty((R, self.A), np.float64)
-        hops = np.empty((R, self.A), np.uint32)
-        kind = np.empty((R, self.A), np.uint8) if want_kind else None
+        mk = pinned_empty if pinned else np.empty
+        lat = mk((R, self.A), np.float64)
+        rel = mk((R, self.A), np.float64)
+        hops = mk((R, self.A), np.uint32) if want_hops else None
+        kind = mk((R, self.A), np.uint8) if want_kind else None
+        self.compute_rows_into(row_begin, row_end, lat, rel, hops, kind)
+        return lat, rel, hops, kind
+
+    def compute_rows_into(self, row_begin, row_end, lat, rel, hops=None, kind=None):
+        """rows [row_begin, row_end) into caller-owned host arrays ([rows, A], C order)"""
+        for a, dt in ((lat, np.float64), (rel, np.float64), (hops, np.uint32), (kind, np.uint8)):
+            if a is not None and (a.dtype != dt or not a.flags.c_contiguous or a.size < (row_end - row_begin) * self.A):
+                raise ValueError("output arrays must be C-contiguous [rows, A] of the right dtype")
         _check(lib().shadowtopo_compute_rows(self._h, int(row_begin), int(row_end), _ptr(lat), _ptr(rel), _ptr(hops),
                                              _ptr(kind), MEM_HOST, None))
-        return lat, rel, hops, kind
 
     def compute_rows_device(self, row_begin, row_end, lat_ptr, rel_ptr, hops_ptr, kind_ptr=None, stream=None):
         """device outputs (raw pointers, e.g. torch tensors' data_ptr()) on `stream`"""

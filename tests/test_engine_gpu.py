@@ -7,7 +7,7 @@ reference's order, topology.c:1429-1499); the north-star tolerance for reliabili
 import numpy as np
 import pytest
 
-from paritylib import compare, oracle_for
+from paritylib import assert_bitexact, compare, oracle_for, oracle_matrix
 from shadow_amd import engine as E
 from shadow_amd import synth
 
@@ -306,3 +306,36 @@ def test_dense_prune_same_results(case):
                               y.view(np.uint8) if y.dtype == np.float64 else y)
     if case != "geometric_big":
         assert compare(g, layout="dense")["dense"] == 1
+
+
+@pytest.mark.parametrize("layout", ["csr", "dense"])
+def test_pinned_host_rows_pipelined(layout):
+    """Rows into page-locked host memory (the shim's path): with several batch groups the
+    copy of group g runs on the copy stream behind group g + 1 through two staging slots;
+    without hops (the shim never copies them).  Bit-identical to pageable buffers and to the
+    oracle."""
+    g = synth.random_sparse(V=700, avg_deg=5, seed=52, A=500)
+    lat_o, rel_o, hops_o, kind_o, _ = oracle_matrix(g)
+    eng = E.Engine.from_synth(g, layout=layout)
+    eng.set_option(E.OPT_BATCHES_IN_FLIGHT, 2)  # 500 rows -> 8 batches -> 4 groups
+    eng.set_attached(g.attached)
+    A = len(g.attached)
+    lat = E.pinned_empty((A, A), np.float64)
+    rel = E.pinned_empty((A, A), np.float64)
+    kind = E.pinned_empty((A, A), np.uint8)
+    lat[:] = 7.0
+    eng.compute_rows_into(0, A, lat, rel, None, kind)
+    assert_bitexact("latency", lat, lat_o)
+    assert_bitexact("reliability", rel, rel_o)
+    assert_bitexact("kind", kind, kind_o)
+    # a sub-range with hops, pinned, against the pageable path
+    hops = E.pinned_empty((A - 130, A), np.uint32)
+    lat2 = E.pinned_empty((A - 130, A), np.float64)
+    rel2 = E.pinned_empty((A - 130, A), np.float64)
+    eng.compute_rows_into(100, A - 30, lat2, rel2, hops, None)
+    pl, pr, ph, _ = eng.compute_rows(100, A - 30, want_kind=False)
+    eng.close()
+    assert_bitexact("latency", lat2, pl)
+    assert_bitexact("reliability", rel2, pr)
+    assert_bitexact("hops", hops, ph)
+    assert_bitexact("hops", hops, hops_o[100:A - 30])
