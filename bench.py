@@ -215,29 +215,19 @@ def main():
     # same bytes) are computed in `chunks` row chunks; each chunk's lat/rel/hops rows live in
     # ONE packed byte buffer [lat f64 | rel f64 | hops i32], so one RCCL all-gather per chunk
     # moves all three, and chunk c's all-gather (RCCL's own stream, xGMI) overlaps the
-    # computation of chunk c+1 on the engine's stream.  Every rank ends with the full matrix
-    # in the layout [chunk][rank][lat | rel | hops][chunk rows][A] (shard.pack_views).
+    # computation of chunk c+1 on the engine's stream (shard.RowExchange; the same code path
+    # runs in tests/test_shard_gloo.py with world size 2 on gloo).
     # (measured at N=1: 2 chunks cost +0.9 ms of per-chunk overhead, so overlap pays only
     # where the exchange is long: 8 ranks move ~1.1 GB into every GPU per step)
     chunks = args.chunks or (2 if world >= 8 else 1)
-    bounds = shard.chunk_rows(per, chunks)
-    packs = [torch.zeros(shard.packed_bytes(n, A), dtype=torch.uint8, device=dev) for _, n in bounds]
-    views = [shard.pack_views(b, n, A) for b, (_, n) in zip(packs, bounds)]
-    gathered = ([torch.empty(world * p.numel(), dtype=torch.uint8, device=dev) for p in packs]
-                if world > 1 else None)
+    ex = shard.RowExchange(dist, A, world, rank, dev, chunks)
+
+    def compute(a, z, lat, rel, hops):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
 
     def step():
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        works = []
-        for c, (c0, n) in enumerate(bounds):
-            a, z = r0 + c0, min(r1, r0 + c0 + n)  # this chunk's real rows
-            if z > a:
-                lat, rel, hops = views[c]
-                eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
-            if world > 1:  # returns after the chunk is computed; the gather runs behind the next chunk
-                works.append(dist.all_gather_into_tensor(gathered[c], packs[c], async_op=True))
-        for w in works:
-            w.wait()
+        ex.step(compute)
 
     for i in range(max(1, args.warmup)):
         step()

@@ -75,3 +75,57 @@ def assemble(dist, compute_block, A, world, rank, device, dtypes):
     if world == 1:
         return [b[:A] for b in bufs]
     return [gather_rows(dist, b, per, world)[:A] for b in bufs]
+
+
+class RowExchange:
+    """The multi-GPU step of bench.py: this rank's source rows, computed in
+    row chunks of whole 64-source batches into packed [lat | rel | hops] buffers (one
+    buffer per chunk, ``pack_views``), each chunk all-gathered asynchronously (RCCL over
+    xGMI with backend "nccl") while the next chunk is computed; after ``step`` every rank
+    holds every rank's rows.  ``compute(a, z, lat, rel, hops)`` fills rows [a, z) of the
+    attached-pair matrix into the [z - a, A] views (the engine on a GPU; tests pass a CPU
+    stand-in and the gloo backend)."""
+
+    def __init__(self, dist, A: int, world: int, rank: int, device, chunks: int = 1):
+        import torch
+        self.dist, self.A, self.world, self.rank = dist, A, world, rank
+        self.r0, self.r1, self.per = shard_rows(A, world, rank)
+        self.bounds = chunk_rows(self.per, chunks)
+        self.packs = [torch.zeros(packed_bytes(n, A), dtype=torch.uint8, device=device) for _, n in self.bounds]
+        self.views = [pack_views(b, n, A) for b, (_, n) in zip(self.packs, self.bounds)]
+        self.gathered = ([torch.empty(world * p.numel(), dtype=torch.uint8, device=device) for p in self.packs]
+                         if world > 1 else None)
+
+    @property
+    def rows(self) -> int:
+        return self.r1 - self.r0
+
+    def step(self, compute):
+        works = []
+        for c, (c0, n) in enumerate(self.bounds):
+            a, z = self.r0 + c0, min(self.r1, self.r0 + c0 + n)  # this chunk's real rows
+            if z > a:
+                lat, rel, hops = self.views[c]
+                compute(a, z, lat, rel, hops)
+            if self.world > 1:  # returns once the chunk is computed; the gather runs behind the next chunk
+                works.append(self.dist.all_gather_into_tensor(self.gathered[c], self.packs[c], async_op=True))
+        for w in works:
+            w.wait()
+
+    def full(self):
+        """the assembled [A, A] lat, rel, hops (torch, on the buffers' device) after step()"""
+        import torch
+        dev = self.packs[0].device
+        out = (torch.empty((self.A, self.A), dtype=torch.float64, device=dev),
+               torch.empty((self.A, self.A), dtype=torch.float64, device=dev),
+               torch.empty((self.A, self.A), dtype=torch.int32, device=dev))
+        for c, (c0, n) in enumerate(self.bounds):
+            parts = (unpack_gathered(self.gathered[c], self.world, n, self.A) if self.world > 1
+                     else [self.views[c]])
+            for rr, views in enumerate(parts):
+                s0, s1, _ = shard_rows(self.A, self.world, rr)
+                a, z = s0 + c0, min(s1, s0 + c0 + n)
+                if z > a:
+                    for o, v in zip(out, views):
+                        o[a:z] = v[:z - a]
+        return out

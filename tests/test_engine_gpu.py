@@ -339,3 +339,31 @@ def test_pinned_host_rows_pipelined(layout):
     assert_bitexact("reliability", rel2, pr)
     assert_bitexact("hops", hops, ph)
     assert_bitexact("hops", hops, hops_o[100:A - 30])
+
+
+def test_row_exchange_with_engine_device_rows():
+    """bench.py's step (shard.RowExchange) with the engine's device rows (compute_rows_device
+    on torch's stream) in two row chunks, world size 1: the assembled matrix equals the
+    oracle's"""
+    import torch
+
+    from shadow_amd import shard
+    g = synth.random_sparse(V=600, avg_deg=5, seed=53, A=300)
+    lat_o, rel_o, hops_o, _, _ = oracle_matrix(g)
+    eng = E.Engine.from_synth(g)
+    eng.set_attached(g.attached)
+    dev = torch.device("cuda:0")
+    ex = shard.RowExchange(None, len(g.attached), 1, 0, dev, chunks=2)
+    assert len(ex.bounds) == 2
+
+    def compute(a, z, lat, rel, hops):
+        eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(),
+                                stream=torch.cuda.current_stream(dev).cuda_stream)
+
+    ex.step(compute)
+    torch.cuda.synchronize(dev)
+    lat, rel, hops = (x.cpu().numpy() for x in ex.full())
+    eng.close()
+    assert_bitexact("latency", lat, lat_o)
+    assert_bitexact("reliability", rel, rel_o)
+    assert_bitexact("hops", hops.astype(np.uint32), hops_o)

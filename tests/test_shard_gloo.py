@@ -139,3 +139,58 @@ def test_chunk_rows_cover_exactly():
             assert sum(n for _, n in b) == per
             assert all(o % 64 == 0 for o, _ in b)
             assert [o for o, _ in b] == sorted(o for o, _ in b)
+
+
+def _worker_exchange(rank, world, port, A_sel, chunks, q):
+    """bench.py's own step (shard.RowExchange), run twice, with the oracle as the compute
+    stand-in (the engine needs a GPU; tests/test_engine_gpu.py drives the same class with
+    the engine's device rows)"""
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from shadow_amd import synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = synth.random_sparse(V=160, avg_deg=4, seed=79, A=A_sel)
+    og = O.OracleGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss)
+    flags = og.flags()
+    A = len(g.attached)
+    ex = shard.RowExchange(dist, A, world, rank, "cpu", chunks)
+    calls = []
+
+    def compute(a, z, lat, rel, hops):
+        l, r, h, _, _ = og.pair_rows(flags, g.attached, a, z)
+        lat[:z - a] = torch.from_numpy(l)
+        rel[:z - a] = torch.from_numpy(r)
+        hops[:z - a] = torch.from_numpy(h.astype(np.int32))
+        calls.append((a, z))
+
+    full = og.pair_rows(flags, g.attached)
+    ok = True
+    for _ in range(2):  # buffers are reused step after step
+        ex.step(compute)
+        lat, rel, hops = ex.full()
+        ok &= np.array_equal(lat.numpy().view(np.uint64), full[0].view(np.uint64))
+        ok &= np.array_equal(rel.numpy().view(np.uint64), full[1].view(np.uint64))
+        ok &= np.array_equal(hops.numpy(), full[2].astype(np.int32))
+    mine = sorted(set(calls))
+    ok &= sum(z - a for a, z in mine) == ex.rows and all(ex.r0 <= a < z <= ex.r1 for a, z in mine)
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("A_sel,chunks", [(160, 1), (150, 2), (131, 3)])
+def test_two_rank_row_exchange_step(A_sel, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_exchange, args=(r, 2, port, A_sel, chunks, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert res == [(0, True), (1, True)]
