@@ -153,7 +153,8 @@ def main():
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
-    ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists (1, default) or the full grid (0)")
+    ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists when under half the pairs are active (1, default), "
+                         "always (2), or the full grid (0)")
     ap.add_argument("--csr-variant", type=int, default=1,
                     help="3 = changed (tail, source) pairs over worklists, 1 = full recomputation, "
                          "2 = changed tails with stamped f32 keys, 0 = f64 delta rounds")

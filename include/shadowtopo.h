@@ -96,7 +96,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               0 = every chunk filtered, original order. Results are identical. */
 
 #define SHADOWTOPO_OPT_WORKLIST 14         /* CSR FULL rounds: 1 (default) = over compacted frontier worklists (one
-                                              wave per active (vertex, batch) pair), 0 = one wave per pair of the grid */
+                                              wave per active (vertex, batch) pair) when under half the pairs are
+                                              active, the grid otherwise; 2 = worklists always; 0 = one wave per pair
+                                              of the grid */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
                                               engine may take (default 1000); engines sharing one device split it */
 

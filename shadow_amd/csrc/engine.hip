@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <limits>
@@ -245,25 +246,31 @@ __device__ __forceinline__ int32_t get_eid(const GraphDev& g, int32_t from, int3
 }
 
 // ---------------------------------------------------------------- batch state init
-__global__ void k_init(Pools pools, int32_t V) {
+// D = +inf is the whole unreached state for the FULL and MASKED rounds: H, R and P of a
+// (vertex, source) are read only once its D is finite, i.e. after a round wrote all four,
+// so `tree` (set for the kernels that read them eagerly) is the only reason to write them.
+__global__ void k_init(Pools pools, int32_t V, int32_t tree) {
     const BatchDev B = batch_view(pools, blockIdx.y);
     const size_t total = (size_t)V * KL;
     const double inf = dinf();
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         B.D[i] = inf;
-        B.H[i] = 0;
-        B.R[i] = 0.0;
-        B.P[i] = -1;
+        if (tree) {
+            B.H[i] = 0;
+            B.R[i] = 0.0;
+            B.P[i] = -1;
+        }
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
         B.act0[i] = 0;
         B.act1[i] = 0;
     }
     if (B.chm0) {
-        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-            B.BDU[i] = inf;
-            if (B.D32) B.D32[i] = __int_as_float(0x7fc00000);
-        }
+        if (tree)
+            for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+                if (B.BDU) B.BDU[i] = inf;
+                if (B.D32) B.D32[i] = __int_as_float(0x7fc00000);
+            }
         for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
             B.chm0[i] = 0;
             B.chm1[i] = 0;
@@ -2271,13 +2278,15 @@ __global__ void k_extract(GraphDev g, Pools pools, int32_t nsrc, double* dist, i
     const BatchDev B = batch_view(pools, 0);
     const size_t idx = (size_t)v * KL + j;
     const size_t o = (size_t)j * g.V + v;
-    if (dist) dist[o] = B.D[idx];
+    const double d = B.D[idx];
+    const bool reached = d < dinf();  // an unreached state's H / R / P were never written
+    if (dist) dist[o] = d;
     if (pred) {
-        const int32_t p = B.P[idx];
+        const int32_t p = reached ? B.P[idx] : -1;
         pred[o] = p >= 0 ? g.in_src[p] : -1;
     }
-    if (hops) hops[o] = B.H[idx] & HMASK;
-    if (tie) tie[o] = (B.H[idx] & TAINT) ? 1 : 0;
+    if (hops) hops[o] = reached ? B.H[idx] & HMASK : 0u;
+    if (tie) tie[o] = (reached && (B.H[idx] & TAINT)) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- host side
@@ -2368,6 +2377,7 @@ struct shadowtopo_engine {
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
+    int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
@@ -2431,6 +2441,17 @@ void free_batches(shadowtopo_engine* eng) {
     eng->nb_cap = 0;
 }
 
+bool state_bdu(const shadowtopo_engine* eng) {
+    return eng->dense || eng->opt_csr_variant != SHADOWTOPO_CSR_FULL;
+}
+bool state_d32(const shadowtopo_engine* eng) {
+    return eng->dense || eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED;
+}
+// bytes per (vertex, source) of the batch pools
+double state_bytes(const shadowtopo_engine* eng) {
+    return 24.0 + (state_bdu(eng) ? 8.0 : 0.0) + (state_d32(eng) ? 4.0 : 0.0);
+}
+
 int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
     if (eng->nb_cap >= nb) return SHADOWTOPO_OK;
     free_batches(eng);
@@ -2448,10 +2469,11 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.mask, sizeof(unsigned long long) * nb)))
         return rc;
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double))) ||
-        (rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb)))
-        return rc;
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))) return rc;
+    // BDU (the lexicographic key) only for the kernels that fold into a recorded state, D32
+    // only for the f32-filtered ones: the FULL CSR rounds keep 24 bytes per (vertex, source)
+    if (state_bdu(eng) && (rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double)))) return rc;
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.chm, sizeof(unsigned long long) * 2 * eng->Vp * nb))) return rc;
+    if (state_d32(eng) && (rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))) return rc;
     eng->h_srcv.assign((size_t)KL * nb, -1);
     eng->h_row.assign((size_t)KL * nb, -1);
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
@@ -2491,12 +2513,12 @@ int ensure_replay(shadowtopo_engine* eng) {
 int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
-    const double per_batch = (double)eng->Vp * KL * 36.0 + 18.0 * eng->Vp + (eng->dense ? 0.0 : 36.0 * eng->Vp);
+    const double per_batch = (double)eng->Vp * KL * state_bytes(eng) + 18.0 * eng->Vp + (eng->dense ? 0.0 : 36.0 * eng->Vp);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
     // engines sharing one device (SHADOWTOPO_DEVICES listing it twice) split the budget
-    const double budget = std::max(24.0e9, 0.4 * ((double)free_b + held)) * eng->opt_hbm_share / 1000.0;
+    const double budget = std::max(24.0e9, 0.55 * ((double)free_b + held)) * eng->opt_hbm_share / 1000.0;
     const double cap = eng->dense ? 16.0 : 256.0;
     const int32_t nb = (int32_t)std::max(1.0, std::min(cap, std::floor(budget / per_batch)));
     return std::min(nb, need);
@@ -2576,7 +2598,9 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     } else {
         const size_t total = (size_t)eng->Vp * KL;
         int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
-        hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp);
+        const int32_t tree = eng->dense || eng->opt_csr_variant == SHADOWTOPO_CSR_DELTA ||
+                             eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED;
+        hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp, tree);
         if (eng->pools.cm) HIP_TRY(hipMemsetAsync(eng->pools.cm, 0, sizeof(CMask) * (size_t)eng->Vp * nbg, s));
         hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools, eng->dense ? 0 : 1);
         HIP_TRY(hipGetLastError());
@@ -2628,7 +2652,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             if (wl_total == 0) break;  // nothing active: converged
         }
         // worklist only where it pays: a mostly-active round runs the plain grid
-        const bool round_wl = use_wl && (masked || wl_total * 2 < (int64_t)nbg * V);
+        const bool round_wl = use_wl && (masked || eng->opt_worklist == 2 || wl_total * 2 < (int64_t)nbg * V);
         if (round_wl)
             HIP_TRY(hipMemcpyAsync(eng->d_wlpre, eng->h_wlpre, sizeof(int64_t) * (nbg + 1), hipMemcpyHostToDevice, s));
         int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
@@ -2733,6 +2757,12 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     eng->st.delta_ms += ms;
                 }
             }
+        }
+        if (eng->trace_rounds) {
+            float ms = 0;
+            if (eng->opt_timing) (void)hipEventElapsedTime(&ms, eng->ev0, eng->ev1);
+            fprintf(stderr, "[shadowtopo] round %lld batches %d items %lld%s %.3f ms\n", (long long)round, nbg,
+                    (long long)(round_wl ? wl_total : (int64_t)nbg * V), round_wl ? " (worklist)" : "", ms);
         }
         int64_t changed = 0;
         for (int32_t b = 0; b < nbg; ++b) {
@@ -3293,6 +3323,10 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         shadowtopo_destroy(eng);
         return fail(SHADOWTOPO_EDEVICE, "stream/event create failed");
     }
+    {
+        const char* tr = getenv("SHADOWTOPO_TRACE_ROUNDS");
+        eng->trace_rounds = tr && tr[0] == '1';
+    }
     eng->st.n_vertices = V;
     eng->st.n_edges = n_edges;
     eng->st.n_arcs = eng->n_arcs;
@@ -3399,6 +3433,12 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL && value != SHADOWTOPO_CSR_FILTERED &&
                 value != SHADOWTOPO_CSR_MASKED)
                 return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
+            if (eng->nb_cap > 0 && eng->opt_csr_variant != (int32_t)value) {
+                // the pools' layout depends on the variant (state_bdu / state_d32)
+                (void)hipSetDevice(eng->device);
+                if (eng->own_stream) (void)hipStreamSynchronize(eng->own_stream);
+                free_batches(eng);
+            }
             eng->opt_csr_variant = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SOURCE_ORDER:
@@ -3414,7 +3454,7 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_dense_seed = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_WORKLIST:
-            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "worklist must be 0 or 1");
+            if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "worklist must be 0, 1 or 2");
             eng->opt_worklist = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_HBM_SHARE:
