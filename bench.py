@@ -88,7 +88,7 @@ def sparse_step_compulsory(V, n_arcs, sources):
     return nb * (n_arcs * 64 * 8 + (V + 1) * 8 + n_arcs * 12 + V * 64 * STATE_BYTES)
 
 
-VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions/s: 1024 SIMDs, one per 4 cycles at 2.4 GHz
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMD-32s, one wave64 instruction per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md)
 
 
 def load_counters(key):
@@ -297,7 +297,7 @@ def main():
         roofline["valu"] = {"unit": "wave64 VALU instructions/s", "achieved": ach, "peak": VALU_PEAK,
                             "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
                             "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
-                                    "waves / SQ_WAVES; peak = one VALU issue per 4 cycles per SIMD at 2.4 GHz"}
+                                    "waves / SQ_WAVES; peak = one wave64 VALU issue per 2 cycles per SIMD-32 at 2.4 GHz"}
     if not st["dense"] and st["wl_launches"] and args.csr_variant == 1:
         roofline["worklist_kernel"] = {"kernel": "k_relax_wl", "avg_launch_ms": st["wl_ms"] / st["wl_launches"],
                                        "launches_per_step": st["wl_launches"] / args.steps}

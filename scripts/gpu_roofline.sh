@@ -2,14 +2,15 @@
 # One config's measurement on the GPU box: kernel-trace stats + three separate PMC passes
 # (FETCH_SIZE, WRITE_SIZE, SQ) over the SAME bench command, summarised into
 # profiles/roofline_counters.json (key CFG@SCALE@1), then the bench line that reads them.
-# usage: scripts/gpu_roofline.sh TAG CFG SCALE KERNEL_SUBSTR ["extra bench args"]
+# usage: scripts/gpu_roofline.sh TAG CFG SCALE KERNEL_RE ["extra bench args"]
+# (KERNEL_RE: a Python regex over rocprof kernel names, e.g. "k_relax_dense_f<8, 2, 1, true>" or "k_relax\(|k_relax_wl\(")
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=$1
 CFG=${2:-C2}
 SCALE=${3:-1.0}
-KERNEL=${4:-k_relax_dense_f<}
+KERNEL=${4:-k_relax_dense_f<8, 2, 1, true>}
 EXTRA=${5:-}
 B="bench.py --config $CFG --scale $SCALE --steps 3 --warmup 1 --no-cpu-baseline --no-host-rate $EXTRA"
 O=gpurun_out/$TAG

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch counters of the bench's dominant kernel -> profiles/roofline_counters.json
+"""Per-launch counters of the bench's dominant relax kernel(s) -> profiles/roofline_counters.json
 (read by bench.py as roofline.traffic and roofline.valu).
 
 Inputs are three separate rocprofv3 --pmc passes over the SAME bench command
@@ -9,22 +9,25 @@ SQ_WAVES, GRBM_GUI_ACTIVE).  Corrections, MI355X_MICROARCH.md (HBM section):
     coalesced reads, so it is doubled; WRITE_SIZE is taken as is.
   * SQ counters do not cover every wave of a dispatch: the launch's true wave count
     (Grid_Size / 64) over SQ_WAVES scales SQ_INSTS_VALU up to the whole dispatch.
-Only dispatches of the named kernel with the bench's launch shape are used (the largest
-grid: the engine's first computation also runs small one-batch landmark launches of the
-same kernel), averaged per launch.
+Which dispatches: those of the kernels matching KERNEL_RE, in dispatch order, the last
+(warmup + steps) x launches_per_step of them -- exactly the bench's warmup and timed steps
+(the engine's first computation also runs one-batch landmark rounds of the same kernels,
+earlier) -- summed and divided by their count: bytes per launch averaged over the step's
+launches, the unit of bench.py's roofline.
 
-usage: roofline_counters.py KEY KERNEL_SUBSTR BENCH_JSON FETCH_DIR WRITE_DIR SQ_DIR
+usage: roofline_counters.py KEY KERNEL_RE BENCH_JSON FETCH_DIR WRITE_DIR SQ_DIR
 """
 import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 
-def per_dispatch(d, kernel_sub):
-    """{(file, dispatch): {counter: value, '_grid': threads}}"""
+def dispatches(d, kre):
+    """[(dispatch_id, {counter: value, '_grid', '_ns'})] of matching kernels, in order"""
     out = defaultdict(lambda: defaultdict(float))
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -32,43 +35,36 @@ def per_dispatch(d, kernel_sub):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel_sub not in row.get("Kernel_Name", ""):
+                if not re.search(kre, row.get("Kernel_Name", "")):
                     continue
-                k = (f, row["Dispatch_Id"])
+                k = int(row["Dispatch_Id"])
                 out[k][row["Counter_Name"]] += float(row["Counter_Value"])
                 out[k]["_grid"] = float(row["Grid_Size"])
                 out[k]["_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
-    if out:  # the bench's own launches: the largest grid
-        big = max(v["_grid"] for v in out.values())
-        out = {k: v for k, v in out.items() if v["_grid"] == big}
-    return out
-
-
-def mean(xs):
-    xs = list(xs)
-    return sum(xs) / len(xs) if xs else None
+    return [out[k] for k in sorted(out)]
 
 
 def main():
-    key, kernel, bench_json, fdir, wdir, sdir = sys.argv[1:7]
+    key, kre, bench_json, fdir, wdir, sdir = sys.argv[1:7]
     bench = json.loads(open(bench_json).read().strip().splitlines()[-1])
-    f = per_dispatch(fdir, kernel)
-    w = per_dispatch(wdir, kernel)
-    s = per_dispatch(sdir, kernel)
-    if not f or not w or not s:
-        raise SystemExit(f"no dispatches of {kernel}")
-    fetch = mean(v["FETCH_SIZE"] * 1024 * 2 for v in f.values())
-    write = mean(v["WRITE_SIZE"] * 1024 for v in w.values())
-    valu = mean(v["SQ_INSTS_VALU"] * (v["_grid"] / 64.0) / v["SQ_WAVES"] for v in s.values() if v.get("SQ_WAVES"))
-    clk = mean(v["GRBM_GUI_ACTIVE"] / 8.0 / v["_ns"] for v in s.values() if v.get("_ns"))  # GHz
     rf = bench["roofline"]
+    n = int(round((bench["warmup"] + bench["steps"]) * rf["launches_per_step"]))
+    f, w, s = (dispatches(d, kre)[-n:] for d in (fdir, wdir, sdir))
+    if min(len(f), len(w), len(s)) < n:
+        raise SystemExit(f"expected {n} dispatches matching {kre}, found {len(f)}/{len(w)}/{len(s)}")
+    fetch = sum(v["FETCH_SIZE"] for v in f) * 1024 * 2 / n
+    write = sum(v["WRITE_SIZE"] for v in w) * 1024 / n
+    valu = sum(v["SQ_INSTS_VALU"] * (v["_grid"] / 64.0) / v["SQ_WAVES"] for v in s if v.get("SQ_WAVES")) / n
+    ns = sum(v["_ns"] for v in s)
+    clk = sum(v["GRBM_GUI_ACTIVE"] for v in s) / 8.0 / ns if ns else None  # GHz
     rec = {"kernel": rf["kernel"], "batches_per_launch": rf["batches_per_launch"],
            "hbm_bytes_per_launch": fetch + write, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "valu_insts_per_launch": valu, "effective_clock_ghz_profiled": clk,
-           "dispatches": [len(f), len(w), len(s)],
-           "profiled_avg_launch_ms": mean(v["_ns"] for v in f.values()) / 1e6,
-           "source": f"rocprofv3 --pmc passes over `{bench.get('_cmd', 'bench.py')}`: FETCH_SIZE x1024 x2, "
-                     f"WRITE_SIZE x1024, SQ_INSTS_VALU x (Grid_Size/64)/SQ_WAVES; kernel filter '{kernel}'"}
+           "dispatches": n,
+           "profiled_avg_launch_ms": sum(v["_ns"] for v in f) / n / 1e6,
+           "source": f"rocprofv3 --pmc passes over the bench command of {os.path.basename(bench_json)}: "
+                     f"FETCH_SIZE x1024 x2, WRITE_SIZE x1024, SQ_INSTS_VALU x (Grid_Size/64)/SQ_WAVES; the last "
+                     f"{n} dispatches of kernels matching '{kre}'"}
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "roofline_counters.json")
     db = json.load(open(p)) if os.path.exists(p) else {}
     db[key] = rec
