@@ -153,6 +153,7 @@ typedef struct shadowtopo_stats {
     int64_t relax_batches;   /* sparse: batches in flight, summed over relax launches */
     int64_t wl_launches;     /* sparse: relax launches over frontier worklists (k_relax_wl), included above */
     double wl_ms;            /* OPT_TIMING: their HIP-event time, included in relax_ms */
+    int64_t sparse_deltas;   /* dense: delta launches that walked live-chunk lists only */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -1715,6 +1715,42 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta(const double* __r
     }
 }
 
+// Sparse delta rounds: per batch, the 64-row chunks holding a row whose change mask (the
+// previous round's) is non-zero, in ascending order -- the delta round then walks only
+// those chunks (a round after a round that changed few pairs is nearly free instead of
+// a full walk of every chunk's slab and barriers).  One block per batch.
+__global__ __launch_bounds__(256) void k_live_chunks(Pools pools, int32_t V, int32_t nvc, int32_t parity,
+                                                     const int32_t* __restrict__ cnt_prev, int32_t* __restrict__ live,
+                                                     int32_t* __restrict__ nlive) {
+    __shared__ int32_t sbase;
+    const int32_t b = blockIdx.x;
+    const BatchDev B = batch_view(pools, b);
+    const unsigned long long* chp = B.chm(parity ^ 1);
+    if (threadIdx.x == 0) sbase = 0;
+    __syncthreads();
+    for (int32_t c0 = 0; c0 < nvc; c0 += 256) {
+        const int32_t c = c0 + threadIdx.x;
+        bool any = false;
+        if (c < nvc && cnt_prev[b] != 0)
+            for (int r = 0; r < KL && c * KL + r < V; ++r) any |= chp[c * KL + r] != 0ull;
+        // ascending order: wave ballots, waves in turn
+        const unsigned long long bal = __ballot(any);
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        __shared__ int32_t swc[4];
+        if (lane == 0) swc[wave] = __popcll(bal);
+        __syncthreads();
+        int32_t off = sbase;
+        for (int k = 0; k < wave; ++k) off += swc[k];
+        if (any)
+            live[(size_t)b * nvc + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) sbase += swc[0] + swc[1] + swc[2] + swc[3];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) nlive[b] = sbase;
+}
+
 // Staged f32 dense delta round, lane = candidate pair (the round semantics of
 // k_relax_dense_delta).  The block (one batch, 64 destinations, 4 waves of 16 sources) walks
 // the rows in 64-row chunks; each chunk's W32 slab W32[u0..u0+63][v0..v0+63] is loaded once,
@@ -1737,7 +1773,9 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
                                                                  const double* __restrict__ in_r, Pools pools,
                                                                  int32_t V, int32_t nb, int32_t nvc, int32_t parity,
                                                                  int32_t thresh, const int32_t* __restrict__ cnt_prev,
-                                                                 int32_t* __restrict__ cnt) {
+                                                                 int32_t* __restrict__ cnt,
+                                                                 const int32_t* __restrict__ live,
+                                                                 const int32_t* __restrict__ nlive) {
     constexpr int SW = KL / DW;  // sources per wave
     constexpr int PF = KL * KL / 4 / (64 * DW);  // float4 of one W32 slab per thread
     __shared__ __attribute__((aligned(16))) float sT[KL * SWS];  // [s][v] thresholds
@@ -1840,12 +1878,22 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         }
     };
 
-    fetch(0);
-    stash();
-    unsigned long long mnext = chp[lane];  // rows < Vp exist; rows >= V are masked at use
+    // the 64-row chunks to walk: every chunk, or (sparse rounds) the batch's chunks that
+    // hold a changed row, in ascending order (k_live_chunks)
+    const int32_t nl = live ? nlive[b] : (V + KL - 1) / KL;
+    auto chunk_u0 = [&](int32_t i) { return (live ? live[(size_t)b * nvc + i] : i) * KL; };
+    unsigned long long mnext = 0;
+    if (nl > 0) {
+        const int32_t f0 = chunk_u0(0);
+        fetch(f0);
+        stash();
+        mnext = chp[f0 + lane];  // rows < Vp exist; rows >= V are masked at use
+    }
     __syncthreads();
-    for (int32_t u0 = 0; u0 < V; u0 += KL) {
-        const bool more = u0 + KL < V;
+    for (int32_t ci = 0; ci < nl; ++ci) {
+        const int32_t u0 = chunk_u0(ci);
+        const bool more = ci + 1 < nl;
+        const int32_t un = more ? chunk_u0(ci + 1) : 0;
         const unsigned long long m = (u0 + lane < V) ? (mnext & srange) : 0ull;
         // exclusive prefix sum of the per-row pair counts (<= 16, five bits) from ballots
         // and mbcnt: no cross-lane LDS round trips
@@ -1860,9 +1908,9 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         // the next chunk's change masks and W32 slab are in flight while this chunk drains
         // (issued after this chunk's masks are consumed, waited for at the stash);
         // u0 + KL + 63 < Vp when `more`
-        pma = chp + (more ? u0 + KL : 0) + lane;
+        pma = chp + un + lane;
         mnext = *pma;
-        if (more) fetch(u0 + KL);
+        if (more) fetch(un);
         if (tot) {
             unsigned long long mm = m;
             while (mm) {
@@ -2378,6 +2426,10 @@ struct shadowtopo_engine {
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
+    int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
+    int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
+    int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
+    int32_t* d_nlive = nullptr;        // [nb_cap]
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
@@ -2436,6 +2488,8 @@ void free_batches(shadowtopo_engine* eng) {
     eng->d_wl = nullptr;
     eng->d_wlcnt = nullptr;
     eng->d_wlpre = nullptr;
+    eng->d_live = nullptr;
+    eng->d_nlive = nullptr;
     eng->h_srcv.clear();
     eng->h_row.clear();
     eng->nb_cap = 0;
@@ -2690,10 +2744,37 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     hipLaunchKernelGGL(k_relax_dense_delta, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
                                        eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par,
                                        thresh, cnt_prev, cnt_cur);
-                else
+                else {
+                    // a round after one that changed few pairs walks only the chunks holding
+                    // a changed row (k_live_chunks); after a full sweep nearly every chunk does
+                    int64_t dch = 0, dpairs = 0;
+                    for (int32_t b = 0; b < nbg; ++b)
+                        if (eng->h_cnt[b] > 0 && eng->h_cnt[b] <= thresh) {
+                            dch += eng->h_cnt[b];
+                            dpairs += (int64_t)V * KL;
+                        }
+                    const bool sparse = eng->opt_delta_live == 1 ||
+                                        (eng->opt_delta_live == 2 && dch * eng->opt_delta_live_div <= dpairs);
+                    const int32_t* live = nullptr;
+                    const int32_t* nlive = nullptr;
+                    if (sparse) {
+                        if (!eng->d_live) {
+                            int rc2;
+                            if ((rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_live,
+                                                 sizeof(int32_t) * (size_t)eng->nb_cap * nvc)) ||
+                                (rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_nlive, sizeof(int32_t) * eng->nb_cap)))
+                                return rc2;
+                        }
+                        hipLaunchKernelGGL(k_live_chunks, dim3(nbg), dim3(256), 0, s, eng->pools, V, nvc, par, cnt_prev,
+                                           eng->d_live, eng->d_nlive);
+                        live = eng->d_live;
+                        nlive = eng->d_nlive;
+                        eng->st.sparse_deltas++;
+                    }
                     hipLaunchKernelGGL(k_relax_dense_delta_s, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
                                        eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
-                                       nbg, nvc, par, thresh, cnt_prev, cnt_cur);
+                                       nbg, nvc, par, thresh, cnt_prev, cnt_cur, live, nlive);
+                }
                 eng->st.delta_sweeps++;
             }
         } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED) {
@@ -2758,16 +2839,18 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 }
             }
         }
-        if (eng->trace_rounds) {
-            float ms = 0;
-            if (eng->opt_timing) (void)hipEventElapsedTime(&ms, eng->ev0, eng->ev1);
-            fprintf(stderr, "[shadowtopo] round %lld batches %d items %lld%s %.3f ms\n", (long long)round, nbg,
-                    (long long)(round_wl ? wl_total : (int64_t)nbg * V), round_wl ? " (worklist)" : "", ms);
-        }
         int64_t changed = 0;
         for (int32_t b = 0; b < nbg; ++b) {
             changed += eng->h_cnt[b];
             if (round_full && full_b[b]) eng->st.full_changes += eng->h_cnt[b];
+        }
+        if (eng->trace_rounds) {
+            float ms = 0;
+            if (eng->opt_timing) (void)hipEventElapsedTime(&ms, eng->ev0, eng->ev1);
+            fprintf(stderr, "[shadowtopo] round %lld batches %d items %lld%s%s%s changed %lld %.3f ms\n",
+                    (long long)round, nbg, (long long)(round_wl ? wl_total : (int64_t)nbg * V),
+                    round_wl ? " (worklist)" : "", round_full ? " full" : "", round_delta ? " delta" : "",
+                    (long long)changed, ms);
         }
         if (eng->dense && eng->opt_profile) eng->st.changes += changed;  // changed (vertex, source) pairs
         if (changed == 0) break;
@@ -3326,6 +3409,10 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     {
         const char* tr = getenv("SHADOWTOPO_TRACE_ROUNDS");
         eng->trace_rounds = tr && tr[0] == '1';
+        const char* dl = getenv("SHADOWTOPO_DELTA_LIVE");  // A/B knob: 0, 1 or 2 (default)
+        if (dl && dl[0] >= '0' && dl[0] <= '2') eng->opt_delta_live = dl[0] - '0';
+        const char* dd = getenv("SHADOWTOPO_DELTA_LIVE_DIV");
+        if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
     }
     eng->st.n_vertices = V;
     eng->st.n_edges = n_edges;

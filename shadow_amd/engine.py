@@ -73,7 +73,7 @@ class Stats(ctypes.Structure):
         ("full_sweeps", ctypes.c_int64), ("delta_sweeps", ctypes.c_int64),
         ("full_ms", ctypes.c_double), ("delta_ms", ctypes.c_double),
         ("full_batches", ctypes.c_int64), ("full_changes", ctypes.c_int64), ("relax_batches", ctypes.c_int64),
-        ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double),
+        ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double), ("sparse_deltas", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -367,3 +367,25 @@ def test_row_exchange_with_engine_device_rows():
     assert_bitexact("latency", lat, lat_o)
     assert_bitexact("reliability", rel, rel_o)
     assert_bitexact("hops", hops.astype(np.uint32), hops_o)
+
+
+@pytest.mark.parametrize("live", ["0", "1"])
+@pytest.mark.parametrize("case", ["ties", "geometric", "directed", "vloss_prefer"])
+def test_dense_delta_live_chunks(case, live, monkeypatch):
+    """Delta rounds that walk only the 64-row chunks holding a changed row (k_live_chunks)
+    against the full walk: the same matrices, bit for bit, and the oracle's.  Forced on for
+    every delta round (SHADOWTOPO_DELTA_LIVE=1) and off (=0)."""
+    monkeypatch.setenv("SHADOWTOPO_DELTA_LIVE", live)
+    if case == "ties":
+        g = synth.integer_grid(rows=11, cols=12, seed=6)
+    elif case == "directed":
+        g = synth.random_sparse(V=260, avg_deg=5, seed=9, directed=True)
+    elif case == "vloss_prefer":
+        rng = np.random.default_rng(5)
+        g = synth.random_sparse(V=170, avg_deg=8, seed=7, vloss=rng.uniform(0, 0.1, 170))
+        g.prefer_direct = True
+    else:
+        g = synth.geometric_complete_ish(V=900, A=200)
+    st = compare(g, layout="dense", delta_permille=1000)
+    assert st["dense"] == 1 and st["delta_sweeps"] > 0
+    assert (st["sparse_deltas"] > 0) == (live == "1")
