@@ -1218,16 +1218,25 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
     constexpr int DQ = SRS * KL / 4 / 256;       // float4 of one batch's D32 chunk per thread
     constexpr int WQT = (SRS * WQ + 255) / 256;  // float4 of W32 per thread
     f4 pd[TB][DQ], pw[WQT];
-    // PR: permuted row ids of the chunk being fetched (loaded one fetch ahead), and the
-    // chunk's skip bounds (md: min D32 per lane and batch, mw: min W32 of the wave's tile)
-    int32_t prow[DQ];
+    // PR: the chunk's skip bounds (md: min D32 per lane and batch, mw: min W32 of the
+    // wave's tile columns)
     float mdn[TB], mdc[TB], mwn[TDT], mwc[TDT];
     const int32_t ncol = (V + BW - 1) / BW * BW;  // columns per chunk row of minW
-    if (PR) {
+    // PR: chunks in the order vt, vt+1, .., wrapping: the block's own tile (its destinations'
+    // nearest rows) first, which gives unreached and arc-less (t, s) pairs a tight threshold
+    // before the far chunks are tested
+    const int32_t c0 = PR ? (int32_t)((int64_t)vt * BW / SRS % nchunks) : 0;  // the chunk holding the tile
+    auto chunk_of = [&](int32_t j) { return PR ? (c0 + j) % nchunks : j; };
+    // fetch the chunk of order index j into registers (rows in the locality order: PR reads
+    // each row's vertex from perm, an L2-resident 40 KB table)
+    auto fetch = [&](int32_t j) {
+        const int32_t c = chunk_of(j);
+        const int32_t u0 = c * SRS;
+        int32_t prow[DQ];
+        if (PR) {
 #pragma unroll
-        for (int i = 0; i < DQ; ++i) prow[i] = perm[(int32_t)((int64_t)vt * BW / SRS % nchunks) * SRS + (threadIdx.x + i * 256) / (KL / 4)];
-    }
-    auto fetch = [&](int32_t u0) {
+            for (int i = 0; i < DQ; ++i) prow[i] = perm[u0 + (threadIdx.x + i * 256) / (KL / 4)];
+        }
 #pragma unroll
         for (int k = 0; k < TB; ++k)
 #pragma unroll
@@ -1239,17 +1248,11 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
                     pd[k][i] = *(gf4*)(B[k].D32 + (size_t)u0 * KL + (size_t)e * 4);
             }
         if (PR) {
-            const int32_t c = u0 / SRS;
 #pragma unroll
             for (int k = 0; k < TB; ++k)
                 mdn[k] = minD[((size_t)(live[k] ? b0 + k : first) * nchunks + c) * KL + lane];
 #pragma unroll
             for (int t = 0; t < TDT; ++t) mwn[t] = minW[(size_t)c * ncol + v0 + t];
-#pragma unroll
-            for (int i = 0; i < DQ; ++i) {
-                const int32_t r = (c + 1 == nchunks ? 0 : c + 1) * SRS + (threadIdx.x + i * 256) / (KL / 4);
-                prow[i] = perm[r];
-            }
         }
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
@@ -1279,20 +1282,96 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
             for (int t = 0; t < TDT; ++t) mwc[t] = mwn[t];
         }
     };
-    // PR: chunks in the order vt, vt+1, .., wrapping: the block's own tile (its destinations'
-    // nearest rows) first, which gives unreached and arc-less (t, s) pairs a tight threshold
-    // before the far chunks are tested
-    const int32_t c0 = PR ? (int32_t)((int64_t)vt * BW / SRS % nchunks) : 0;  // the chunk holding the tile
-    fetch(c0 * SRS);
-    stash(0);
-    advance();
+    // PR: block-wide chunk skipping.  Most chunk iterations of a pruned sweep are dead for
+    // all four waves of a block at once (C2: 71 %), and a dead iteration still cost a load
+    // round trip and a barrier.  So the block decides, for a window of chunks at a time and
+    // with its current thresholds, which chunks any of its waves can pass (the per-wave chunk
+    // bound below, evaluated for the window: lane = source, one minD load per chunk), ORs the
+    // four waves' masks in LDS and loads, stages and visits only those.  Thresholds only
+    // tighten during the sweep, so a chunk dead at the window's evaluation is dead for the
+    // rest of it: the skip is exact (the per-wave test inside a live chunk still uses the
+    // newest thresholds).  Window 0 is the block's own chunk alone (it tightens the
+    // thresholds most), then windows of 64.  A dead chunk's hit log entries are zeroed at
+    // the evaluation.
+    __shared__ unsigned long long sWin[2];
+    if (PR && threadIdx.x == 0) sWin[0] = sWin[1] = 0ull;
     __syncthreads();
-    for (int32_t it = 0; it < nchunks; ++it) {
-        const int32_t c = PR ? (c0 + it) % nchunks : it;
+    int32_t cur_win = -1;
+    unsigned long long cur_live = 0ull;
+    auto win_of = [&](int32_t j) { return j == 0 ? 0 : 1 + (j - 1) / 64; };
+    auto win_base = [&](int32_t wi) { return wi == 0 ? 0 : 1 + (wi - 1) * 64; };
+    constexpr int WG = 4;  // chunks whose bounds are in flight at once in a window evaluation
+    auto eval_window = [&](int32_t wi) -> unsigned long long {
+        const int32_t base = win_base(wi);
+        const int32_t nw = wi == 0 ? 1 : (nchunks - base < 64 ? nchunks - base : 64);
+        unsigned long long wm = 0ull;
+        for (int32_t j0 = 0; j0 < nw; j0 += WG) {
+            float md[TB][WG], mw8[WG][TDT];
+#pragma unroll
+            for (int jj = 0; jj < WG; ++jj) {
+                const int32_t c = chunk_of(base + (j0 + jj < nw ? j0 + jj : 0));
+#pragma unroll
+                for (int k = 0; k < TB; ++k)
+                    md[k][jj] = minD[((size_t)(live[k] ? b0 + k : first) * nchunks + c) * KL + lane];
+#pragma unroll
+                for (int t = 0; t < TDT; ++t) mw8[jj][t] = minW[(size_t)c * ncol + v0 + t];
+            }
+#pragma unroll
+            for (int jj = 0; jj < WG; ++jj) {
+                bool p = false;
+#pragma unroll
+                for (int k = 0; k < TB; ++k) {
+                    float tm = thr[k][0] - mw8[jj][0];
+#pragma unroll
+                    for (int t = 1; t < TDT; ++t) tm = fmaxf(tm, thr[k][t] - mw8[jj][t]);
+                    p |= md[k][jj] <= tm;
+                }
+                if (__ballot(p) && j0 + jj < nw) wm |= 1ull << (j0 + jj);
+            }
+        }
+        if (threadIdx.x == 0) sWin[(wi + 1) & 1] = 0ull;  // the next window's slot: nobody ORs into it before this barrier
+        if (lane == 0 && wm) atomicOr(&sWin[wi & 1], wm);
+        __syncthreads();
+        const unsigned long long lv =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sWin[wi & 1] >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sWin[wi & 1]);
+        if (lane < nw && !((lv >> lane) & 1ull)) {
+            const int32_t c = chunk_of(base + lane);
+#pragma unroll
+            for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + c] = 0u;
+        }
+        return lv;
+    };
+    // order index of the next chunk to visit at or after `from`, -1 past the end
+    auto next_live = [&](int32_t from) -> int32_t {
+        if (!PR) return from < nchunks ? from : -1;
+        while (from < nchunks) {
+            const int32_t wi = win_of(from);
+            if (wi != cur_win) {
+                cur_win = wi;
+                cur_live = eval_window(wi);
+            }
+            const unsigned long long m = cur_live & (~0ull << (from - win_base(wi)));
+            if (m) return win_base(wi) + __builtin_ctzll(m);
+            from = win_base(wi + 1);
+        }
+        return -1;
+    };
+    int32_t itc = next_live(0);
+    if (itc >= 0) {
+        fetch(itc);
+        stash(0);
+        advance();
+    }
+    __syncthreads();
+    int bufc = 0;
+    while (itc >= 0) {
+        const int32_t c = chunk_of(itc);
         const int32_t u0 = c * SRS;
-        const int cur = it & 1;
-        const bool more = it + 1 < nchunks;
-        if (more) fetch((c + 1 == nchunks ? 0 : c + 1) * SRS);
+        const int cur = bufc;
+        const int32_t itn = next_live(itc + 1);  // block-uniform (a window evaluation holds a barrier)
+        const bool more = itn >= 0;
+        if (more) fetch(itn);
         bool run = true;
         if (PR) {
             bool p = false;
@@ -1368,6 +1447,8 @@ __global__ __launch_bounds__(256) void k_relax_dense_f(const float* __restrict__
             advance();
         }
         __syncthreads();
+        bufc ^= 1;
+        itc = itn;
     }
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
     // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
