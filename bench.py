@@ -136,6 +136,98 @@ def cpu_baseline(g, n_sources, budget_s=20.0, all_cores=16):
     return out
 
 
+def roofline_of(st, g, config, scale, world, rows, steps, csr_variant=1, dense_variant=0):
+    """Roofline of the dominant kernel, timed with HIP events on the engine's stream around
+    every launch: the f32 dense full sweep (k_relax_dense_f) on complete-ish graphs, the CSR
+    relax rounds (k_relax, with the k_relax_wl worklist rounds) otherwise.  achieved = that
+    kernel's compulsory bytes per launch / its average launch time; traffic =
+    this round's rocprofv3 FETCH/WRITE passes over the same launch shape (or None)."""
+    if st["dense"]:
+        kname = "k_relax_dense" if dense_variant == 1 else "k_relax_dense_f"
+        launches, kms = max(1, st["full_sweeps"]), st["full_ms"]
+        Vp = -(-g.n // 64) * 64
+        bytes_per_launch = dense_sweep_compulsory(Vp, st)
+        batches_per_launch = st["full_batches"] / launches
+    else:
+        # every relax round of the step (grid and worklist launches alike): achieved = the
+        # step's compulsory bytes / the relax kernels' time in the step
+        kname = {0: "k_relax_delta", 1: "k_relax", 2: "k_relax_st", 3: "k_relax_cm"}[csr_variant]
+        launches, kms = max(1, st["relax_launches"]), st["relax_ms"]
+        bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * steps / launches
+        batches_per_launch = st["relax_batches"] / launches
+    avg_launch_s = kms / launches / 1e3
+    achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
+    ckey = f"{config}@{scale}@{world}"
+    cnt = load_counters(ckey)
+    if cnt and (cnt.get("kernel") != kname or abs(cnt.get("batches_per_launch", -1) - batches_per_launch) > 0.5):
+        log(f"counter record {ckey} is for another launch shape ({cnt.get('kernel')}, "
+            f"{cnt.get('batches_per_launch')} batches); not used")
+        cnt = None
+    traffic = cnt["hbm_bytes_per_launch"] if cnt else None
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "kernel": kname, "avg_launch_ms": avg_launch_s * 1e3,
+                "launches_per_step": launches / steps, "batches_per_launch": batches_per_launch,
+                "compulsory_bytes_per_launch": bytes_per_launch,
+                "traffic_over_compulsory": (traffic / bytes_per_launch) if traffic else None,
+                "measured_hbm_gbs": (traffic / avg_launch_s / 1e9) if (traffic and avg_launch_s > 0) else None,
+                "counters": (cnt.get("source") if cnt else None)}
+    if cnt and cnt.get("valu_insts_per_launch") and avg_launch_s > 0:
+        ach = cnt["valu_insts_per_launch"] / avg_launch_s
+        roofline["valu"] = {"unit": "wave64 VALU instructions/s", "achieved": ach, "peak": VALU_PEAK,
+                            "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
+                            "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
+                                    "waves / SQ_WAVES; peak = one wave64 VALU issue per 2 cycles per SIMD-32 at 2.4 GHz"}
+    if not st["dense"] and st["wl_launches"] and csr_variant == 1:
+        roofline["worklist_kernel"] = {"kernel": "k_relax_wl", "avg_launch_ms": st["wl_ms"] / st["wl_launches"],
+                                       "launches_per_step": st["wl_launches"] / steps}
+    if st["dense"] and st["delta_sweeps"]:
+        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if dense_variant == 1 else "k_relax_dense_delta_s",
+                                    "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
+                                    "launches_per_step": st["delta_sweeps"] / steps}
+    return roofline
+
+
+def north_star_c4(device, steps=5, warmup=1):
+    """The north-star workload (BASELINE.json configs[3], SURVEY.md 8d C4: a 10^5-vertex
+    Barabasi-Albert graph, 10^4 attached hosts) on this one GPU, timed like the headline
+    (inputs resident, rows into HBM, synchronize around exactly `steps` matrix builds), so
+    the driver's own run carries it beside the configs[1] line."""
+    import torch
+    from shadow_amd import engine as E
+    g, _per, desc = build_workload("C4", 1, 1.0)
+    A = len(g.attached)
+    eng = E.Engine.from_synth(g, device=device.index or 0)
+    try:
+        eng.set_attached(g.attached)
+        eng.set_option(E.OPT_TIMING, 1)
+        lat = torch.empty((A, A), dtype=torch.float64, device=device)
+        rel = torch.empty((A, A), dtype=torch.float64, device=device)
+        hops = torch.empty((A, A), dtype=torch.int32, device=device)
+
+        def step():
+            stream = torch.cuda.current_stream(device).cuda_stream
+            eng.compute_rows_device(0, A, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
+
+        for _ in range(max(1, warmup)):
+            step()
+        torch.cuda.synchronize(device)
+        eng.reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(device)
+        elapsed = time.perf_counter() - t0
+        st = eng.stats()
+        return {"workload": desc, "n_vertices": g.n, "n_arcs": st["n_arcs"], "attached": A,
+                "steps": steps, "warmup": warmup, "matrix_build_ms": elapsed / steps * 1e3,
+                "value": A * steps / elapsed, "unit": "source-paths/s",
+                "rounds_per_step": st["rounds"] / steps,
+                "roofline": roofline_of(st, g, "C4", 1.0, 1, A, steps)}
+    finally:
+        eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,6 +238,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-rate", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
     ap.add_argument("--cpu-sources", type=int, default=12)
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the C4 north-star record the default (C2, 1 GPU) run adds to its line")
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
@@ -257,54 +351,9 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # roofline of the dominant kernel, timed with HIP events on the engine's stream around
-    # every launch: the f32 dense full sweep (k_relax_dense_f) on complete-ish graphs, the
-    # CSR relax round (k_relax) otherwise.  achieved = that kernel's compulsory bytes per
-    # launch / its average launch time.
-    if st["dense"]:
-        kname = "k_relax_dense" if args.dense_variant == 1 else "k_relax_dense_f"
-        launches, kms = max(1, st["full_sweeps"]), st["full_ms"]
-        Vp = -(-g.n // 64) * 64
-        bytes_per_launch = dense_sweep_compulsory(Vp, st)
-        batches_per_launch = st["full_batches"] / launches
-    else:
-        # the grid rounds (k_relax): the worklist rounds (k_relax_wl, sparse frontiers) are the
-        # minority of the time and are reported beside it
-        # every relax round of the step (grid and worklist launches alike): achieved = the
-        # step's compulsory bytes / the relax kernels' time in the step
-        kname = {0: "k_relax_delta", 1: "k_relax", 2: "k_relax_st", 3: "k_relax_cm"}[args.csr_variant]
-        launches, kms = max(1, st["relax_launches"]), st["relax_ms"]
-        bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * args.steps / launches
-        batches_per_launch = st["relax_batches"] / launches
-    avg_launch_s = kms / launches / 1e3
-    achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
-    ckey = f"{args.config}@{args.scale}@{world}"
-    cnt = load_counters(ckey)
-    if cnt and (cnt.get("kernel") != kname or abs(cnt.get("batches_per_launch", -1) - batches_per_launch) > 0.5):
-        log(f"counter record {ckey} is for another launch shape ({cnt.get('kernel')}, "
-            f"{cnt.get('batches_per_launch')} batches); not used")
-        cnt = None
-    traffic = cnt["hbm_bytes_per_launch"] if cnt else None
-    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "kernel": kname, "avg_launch_ms": avg_launch_s * 1e3,
-                "launches_per_step": launches / args.steps, "batches_per_launch": batches_per_launch,
-                "compulsory_bytes_per_launch": bytes_per_launch,
-                "traffic_over_compulsory": (traffic / bytes_per_launch) if traffic else None,
-                "measured_hbm_gbs": (traffic / avg_launch_s / 1e9) if (traffic and avg_launch_s > 0) else None,
-                "counters": (cnt.get("source") if cnt else None)}
-    if cnt and cnt.get("valu_insts_per_launch") and avg_launch_s > 0:
-        ach = cnt["valu_insts_per_launch"] / avg_launch_s
-        roofline["valu"] = {"unit": "wave64 VALU instructions/s", "achieved": ach, "peak": VALU_PEAK,
-                            "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
-                            "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
-                                    "waves / SQ_WAVES; peak = one wave64 VALU issue per 2 cycles per SIMD-32 at 2.4 GHz"}
-    if not st["dense"] and st["wl_launches"] and args.csr_variant == 1:
-        roofline["worklist_kernel"] = {"kernel": "k_relax_wl", "avg_launch_ms": st["wl_ms"] / st["wl_launches"],
-                                       "launches_per_step": st["wl_launches"] / args.steps}
-    if st["dense"] and st["delta_sweeps"]:
-        roofline["delta_kernel"] = {"kernel": "k_relax_dense_delta" if args.dense_variant == 1 else "k_relax_dense_delta_s",
-                                    "avg_launch_ms": st["delta_ms"] / st["delta_sweeps"],
-                                    "launches_per_step": st["delta_sweeps"] / args.steps}
+    # every launch
+    roofline = roofline_of(st, g, args.config, args.scale, world, rows, args.steps, args.csr_variant,
+                           args.dense_variant)
 
     # the drop-in boundary hands host buffers over (topology_hip.c: MEM_HOST); its
     # PCIe-inclusive rate, measured once outside the timed region (never `value`)
@@ -325,6 +374,15 @@ def main():
         eng.compute_rows_into(r0, r1, *outs)
         host_pageable_ms = (time.perf_counter() - h0) * 1e3
         del outs
+
+    north = None
+    if rank == 0 and world == 1 and args.config == "C2" and args.scale == 1.0 and not args.no_north_star:
+        eng.close()
+        eng = None
+        try:
+            north = north_star_c4(dev)
+        except Exception as e:  # report, never fake
+            north = {"error": str(e)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -353,6 +411,7 @@ def main():
                        "parallelism": f"sources sharded x{world}" + (f" + RCCL all-gather ({chunks} chunks, overlapped)" if world > 1 else "")},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "north_star": north,
             "engine": {"rounds_per_step": st["rounds"] / args.steps, "replayed_sources": st["replayed_sources"],
                        "relax_ms_per_step": st["relax_ms"] / args.steps,
                        "compose_ms_per_step": st["compose_ms"] / args.steps, "dense": st["dense"],
@@ -364,7 +423,8 @@ def main():
                        "host_buffers_source_paths_per_s": (rows / host_ms * 1e3) if host_ms else None},
         }
         print(json.dumps(out), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

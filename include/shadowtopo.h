@@ -154,6 +154,9 @@ typedef struct shadowtopo_stats {
     int64_t wl_launches;     /* sparse: relax launches over frontier worklists (k_relax_wl), included above */
     double wl_ms;            /* OPT_TIMING: their HIP-event time, included in relax_ms */
     int64_t sparse_deltas;   /* dense: delta launches that walked live-chunk lists only */
+    double self_ms;          /* host wall time of the self-path rule (k_self), once per attached set
+                                (the reference's selfPathTotalTime, topology.c:1608-1617) */
+    int64_t self_paths;      /* attached vertices the self-path rule ran for */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -28,9 +28,14 @@ typedef struct topology_hip_info {
     int32_t device;
     double min_path_latency;  /* value handed to worker_updateMinTimeJump */
     double compute_seconds;   /* wall time of the eager attached-pair computation */
-    int64_t compute_count;    /* sources computed ("shortest paths with dijkstra") */
+    int64_t compute_count;    /* source rows computed on the GPU */
     int32_t n_devices;        /* GPUs the attached-pair rows are sharded over */
     int32_t compute_failed;   /* 1 after a failed computation: queries fail without retrying it */
+    /* the reference's path cache, emulated over the eager matrix (topology_hip.c cache_resolve) */
+    int64_t dijkstra_runs;    /* _topology_computeSourcePaths calls the reference would have made */
+    int64_t self_path_count;  /* _topology_computeShortestPathToSelf calls */
+    int64_t cached_paths;     /* Paths in the cache */
+    double self_seconds;      /* engine time of the self-path rule */
 } topology_hip_info;
 
 /* HIP device the engine uses (default: $SHADOWTOPO_DEVICE or 0); before the first query */

@@ -1,0 +1,109 @@
+"""Test infrastructure (never imported by the product): a restatement of the reference's
+path cache -- which attached pairs Shadow 1.14 has cached, in which direction, after a
+sequence of queries -- so the tests can say what the drop-in getters must return.
+
+It follows /root/reference/src/main/routing/topology.c:
+  _topology_getPathEntry            :1969-2051  (cache lookup (s, t), then (t, s) when
+                                                 undirected; on a miss: direct lookup,
+                                                 self path or one Dijkstra from s)
+  _topology_getPathFromCache        :1284-1303
+  _topology_shouldStorePath         :1305-1334
+  _topology_storePathInCache        :1336-1386  (running minimum -> worker_updateMinTimeJump)
+  _topology_computeSourcePaths      :1655-1875  (stores every reachable attached target)
+  _topology_computeShortestPathToSelf :1545-1653
+  _topology_lookupDirectPath        :1877-1927
+
+The path VALUES come from the caller (the oracle's own-row matrix: entry (s, t) is what
+s's own computation gives), so this module decides only which entry a query sees.
+Self pairs reached from a Dijkstra run take the configured self value.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+class RefPathCache:
+    def __init__(self, lat, kind, *, directed, complete, prefer_direct, adjacent, reverse_blocks_directed=True):
+        """lat / kind: [A, A] oracle matrices over attached indices (kind 0 = unroutable);
+        adjacent(i, j): the graph has an edge i -> j (either way when undirected; i == j:
+        a self-loop).  reverse_blocks_directed: _topology_shouldStorePath refuses (s, t)
+        when (t, s) is cached even in a directed graph (topology.c:1311-1317), so there the
+        later query (s, t) finds no Path and fails; False models the drop-in, which stores
+        (s, t) in a directed graph (documented deviation)."""
+        self.lat = np.asarray(lat)
+        self.kind = np.asarray(kind)
+        self.A = self.lat.shape[0]
+        self.directed, self.complete, self.prefer_direct = directed, complete, prefer_direct
+        self.adjacent = adjacent
+        self.reverse_blocks = reverse_blocks_directed or not directed
+        self.cache = {}          # (s, t) -> latency of the stored Path
+        self.min_latency = 0.0   # topology.c minimumPathLatency
+        self.upcalls = []        # every value handed to worker_updateMinTimeJump
+        self.dijkstra_runs = 0
+        self.self_paths = 0
+
+    # ---------------------------------------------------------------- :1284-1386
+    def _from_cache(self, s, t):
+        return (s, t) if (s, t) in self.cache else None
+
+    def _should_store(self, is_direct, s, t):
+        if (s, t) in self.cache or (self.reverse_blocks and (t, s) in self.cache):
+            return False
+        if self.complete and not is_direct:
+            return False
+        if self.prefer_direct and not is_direct and self.adjacent(s, t):
+            return False
+        return True
+
+    def _store(self, is_direct, s, t):
+        if not self._should_store(is_direct, s, t):
+            return
+        latency = float(self.lat[s, t])
+        self.cache[(s, t)] = latency
+        if self.min_latency == 0 or latency < self.min_latency:
+            self.min_latency = latency
+            self.upcalls.append(latency)
+
+    # ---------------------------------------------------------------- miss branches
+    def _lookup_direct(self, s, t):  # :1877-1927 (get_eid fails without an edge)
+        if self.adjacent(s, t):
+            self._store(True, s, t)
+
+    def _self_path(self, s):  # :1545-1653 (no incident edge: no path)
+        self.self_paths += 1
+        if self.kind[s, s] != 0:
+            self._store(False, s, s)
+
+    def _compute_source_paths(self, s, t):  # :1655-1875
+        if s == t:
+            return self._self_path(s)
+        self.dijkstra_runs += 1
+        for position in range(self.A):  # the unique attached targets
+            if self.kind[s, position] == 0:  # igraph returns an empty path: nothing stored
+                continue
+            self._store(False, s, position)
+
+    # ---------------------------------------------------------------- :1969-2051
+    def get_path_entry(self, s, t):
+        """the (row, column) of the cached Path the query (s, t) returns, or None"""
+        path = self._from_cache(s, t)
+        if path is None and not self.directed:
+            path = self._from_cache(t, s)
+        if path is None:
+            if self.complete or (self.prefer_direct and self.adjacent(s, t)):
+                self._lookup_direct(s, t)
+            else:
+                self._compute_source_paths(s, t)
+            path = self._from_cache(s, t) or (None if self.directed else self._from_cache(t, s))
+        return path
+
+
+def adjacency_of(g, attached=None):
+    """adjacent(i, j) over attached indices of a synth graph (edge list g.src -> g.dst)"""
+    att = list(g.attached if attached is None else attached)
+    pairs = set()
+    for a, b in zip(np.asarray(g.src).tolist(), np.asarray(g.dst).tolist()):
+        pairs.add((a, b))
+        if not g.directed:
+            pairs.add((b, a))
+    return lambda i, j: (att[i], att[j]) in pairs

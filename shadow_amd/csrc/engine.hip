@@ -2662,9 +2662,16 @@ int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
 int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->self_ready) return SHADOWTOPO_OK;
     if (eng->A > 0) {
+        // timed on its own (one stream synchronisation per attached set): the shim reports it
+        // as the reference's self-path seconds (topology.c:1277-1280)
+        HIP_TRY(hipStreamSynchronize(s));
+        const auto t0 = std::chrono::steady_clock::now();
         hipLaunchKernelGGL(k_self, dim3((eng->A + 3) / 4), dim3(256), 0, s, eng->g, eng->d_attached, eng->A,
                            eng->d_self_lat, eng->d_self_rel, eng->d_self_hops, eng->d_self_kind);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(s));
+        eng->st.self_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        eng->st.self_paths += eng->A;
     }
     eng->self_ready = true;
     return SHADOWTOPO_OK;

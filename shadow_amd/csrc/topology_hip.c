@@ -145,6 +145,9 @@ typedef struct matrix {
     double* lat;
     double* rel;
     uint8_t* kind;
+    /* undirected late attach: rows [0, partial) hold the reverse-direction entries in
+     * columns >= partial until an old source's own row is needed (fill_old_rows) */
+    int32_t partial;
     struct matrix* next; /* retired matrices (readers may still hold them) */
 } matrix;
 
@@ -230,11 +233,17 @@ struct _Topology {
     int32_t ndev;
     int32_t devices[SHADOWTOPO_MAX_DEVICES];
     shadowtopo_engine* engs[SHADOWTOPO_MAX_DEVICES];
+    /* the reference's path cache as a set of attached pairs (cache_resolve): bit j % 64 of
+     * word i % 64 in the 64 x 64 tile (i / 64, j / 64), allocated on first store */
+    _Atomic(_Atomic(uint64_t*)*)* srow;
+    pthread_mutex_t cache_lock; /* misses (the reference's pathCacheLock writer side) */
     int self_rule;
     double min_latency;
     double compute_s;
-    int64_t compute_count;
-    int64_t self_count;
+    int64_t compute_count;   /* source rows computed on the GPU */
+    int64_t dijkstra_runs;   /* _topology_computeSourcePaths calls the reference would make */
+    int64_t self_count;      /* _topology_computeShortestPathToSelf calls */
+    int64_t cached_paths;    /* Paths in the emulated cache */
 };
 /* ------------------------------------------------------------ attribute helpers
  * _topology_find{Vertex,Edge,Graph}Attribute{String,Double} (topology.c:284-369): a value
@@ -706,24 +715,16 @@ static void free_snap(ip_snap* s) {
     free(s);
 }
 
-/* counter cell of attached pair (i, j): one per cached Path, i.e. per unordered pair in
- * undirected graphs (the reference stores one direction, topology.c:1312-1318); the
- * stored value is count + 1 so a touched pair is non-zero (the teardown log lists touched
- * pairs).  Tiles are allocated on first touch with a compare-and-swap, no lock. */
-static _Atomic uint64_t* counter_slot(Topology* top, int32_t i, int32_t j) {
-    if (!top->directed && j < i) {
-        int32_t t = i;
-        i = j;
-        j = t;
-    }
-    const int32_t ti = i / CTILE, tj = j / CTILE;
-    if (ti >= top->ctd || tj >= top->ctd) return NULL;
-    _Atomic(uint64_t*)* row = atomic_load_explicit(&top->crow[ti], memory_order_acquire);
+/* tile (ti, tj) of `words` u64 in a rows -> tiles table, allocated on first touch with a
+ * compare-and-swap (no lock); NULL when out of range or out of memory */
+static uint64_t* tile_get(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd, int32_t ti, int32_t tj, size_t words) {
+    if (!rows || ti >= ctd || tj >= ctd) return NULL;
+    _Atomic(uint64_t*)* row = atomic_load_explicit(&rows[ti], memory_order_acquire);
     if (!row) {
-        _Atomic(uint64_t*)* fresh = calloc((size_t)top->ctd, sizeof(*fresh));
+        _Atomic(uint64_t*)* fresh = calloc((size_t)ctd, sizeof(*fresh));
         if (!fresh) return NULL;
         _Atomic(uint64_t*)* expect = NULL;
-        if (atomic_compare_exchange_strong_explicit(&top->crow[ti], &expect, fresh, memory_order_acq_rel,
+        if (atomic_compare_exchange_strong_explicit(&rows[ti], &expect, fresh, memory_order_acq_rel,
                                                     memory_order_acquire))
             row = fresh;
         else {
@@ -733,7 +734,7 @@ static _Atomic uint64_t* counter_slot(Topology* top, int32_t i, int32_t j) {
     }
     uint64_t* tile = atomic_load_explicit(&row[tj], memory_order_acquire);
     if (!tile) {
-        uint64_t* fresh = calloc(CTILE * CTILE, sizeof(uint64_t));
+        uint64_t* fresh = calloc(words, sizeof(uint64_t));
         if (!fresh) return NULL;
         uint64_t* expect = NULL;
         if (atomic_compare_exchange_strong_explicit(&row[tj], &expect, fresh, memory_order_acq_rel,
@@ -744,7 +745,38 @@ static _Atomic uint64_t* counter_slot(Topology* top, int32_t i, int32_t j) {
             tile = expect;
         }
     }
-    return (_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)];
+    return tile;
+}
+
+/* the tile if it exists (readers: no allocation) */
+static uint64_t* tile_peek(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd, int32_t ti, int32_t tj) {
+    if (!rows || ti >= ctd || tj >= ctd) return NULL;
+    _Atomic(uint64_t*)* row = atomic_load_explicit(&rows[ti], memory_order_acquire);
+    return row ? atomic_load_explicit(&row[tj], memory_order_acquire) : NULL;
+}
+
+static void tiles_free(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd) {
+    if (!rows) return;
+    for (int32_t ti = 0; ti < ctd; ti++) {
+        _Atomic(uint64_t*)* row = atomic_load(&rows[ti]);
+        if (!row) continue;
+        for (int32_t tj = 0; tj < ctd; tj++) free(atomic_load(&row[tj]));
+        free((void*)row);
+    }
+    free((void*)rows);
+}
+
+/* counter cell of attached pair (i, j): one per cached Path, i.e. per unordered pair in
+ * undirected graphs (the reference stores one direction, topology.c:1312-1318); the
+ * stored value is count + 1 so a touched pair is non-zero. */
+static _Atomic uint64_t* counter_slot(Topology* top, int32_t i, int32_t j) {
+    if (!top->directed && j < i) {
+        int32_t t = i;
+        i = j;
+        j = t;
+    }
+    uint64_t* tile = tile_get(top->crow, top->ctd, i / CTILE, j / CTILE, CTILE * CTILE);
+    return tile ? (_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)] : NULL;
 }
 
 static uint64_t counter_peek(const Topology* top, int32_t i, int32_t j) {
@@ -753,13 +785,17 @@ static uint64_t counter_peek(const Topology* top, int32_t i, int32_t j) {
         i = j;
         j = t;
     }
-    const int32_t ti = i / CTILE, tj = j / CTILE;
-    if (!top->crow || ti >= top->ctd || tj >= top->ctd) return 0;
-    _Atomic(uint64_t*)* row = atomic_load_explicit(&top->crow[ti], memory_order_acquire);
-    if (!row) return 0;
-    uint64_t* tile = atomic_load_explicit(&row[tj], memory_order_acquire);
-    if (!tile) return 0;
-    return atomic_load_explicit((_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)], memory_order_relaxed);
+    uint64_t* tile = tile_peek(top->crow, top->ctd, i / CTILE, j / CTILE);
+    return tile ? atomic_load_explicit((_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)],
+                                       memory_order_relaxed)
+                : 0;
+}
+
+/* is the Path of attached pair (i, j) -- this direction -- in the emulated cache */
+static int stored_test(const Topology* top, int32_t i, int32_t j) {
+    uint64_t* tile = tile_peek(top->srow, top->ctd, i / CTILE, j / CTILE);
+    return tile && ((atomic_load_explicit((_Atomic uint64_t*)&tile[i % CTILE], memory_order_acquire) >>
+                     (j % CTILE)) & 1u);
 }
 
 static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix* m, int32_t i, int32_t j,
@@ -777,45 +813,44 @@ static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix
 void topology_free(Topology* top) {
     if (!top) return;
     matrix* m = atomic_load(&top->mat);
-    if (m && top->crow && shadowtopo_log_enabled(ST_INFO)) {
-        /* _topology_logAllCachedPaths (topology.c:1929-1967): every pair a query touched,
-         * with every packet counted since the first query (late attaches included) */
+    if (m && top->srow && shadowtopo_log_enabled(ST_INFO)) {
+        /* _topology_logAllCachedPaths (topology.c:1929-1967): every Path in the (emulated)
+         * cache, with every packet counted on it (late attaches included) */
         char buf[512];
         for (int32_t ti = 0; ti < top->ctd; ti++) {
-            _Atomic(uint64_t*)* row = atomic_load(&top->crow[ti]);
-            if (!row) continue;
             for (int32_t tj = 0; tj < top->ctd; tj++) {
-                uint64_t* tile = atomic_load(&row[tj]);
+                uint64_t* tile = tile_peek(top->srow, top->ctd, ti, tj);
                 if (!tile) continue;
-                for (int32_t k = 0; k < CTILE * CTILE; k++) {
-                    if (!tile[k]) continue;
-                    int32_t i = ti * CTILE + k / CTILE, j = tj * CTILE + k % CTILE;
-                    if (i >= m->A || j >= m->A) continue;
-                    int32_t s = top->attached[i], t = top->attached[j];
-                    st_info("Found path %s%s%s in cache: %s", vid(top, s), top->directed ? "->" : "<->",
-                            vid(top, t), path_string(top, s, t, m, i, j, tile[k] - 1, buf, sizeof buf));
+                for (int32_t a = 0; a < CTILE; a++) {
+                    for (uint64_t w = tile[a]; w; w &= w - 1) {
+                        int32_t i = ti * CTILE + a, j = tj * CTILE + __builtin_ctzll(w);
+                        if (i >= m->A || j >= m->A) continue;
+                        uint64_t c = counter_peek(top, i, j);
+                        int32_t s = top->attached[i], t = top->attached[j];
+                        st_info("Found path %s%s%s in cache: %s", vid(top, s), top->directed ? "->" : "<->",
+                                vid(top, t), path_string(top, s, t, m, i, j, c ? c - 1 : 0, buf, sizeof buf));
+                    }
                 }
             }
         }
     }
+    /* topology.c:1276-1280; the Dijkstra seconds are the GPU computation's, the self-path
+     * seconds the engine's self-rule kernel */
+    shadowtopo_stats est;
+    double self_s = 0.0;
+    for (int32_t k = 0; k < top->ndev; k++)
+        if (top->engs[k] && shadowtopo_get_stats(top->engs[k], &est) == SHADOWTOPO_OK) self_s += est.self_ms * 1e-3;
     st_message("path cache cleared, spent %f seconds computing %u shortest paths with dijkstra, "
                "and %f seconds computing %u shortest self paths",
-               top->compute_s, (unsigned)top->compute_count, 0.0, (unsigned)top->self_count);
+               top->compute_s, (unsigned)top->dijkstra_runs, self_s, (unsigned)top->self_count);
     free_matrix(m);
     for (matrix* r = top->retired; r;) {
         matrix* n = r->next;
         free_matrix(r);
         r = n;
     }
-    if (top->crow) {
-        for (int32_t ti = 0; ti < top->ctd; ti++) {
-            _Atomic(uint64_t*)* row = atomic_load(&top->crow[ti]);
-            if (!row) continue;
-            for (int32_t tj = 0; tj < top->ctd; tj++) free(atomic_load(&row[tj]));
-            free((void*)row);
-        }
-        free((void*)top->crow);
-    }
+    tiles_free(top->crow, top->ctd);
+    tiles_free(top->srow, top->ctd);
     free_snap(atomic_load(&top->snap));
     for (ip_snap* r = top->snap_retired; r;) {
         ip_snap* n = r->next;
@@ -839,6 +874,7 @@ void topology_free(Topology* top) {
     pthread_mutex_destroy(&top->compute_lock);
     pthread_mutex_destroy(&top->snap_lock);
     pthread_mutex_destroy(&top->idx_lock);
+    pthread_mutex_destroy(&top->cache_lock);
     top->magic = 0;
     free(top);
 }
@@ -860,6 +896,7 @@ Topology* topology_new(const char* graphPath) {
     pthread_mutex_init(&top->compute_lock, NULL);
     pthread_mutex_init(&top->snap_lock, NULL);
     pthread_mutex_init(&top->idx_lock, NULL);
+    pthread_mutex_init(&top->cache_lock, NULL);
     atomic_store(&top->ip_version, 1);
     atomic_store(&top->snap, NULL);
     const char* dev = getenv("SHADOWTOPO_DEVICE");
@@ -922,6 +959,7 @@ Topology* topology_new(const char* graphPath) {
     for (int32_t v = 0; v < top->V; v++) atomic_init(&top->att_index[v], -1);
     top->ctd = (top->V + CTILE - 1) / CTILE;
     top->crow = calloc((size_t)(top->ctd > 0 ? top->ctd : 1), sizeof(*top->crow));
+    top->srow = calloc((size_t)(top->ctd > 0 ? top->ctd : 1), sizeof(*top->srow));
     return top;
 }
 /* ------------------------------------------------------------ attach
@@ -1409,21 +1447,12 @@ static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A,
             m->kind[o] = m->kind[r];
         }
     }
+    m->partial = A0;
     clock_gettime(CLOCK_MONOTONIC, &t1);
     top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
-    top->compute_count += top->complete ? 0 : A - A0;
-    top->self_count += top->complete ? 0 : A - A0;
-    /* _topology_storePathInCache's running minimum (topology.c:1374-1385), over every path
-     * the matrix holds (it covers all attached pairs at once; the reference folds in paths
-     * as they are cached, so this window can be smaller, never larger: DESIGN.md 2) */
-    double mn = 0;
-    const size_t n = (size_t)A * (size_t)A;
-    for (size_t k = 0; k < n; k++)
-        if (m->kind[k] != SHADOWTOPO_KIND_NONE && (mn == 0 || m->lat[k] < mn)) mn = m->lat[k];
-    if (mn > 0 && (top->min_latency == 0 || mn < top->min_latency)) {
-        top->min_latency = mn;
-        worker_updateMinTimeJump(top->min_latency);
-    }
+    top->compute_count += A - A0;
+    /* the running minimum handed to worker_updateMinTimeJump is folded in as paths enter
+     * the emulated cache (cache_resolve), as the reference does */
     st_info("computed %d x %d attached-pair matrix (%d new rows) on %d device(s) (first %d) in %f seconds", A, A,
             A - A0, (int)top->ndev, (int)top->device, top->compute_s);
     return m;
@@ -1464,6 +1493,145 @@ static matrix* current_matrix(Topology* top, int32_t need) {
     }
     pthread_mutex_unlock(&top->compute_lock);
     return m;
+}
+
+/* Rows [0, m->partial) of an undirected late-attach matrix with their own entries for the
+ * columns the late attach added (compute_matrix copied the reverse direction there):
+ * needed once an old source's paths enter the cache (the reference reruns that source's
+ * Dijkstra against the grown target list).  Only entries that differ are written, so a
+ * reader of a cached entry never sees a store.  Caller holds cache_lock. */
+static int fill_old_rows(Topology* top, matrix* m) {
+    const int32_t P = m->partial, A = m->A;
+    if (P <= 0) return 0;
+    pthread_mutex_lock(&top->compute_lock);
+    int rc = -1;
+    int32_t* att = malloc(sizeof(int32_t) * (size_t)A);
+    matrix tmp;
+    memset(&tmp, 0, sizeof tmp);
+    tmp.A = A;
+    tmp.lat = malloc(sizeof(double) * (size_t)P * (size_t)A);
+    tmp.rel = malloc(sizeof(double) * (size_t)P * (size_t)A);
+    tmp.kind = malloc((size_t)P * (size_t)A);
+    if (att && tmp.lat && tmp.rel && tmp.kind) {
+        pthread_rwlock_rdlock(&top->ip_lock);
+        memcpy(att, top->attached, sizeof(int32_t) * (size_t)A);  /* attach order: a stable prefix */
+        pthread_rwlock_unlock(&top->ip_lock);
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        if (ensure_engine(top) == 0 && compute_rows_sharded(top, att, A, 0, P, &tmp) == 0) {
+            for (size_t o = 0; o < (size_t)P * (size_t)A; o++) {
+                if (memcmp(&m->lat[o], &tmp.lat[o], sizeof(double))) m->lat[o] = tmp.lat[o];
+                if (memcmp(&m->rel[o], &tmp.rel[o], sizeof(double))) m->rel[o] = tmp.rel[o];
+                if (m->kind[o] != tmp.kind[o]) m->kind[o] = tmp.kind[o];
+            }
+            m->partial = 0;
+            top->compute_count += P;
+            rc = 0;
+        }
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    }
+    free(att);
+    free(tmp.lat);
+    free(tmp.rel);
+    free(tmp.kind);
+    pthread_mutex_unlock(&top->compute_lock);
+    if (rc) st_critical("recomputing the rows of hosts attached before a late attach failed");
+    return rc;
+}
+
+/* _topology_storePathInCache (topology.c:1336-1386) for attached pair (i, j) of m, whose
+ * _topology_shouldStorePath checks the caller made; returns the stored latency */
+static double cache_store(Topology* top, const matrix* m, int32_t i, int32_t j) {
+    uint64_t* tile = tile_get(top->srow, top->ctd, i / CTILE, j / CTILE, CTILE);
+    if (tile) atomic_fetch_or_explicit((_Atomic uint64_t*)&tile[i % CTILE], 1ull << (j % CTILE), memory_order_release);
+    top->cached_paths++;
+    return m->lat[(size_t)i * m->A + j];
+}
+
+/* The reference's path cache over the eager matrix.  Every value is computed up front; what
+ * follows the reference's query order is WHICH pairs are cached and in which direction, so
+ * a getter returns exactly the entry the reference would (_topology_getPathEntry tries
+ * (s, t), then (t, s) in undirected graphs, topology.c:1983-1990), the minimum handed to
+ * worker_updateMinTimeJump changes when the reference's would (:1374-1385), the teardown
+ * log lists the reference's cached Paths (:1929-1967), and the Dijkstra / self-path counts
+ * are the reference's.  A miss (:1992-2045) replays the reference's branch, which the pair's
+ * kind already encodes (k_compose's dispatch of the same rules):
+ *   DIRECT    -> _topology_lookupDirectPath: (s, t) alone;
+ *   s == t    -> _topology_computeShortestPathToSelf: (s, s);
+ *   otherwise -> _topology_computeSourcePaths (:1655-1875): one Dijkstra from s, storing
+ *                (s, t') for every attached t' that igraph reaches and that
+ *                _topology_shouldStorePath accepts (:1309-1334: neither direction cached
+ *                yet; not a non-direct path where the graph prefers an existing direct
+ *                edge), t' = s included with the configured self value.
+ * Returns the cached direction in (si, sj), or -1 when the pair has no path. */
+static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32_t* si, int32_t* sj) {
+    matrix* m = *mp;
+    if (stored_test(top, i, j)) goto fwd;
+    if (!top->directed && stored_test(top, j, i)) goto rev;
+    pthread_mutex_lock(&top->cache_lock);
+    if (stored_test(top, i, j)) {
+        pthread_mutex_unlock(&top->cache_lock);
+        goto fwd;
+    }
+    if (!top->directed && stored_test(top, j, i)) {
+        pthread_mutex_unlock(&top->cache_lock);
+        goto rev;
+    }
+    /* a late attach may have published a larger matrix meanwhile: its target list is the
+     * one the reference's Dijkstra would use now */
+    matrix* cur = atomic_load_explicit(&top->mat, memory_order_acquire);
+    if (cur && cur->A > (i > j ? i : j)) *mp = m = cur;
+    const int32_t A = m->A;
+    const uint8_t k = m->kind[(size_t)i * A + j];
+    double mn = 0.0;
+    int stored = 0;
+    if (k == SHADOWTOPO_KIND_DIRECT || top->complete) {
+        if (k == SHADOWTOPO_KIND_DIRECT) {  /* a complete graph without the edge: get_eid fails */
+            mn = cache_store(top, m, i, j);
+            stored = 1;
+        }
+    } else if (i == j) {
+        top->self_count++;
+        if (k != SHADOWTOPO_KIND_NONE) {
+            mn = cache_store(top, m, i, i);
+            stored = 1;
+        }
+    } else {
+        top->dijkstra_runs++;
+        if (i < m->partial && fill_old_rows(top, m)) {
+            pthread_mutex_unlock(&top->cache_lock);
+            return -1;
+        }
+        const uint8_t* kr = m->kind + (size_t)i * A;
+        for (int32_t t = 0; t < A; t++) {
+            /* reachable targets only (an empty igraph path is never stored); a pair whose
+             * rule is the direct edge is not stored from a Dijkstra run */
+            if (kr[t] == SHADOWTOPO_KIND_NONE || kr[t] == SHADOWTOPO_KIND_DIRECT) continue;
+            if (stored_test(top, i, t) || (!top->directed && stored_test(top, t, i))) continue;
+            const double l = cache_store(top, m, i, t);
+            if (!stored || l < mn) mn = l;
+            stored = 1;
+        }
+    }
+    /* the running minimum (topology.c:1374-1385: `minimumPathLatency == 0 || lower`) */
+    if (stored && (top->min_latency == 0 || mn < top->min_latency)) {
+        top->min_latency = mn;
+        worker_updateMinTimeJump(top->min_latency);
+    }
+    const int fwd_ok = stored_test(top, i, j), rev_ok = !top->directed && stored_test(top, j, i);
+    pthread_mutex_unlock(&top->cache_lock);
+    if (fwd_ok) goto fwd;
+    if (rev_ok) goto rev;
+    return -1;
+fwd:
+    *si = i;
+    *sj = j;
+    return 0;
+rev:
+    *si = j;
+    *sj = i;
+    return 0;
 }
 
 /* IP -> vertex snapshot for the per-packet path: rebuilt (under snap_lock) only when an
@@ -1528,14 +1696,12 @@ static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off
     int32_t i = atomic_load_explicit(&top->att_index[vs], memory_order_acquire);
     int32_t j = atomic_load_explicit(&top->att_index[vd], memory_order_acquire);
     matrix* m = (i >= 0 && j >= 0) ? current_matrix(top, i > j ? i : j) : NULL;
-    if (m) {
-        size_t o = (size_t)i * (size_t)m->A + (size_t)j;
-        if (m->kind[o] != SHADOWTOPO_KIND_NONE) {
-            *off = o;
-            if (ri) *ri = i;
-            if (rj) *rj = j;
-            return m;
-        }
+    int32_t si, sj;
+    if (m && cache_resolve(top, &m, i, j, &si, &sj) == 0) {
+        *off = (size_t)si * (size_t)m->A + (size_t)sj;
+        if (ri) *ri = si;
+        if (rj) *rj = sj;
+        return m;
     }
     st_error("unable to find path between node %s at %s (vertex %i) and node %s at %s (vertex %i)",
              address_toString(src), vid(top, vs), (int)vs, address_toString(dst), vid(top, vd), (int)vd);
@@ -1623,6 +1789,13 @@ int topology_hip_get_info(Topology* top, topology_hip_info* out) {
     out->min_path_latency = top->min_latency;
     out->compute_seconds = top->compute_s;
     out->compute_count = top->compute_count;
+    out->dijkstra_runs = top->dijkstra_runs;
+    out->self_path_count = top->self_count;
+    out->cached_paths = top->cached_paths;
+    shadowtopo_stats est;
+    for (int32_t k = 0; k < top->ndev; k++)
+        if (top->engs[k] && shadowtopo_get_stats(top->engs[k], &est) == SHADOWTOPO_OK)
+            out->self_seconds += est.self_ms * 1e-3;
     out->compute_failed = top->compute_failed;
     return 0;
 }

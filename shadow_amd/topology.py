@@ -35,6 +35,8 @@ class Info(ctypes.Structure):
         ("prefers_direct_paths", ctypes.c_int32), ("n_attached", ctypes.c_int32), ("computed_for", ctypes.c_int32),
         ("device", ctypes.c_int32), ("min_path_latency", ctypes.c_double), ("compute_seconds", ctypes.c_double),
         ("compute_count", ctypes.c_int64), ("n_devices", ctypes.c_int32), ("compute_failed", ctypes.c_int32),
+        ("dijkstra_runs", ctypes.c_int64), ("self_path_count", ctypes.c_int64), ("cached_paths", ctypes.c_int64),
+        ("self_seconds", ctypes.c_double),
     ]
 
     def as_dict(self):

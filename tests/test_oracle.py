@@ -206,3 +206,30 @@ def test_tie_break_second_restatement(case):
             pl, pr, ph = rg.pair(int(s), int(t), p_p)
             assert (pl, pr, ph) == (lat[i, j], rel[i, j], hops[i, j]), (s, t)
     assert ties > 0  # the fixtures do exercise heap-order ties
+
+
+def test_path_cache_model_reference_quirks():
+    """oracle/path_cache_ref.py restates topology.c's cache literally: in an undirected graph
+    the second direction of a pair is served by the first one's Path; in a directed graph
+    _topology_shouldStorePath refuses (s, t) once (t, s) is cached, so the reference's query
+    (s, t) then finds no Path (the drop-in stores it: reverse_blocks_directed=False)"""
+    import numpy as np
+    from oracle.path_cache_ref import RefPathCache
+    lat = np.array([[2.0, 5.0, 7.0], [6.0, 2.0, 4.0], [7.5, 4.5, 3.0]])
+    kind = np.array([[2, 3, 3], [3, 2, 3], [3, 3, 2]])
+    adj = lambda i, j: False  # noqa: E731
+    und = RefPathCache(lat, kind, directed=False, complete=False, prefer_direct=False, adjacent=adj)
+    assert und.get_path_entry(1, 0) == (1, 0)
+    assert und.get_path_entry(0, 1) == (1, 0)  # served by the reverse Path
+    assert und.get_path_entry(0, 2) == (0, 2)  # source 0's Dijkstra: its own row
+    # source 1's run stored (1,0)=6 then (1,1)=2: two upcalls; source 0's run nothing lower
+    assert und.dijkstra_runs == 2 and und.upcalls == [6.0, 2.0] and und.min_latency == 2.0
+    assert und.get_path_entry(0, 0) == (0, 0) and und.self_paths == 0  # cached by source 0's run
+    assert und.get_path_entry(2, 2) == (2, 2) and und.self_paths == 1  # a self-path run
+    d = RefPathCache(lat, kind, directed=True, complete=False, prefer_direct=False, adjacent=adj)
+    assert d.get_path_entry(1, 0) == (1, 0)
+    assert d.get_path_entry(0, 1) is None  # the reference's quirk
+    d2 = RefPathCache(lat, kind, directed=True, complete=False, prefer_direct=False, adjacent=adj,
+                      reverse_blocks_directed=False)
+    d2.get_path_entry(1, 0)
+    assert d2.get_path_entry(0, 1) == (0, 1)

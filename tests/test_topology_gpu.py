@@ -7,6 +7,7 @@ import os
 import numpy as np
 import pytest
 
+from oracle.path_cache_ref import RefPathCache, adjacency_of
 from paritylib import oracle_matrix
 from shadow_amd import synth
 from shadow_amd import topology as T
@@ -44,23 +45,50 @@ def attach_all(top, ips, vertices, base=0):
     return hosts
 
 
+def ref_cache(g, lat_o, kind_o, complete=False):
+    # directed graphs: the drop-in stores (s, t) even when (t, s) is cached (the reference
+    # refuses it and then fails the query: DESIGN.md 2)
+    return RefPathCache(lat_o, kind_o, directed=g.directed, complete=complete, prefer_direct=bool(g.prefer_direct),
+                        adjacent=adjacency_of(g), reverse_blocks_directed=False)
+
+
+def check_cache_state(top, model):
+    """what the reference's path cache would hold after the same queries: the count of
+    cached Paths, Dijkstra and self-path runs, and the minimum handed to the simulator"""
+    inf = top.info()
+    assert inf["cached_paths"] == len(model.cache)
+    assert inf["dijkstra_runs"] == model.dijkstra_runs
+    assert inf["self_path_count"] == model.self_paths
+    assert inf["min_path_latency"] == model.min_latency
+    if model.upcalls:
+        assert T.last_min_time_jump() == model.upcalls[-1]
+
+
 def check_against_oracle(tmp_path, g, n_hosts=None):
+    """every ordered pair, queried row by row: each getter returns the entry of the Path the
+    reference has cached for the pair (its own row's value, or the reverse direction's
+    when the other host's Dijkstra ran first: topology.c:1983-1990)"""
     va, ips = with_vertex_ips(g)
     text = synth.to_graphml(g, extra_vattr=va, prefer_direct=("true" if g.prefer_direct else None))
     top = T.Topology.new(write(tmp_path, "g.xml", text))
     assert top is not None
     hosts = attach_all(top, ips, g.attached)
     lat_o, rel_o, hops_o, kind_o, _ = oracle_matrix(g)
+    model = ref_cache(g, lat_o, kind_o)
+    reversed_seen = 0
     for i, a in enumerate(hosts):
         for j, b in enumerate(hosts):
+            si, sj = model.get_path_entry(i, j)
+            reversed_seen += (si, sj) != (i, j)
             lat = top.getLatency(a, b)
-            assert lat == lat_o[i, j], (i, j, lat, lat_o[i, j])
-            assert top.getReliability(a, b) == rel_o[i, j]
+            assert lat == lat_o[si, sj], (i, j, lat, lat_o[si, sj])
+            assert top.getReliability(a, b) == rel_o[si, sj]
             assert top.isRoutable(a, b)
     inf = top.info()
     assert inf["computed_for"] == len(hosts)
-    valid = kind_o > 0
-    assert T.last_min_time_jump() == lat_o[valid].min() == inf["min_path_latency"]
+    check_cache_state(top, model)
+    if not g.directed:
+        assert reversed_seen > 0  # the lower triangle came from the upper one's Paths
     return top, hosts
 
 
@@ -143,47 +171,94 @@ def _subset(g, k):
 
 @pytest.mark.parametrize("directed", [False, True])
 def test_late_attach_keeps_counters_and_values(tmp_path, directed):
-    """hosts attached after the first query: an undirected graph computes only the new rows
-    (an old source's entry for a new target is the new target's entry for it, the value the
-    reference returns once the new host's paths are cached first, topology.c:1987-1990), a
-    directed graph recomputes every row; packet counters survive both late attaches"""
+    """hosts attached after the first query: an undirected graph computes the new rows (old
+    rows get their own entries for the new targets only once an old host's Dijkstra would
+    run again), a directed graph recomputes every row; every getter returns the entry of
+    the Path the reference has cached at that point, and packet counters survive both late
+    attaches"""
     g = synth.random_sparse(V=90, avg_deg=4, seed=45, A=30, directed=directed)
+    g26 = _subset(g, 26)
+    lat_o, rel_o, _, kind_o, _ = oracle_matrix(g26)
+    model = ref_cache(g26, lat_o, kind_o)
     va, ips = with_vertex_ips(g)
     top = T.Topology.new(write(tmp_path, "l.xml", synth.to_graphml(g, extra_vattr=va)))
     hosts = attach_all(top, ips, g.attached[:10])
     vx = [top.vertex_of_ip(h.ip) for h in hosts]
-    l01 = top.getLatency(hosts[0], hosts[1])
+
+    def q(i, j, a, b):
+        path = model.get_path_entry(i, j)
+        got = top.getLatency(a, b)
+        if path is None:  # unroutable (directed graphs)
+            assert got == -1.0 and top.getReliability(a, b) == -1.0, (i, j)
+            return got
+        si, sj = path
+        assert got == lat_o[si, sj], (i, j, si, sj)
+        assert top.getReliability(a, b) == rel_o[si, sj], (i, j)
+        return got
+
+    model.A = 10
+    l01 = q(0, 1, hosts[0], hosts[1])
     for _ in range(3):
         top.incrementPathPacketCounter(hosts[0], hosts[1])
     top.incrementPathPacketCounter(hosts[2], hosts[5])
+    q(2, 5, hosts[2], hosts[5])
     assert top.info()["computed_for"] == 10
     more = attach_all(top, ips, g.attached[10:20], base=100)
-    assert top.getLatency(hosts[0], more[1]) > 0
+    model.A = 20
+    q(0, 11, hosts[0], more[1])  # host 0's Dijkstra again: its own row for the new targets
     assert top.info()["computed_for"] == 20
-    assert top.getLatency(hosts[0], hosts[1]) == l01
+    assert q(0, 1, hosts[0], hosts[1]) == l01
+    q(13, 4, more[3], hosts[4])  # new source, old target
+    q(4, 13, hosts[4], more[3])
     top.incrementPathPacketCounter(hosts[0], hosts[1])
     top.incrementPathPacketCounter(more[0], hosts[3])
+    model.get_path_entry(10, 3)
     assert top.packet_count(vx[0], vx[1]) == 4
     assert top.packet_count(vx[2], vx[5]) == 1
     even_more = attach_all(top, ips, g.attached[20:26], base=200)
+    model.A = 26
     top.incrementPathPacketCounter(even_more[0], hosts[0])
+    model.get_path_entry(20, 0)
     assert top.info()["computed_for"] == 26
     assert top.packet_count(vx[0], vx[1]) == 4
     assert top.packet_count(top.vertex_of_ip(more[0].ip), vx[3]) == 1
     assert top.packet_count(top.vertex_of_ip(even_more[0].ip), vx[0]) == 1
-    # values: rows from each source's own computation, late columns of older rows from the
-    # reverse direction (undirected) or recomputed (directed)
     all_hosts = hosts + more + even_more
-    lat_o, rel_o, _, _, _ = oracle_matrix(_subset(g, 26))
     for i, a in enumerate(all_hosts):
         for j, b in enumerate(all_hosts):
-            first = 0 if max(i, j) < 10 else (10 if max(i, j) < 20 else 20)  # attach wave that made (i, j) known
-            si, sj = (i, j)
-            if not directed and i < first and j >= first:
-                si, sj = j, i  # the new target's own entry
-            assert top.getLatency(a, b) == lat_o[si, sj], (i, j)
-            assert top.getReliability(a, b) == rel_o[si, sj], (i, j)
+            q(i, j, a, b)
+    check_cache_state(top, model)
     top.free()
+
+
+def test_cache_emulation_upcalls_and_teardown_log(tmp_path, capfd):
+    """the drop-in's cache follows the reference's query order: the minimum handed to
+    worker_updateMinTimeJump after each query, the Dijkstra / self-path run counts, and the
+    teardown log listing every cached Path with its packet count (topology.c:1929-1967)"""
+    g = synth.random_sparse(V=80, avg_deg=4, seed=48, A=12)
+    va, ips = with_vertex_ips(g)
+    top = T.Topology.new(write(tmp_path, "u.xml", synth.to_graphml(g, extra_vattr=va)))
+    hosts = attach_all(top, ips, g.attached)
+    lat_o, _, _, kind_o, _ = oracle_matrix(g)
+    model = ref_cache(g, lat_o, kind_o)
+    rng = np.random.default_rng(3)
+    for _ in range(40):
+        i, j = (int(x) for x in rng.integers(0, len(hosts), 2))
+        si, sj = model.get_path_entry(i, j)
+        assert top.getLatency(hosts[i], hosts[j]) == lat_o[si, sj]
+        top.incrementPathPacketCounter(hosts[i], hosts[j])
+        check_cache_state(top, model)
+    assert 0 < model.dijkstra_runs < len(hosts)
+    T.set_log_level(4)
+    capfd.readouterr()
+    top.free()
+    T.set_log_level(1)
+    err = capfd.readouterr()
+    text = err.out + err.err
+    found = [ln for ln in text.splitlines() if "Found path" in ln]
+    assert len(found) == len(model.cache)
+    assert sum(int(ln.split("PacketCount=")[1].split()[0]) for ln in found) == 40
+    assert "shortest paths with dijkstra" in text
 
 
 def test_c_harness_lookups_under_threads(tmp_path):
@@ -208,10 +283,12 @@ def test_rows_sharded_over_engines(tmp_path, devices):
     top = T.Topology.new(write(tmp_path, "m.xml", synth.to_graphml(g, extra_vattr=va)))
     assert top.set_devices(devices) == 0
     hosts = attach_all(top, ips, g.attached)
-    lat_o, rel_o, _, _, _ = oracle_matrix(g)
+    lat_o, rel_o, _, kind_o, _ = oracle_matrix(g)
+    model = ref_cache(g, lat_o, kind_o)
     for i in range(0, len(hosts), 3):
         for j in range(len(hosts)):
-            assert top.getLatency(hosts[i], hosts[j]) == lat_o[i, j]
-            assert top.getReliability(hosts[i], hosts[j]) == rel_o[i, j]
+            si, sj = model.get_path_entry(i, j)
+            assert top.getLatency(hosts[i], hosts[j]) == lat_o[si, sj]
+            assert top.getReliability(hosts[i], hosts[j]) == rel_o[si, sj]
     assert top.info()["n_devices"] == len(devices)
     top.free()
