@@ -99,6 +99,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               wave per active (vertex, batch) pair) when under half the pairs are
                                               active, the grid otherwise; 2 = worklists always; 0 = one wave per pair
                                               of the grid */
+#define SHADOWTOPO_OPT_GRID_X 15           /* testing: largest x dimension (blocks, a multiple of 8) of the sparse
+                                              relax grids before they go 2-D (default 2^23: 2^31 work-items per
+                                              launch, under the dispatch packet's 32-bit count) */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
                                               engine may take (default 1000); engines sharing one device split it */
 

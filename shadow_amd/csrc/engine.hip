@@ -189,13 +189,19 @@ __device__ __forceinline__ double dmax() { return __longlong_as_double(0x7feffff
 // range [x*S, (x+1)*S) of the group-major (group, tile) order -- so a group's tiles share
 // one XCD (its [V][64] state stays in that L2) when there are >= 8 groups, and a group is
 // spread over several XCDs when there are fewer.  Placement is a speed hint only.
-__device__ __forceinline__ bool xcd_tile(int32_t L, int32_t ngroups, int32_t ntiles, int32_t& grp, int32_t& tile) {
+__device__ __forceinline__ bool xcd_tile(int64_t L, int32_t ngroups, int32_t ntiles, int32_t& grp, int32_t& tile) {
     const int64_t S = ((int64_t)ngroups * ntiles + 7) / 8;
-    const int64_t i = (int64_t)(L & 7) * S + (L >> 3);
+    if ((L >> 3) >= S) return false;  // padding blocks of a 2-D grid (grid_of)
+    const int64_t i = (L & 7) * S + (L >> 3);
     grp = (int32_t)(i / ntiles);
     tile = (int32_t)(i - (int64_t)grp * ntiles);
     return grp < ngroups;
 }
+
+// Linear block id of a grid from grid_of: a launch's work-item count is a 32-bit field of
+// the dispatch packet, so grids past 2^24 blocks of 256 go 2-D (x a multiple of 8, so
+// flat & 7 is still the XCD the block runs on).
+__device__ __forceinline__ int64_t flat_block() { return (int64_t)blockIdx.y * gridDim.x + blockIdx.x; }
 
 // f32 filter key of a distance: rounded toward -inf, NaN when unreached (see k_relax_dense_f)
 __device__ __forceinline__ float f32_key(double d) {
@@ -408,7 +414,7 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
                                                int32_t V, int32_t nb, int32_t nvb, int32_t parity,
                                                int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
     int32_t b, vt;
-    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
+    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int32_t v = vt * 4 + wave;
     if (v >= V) return;
@@ -494,9 +500,10 @@ __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in
                                                   int32_t nb, int64_t S, int32_t* __restrict__ cnt,
                                                   unsigned long long* __restrict__ prof) {
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t i = (int64_t)(blockIdx.x & 7) * S + (int64_t)(blockIdx.x >> 3) * 4 + wave;
+    const int64_t L = flat_block();
+    const int64_t i = (L & 7) * S + (L >> 3) * 4 + wave;
     const int64_t T = prefix[nb];
-    if ((int64_t)(blockIdx.x >> 3) * 4 + wave >= S || i >= T) return;
+    if ((L >> 3) * 4 + wave >= S || i >= T) return;
     const int lane = threadIdx.x & 63;
     const int32_t b = wl_batch(prefix, nb, i, lane);
     const int32_t v = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x;
@@ -522,7 +529,7 @@ __global__ __launch_bounds__(256) void k_relax_delta(const int64_t* __restrict__
                                                      int32_t nb, int32_t nvb, int32_t parity, int32_t* __restrict__ cnt,
                                                      unsigned long long* __restrict__ prof) {
     int32_t b, vt;
-    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
+    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int32_t v = vt * 4 + wave;
     if (v >= V) return;
@@ -745,7 +752,7 @@ __global__ __launch_bounds__(256) void k_relax_st(const int64_t* __restrict__ in
                                                   int32_t nb, int32_t nvb, int32_t parity, int32_t round,
                                                   int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
     int32_t b, vt;
-    if (!xcd_tile(blockIdx.x, nb, nvb, b, vt)) return;
+    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int32_t v = vt * 4 + wave;
     if (v >= V) return;
@@ -864,9 +871,10 @@ __global__ __launch_bounds__(256) void k_relax_cm(const int64_t* __restrict__ in
                                                   int32_t nb, int64_t S_, int32_t* __restrict__ cnt,
                                                   unsigned long long* __restrict__ prof) {
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t i = (int64_t)(blockIdx.x & 7) * S_ + (int64_t)(blockIdx.x >> 3) * 4 + wave;
+    const int64_t Lb = flat_block();
+    const int64_t i = (Lb & 7) * S_ + (Lb >> 3) * 4 + wave;
     const int64_t T = prefix[nb];
-    if ((int64_t)(blockIdx.x >> 3) * 4 + wave >= S_ || i >= T) return;
+    if ((Lb >> 3) * 4 + wave >= S_ || i >= T) return;
     const int lane = threadIdx.x & 63;
     const int32_t b = wl_batch(prefix, nb, i, lane);
     const int4 item = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])];
@@ -2509,6 +2517,7 @@ struct shadowtopo_engine {
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
+    int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
     int32_t* d_nlive = nullptr;        // [nb_cap]
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
@@ -2728,6 +2737,16 @@ hipError_t launch_dense_f(shadowtopo_engine* eng, int32_t nbg, int32_t par, int3
     }
 }
 
+// A 1-D launch of n blocks as a grid whose work-item count fits the dispatch packet's 32-bit
+// fields: x up to 2^23 blocks (a multiple of 8; x 256 threads = 2^31 work-items), y the
+// rest; kernels index with flat_block().  (A 1-D grid past 2^24 blocks wraps the count and
+// silently drops blocks.)
+dim3 grid_of(const shadowtopo_engine* eng, int64_t n) {
+    const int64_t GX = eng->opt_grid_x;
+    if (n <= GX) return dim3((uint32_t)std::max<int64_t>(n, 1));
+    return dim3((uint32_t)GX, (uint32_t)((n + GX - 1) / GX));
+}
+
 // relax rounds for the batch slots [0, nbg) until no vertex changes
 int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = eng->V;
@@ -2867,31 +2886,31 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             }
         } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED) {
             eng->st.relax_batches += nbg;
-            hipLaunchKernelGGL(k_relax_st, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+            hipLaunchKernelGGL(k_relax_st, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_w32, g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1),
                                (int32_t)(round & 0x7fffffff), cnt_cur, eng->d_prof);
         } else if (masked) {
             eng->st.relax_batches += nbg;
             eng->st.wl_launches++;
             const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
-            hipLaunchKernelGGL(k_relax_cm, dim3((uint32_t)(8 * (S / 4))), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+            hipLaunchKernelGGL(k_relax_cm, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 0x7fffffff), eng->d_wl,
                                eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else if (round_wl) {
             eng->st.relax_batches += nbg;
             eng->st.wl_launches++;
             const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
-            hipLaunchKernelGGL(k_relax_wl, dim3((uint32_t)(8 * (S / 4))), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+            hipLaunchKernelGGL(k_relax_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
                                eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FULL) {
             eng->st.relax_batches += nbg;
-            hipLaunchKernelGGL(k_relax, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
+            hipLaunchKernelGGL(k_relax, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
                                g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
                                eng->d_prof);
         } else {
             eng->st.relax_batches += nbg;
-            hipLaunchKernelGGL(k_relax_delta, dim3((uint32_t)nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+            hipLaunchKernelGGL(k_relax_delta, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
                                eng->d_prof);
         }
@@ -3627,6 +3646,11 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_SEED:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");
             eng->opt_dense_seed = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_GRID_X:
+            if (value < 8 || value % 8 || value > ((int64_t)1 << 23))
+                return fail(SHADOWTOPO_EINVAL, "grid x limit must be a multiple of 8 in [8, 2^23]");
+            eng->opt_grid_x = value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_WORKLIST:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "worklist must be 0, 1 or 2");

@@ -59,6 +59,17 @@ def test_csr_full_grid_without_worklists(case):
     compare(g, layout="csr", csr_variant=E.CSR_FULL, worklist=1, batches_in_flight=2)
 
 
+@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL, E.CSR_FILTERED, E.CSR_MASKED])
+@pytest.mark.parametrize("worklist", [0, 1, 2])
+def test_csr_two_dimensional_grids(variant, worklist):
+    """grids past 2^24 blocks (C5: 102 batches x 868k vertices = 22M blocks of 256) go 2-D
+    (grid_of / flat_block: a 1-D launch's 32-bit work-item count would wrap and drop
+    blocks, and a round that dropped a batch could end the iteration early); forcing the
+    2-D form on every launch of a small graph must give the same matrices"""
+    g = synth.random_sparse(V=400, avg_deg=5, seed=38)
+    compare(g, layout="csr", csr_variant=variant, worklist=worklist, grid_x=64)
+
+
 @pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FILTERED, E.CSR_MASKED])
 def test_csr_delta_several_groups(variant):
     g = synth.random_sparse(V=500, avg_deg=4, seed=37)
