@@ -160,6 +160,7 @@ typedef struct shadowtopo_stats {
     double self_ms;          /* host wall time of the self-path rule (k_self), once per attached set
                                 (the reference's selfPathTotalTime, topology.c:1608-1617) */
     int64_t self_paths;      /* attached vertices the self-path rule ran for */
+    int64_t pruned_deltas;   /* dense: delta launches in the locality order with chunk bounds (OPT_DENSE_PRUNE) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

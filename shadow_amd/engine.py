@@ -75,7 +75,7 @@ class Stats(ctypes.Structure):
         ("full_ms", ctypes.c_double), ("delta_ms", ctypes.c_double),
         ("full_batches", ctypes.c_int64), ("full_changes", ctypes.c_int64), ("relax_batches", ctypes.c_int64),
         ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double), ("sparse_deltas", ctypes.c_int64),
-        ("self_ms", ctypes.c_double), ("self_paths", ctypes.c_int64),
+        ("self_ms", ctypes.c_double), ("self_paths", ctypes.c_int64), ("pruned_deltas", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -289,13 +289,24 @@ def test_dense_prune_same_results(case):
         g = synth.geometric_complete_ish(V=2500, A=400, drop=0.2)  # 7 batches, many skipped chunks
     srcs = np.arange(0, g.n, 3, dtype=np.int32)
     rows, mats = [], []
-    for prune in (0, 1):
+    for prune, permille in ((0, 125), (1, 125), (1, 1000)):
         eng = E.Engine.from_synth(g, layout="dense")
         eng.set_option(E.OPT_DENSE_PRUNE, prune)
+        eng.set_option(E.OPT_DELTA_PERMILLE, permille)  # 1000: every round after the first is a delta round
         eng.set_attached(g.attached)
         mats.append(eng.compute_rows(want_kind=True))  # builds the vertex order when pruning
-        rows.append(eng.sssp(srcs))  # full rows through the (pruned) sweep
+        rows.append(eng.sssp(srcs))  # full rows through the (pruned) sweep and delta rounds
+        st = eng.stats()
+        if prune:  # every delta round in the locality order (chunk bounds) or over live-chunk lists
+            assert st["pruned_deltas"] + st["sparse_deltas"] == st["delta_sweeps"]
+            if case == "geometric_big":
+                assert st["pruned_deltas"] > 0
         eng.close()
+    assert np.array_equal(rows[1][0].view(np.uint64), rows[2][0].view(np.uint64))
+    for x, y in zip(mats[1], mats[2]):
+        assert np.array_equal(x.view(np.uint8) if x.dtype == np.float64 else x,
+                              y.view(np.uint8) if y.dtype == np.float64 else y)
+    rows, mats = rows[:2], mats[:2]
     (d0, p0, h0, t0), (d1, p1, h1, t1) = rows
     assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64))
     assert np.array_equal(t0, t1)
@@ -386,6 +397,8 @@ def test_dense_delta_live_chunks(case, live, monkeypatch):
         g.prefer_direct = True
     else:
         g = synth.geometric_complete_ish(V=900, A=200)
-    st = compare(g, layout="dense", delta_permille=1000)
+    # (the live-chunk lists serve the unpruned order; the pruned delta rounds bound chunks
+    # themselves: test_dense_prune_same_results)
+    st = compare(g, layout="dense", delta_permille=1000, dense_prune=0)
     assert st["dense"] == 1 and st["delta_sweeps"] > 0
     assert (st["sparse_deltas"] > 0) == (live == "1")
