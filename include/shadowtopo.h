@@ -102,6 +102,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_GRID_X 15           /* testing: largest x dimension (blocks, a multiple of 8) of the sparse
                                               relax grids before they go 2-D (default 2^23: 2^31 work-items per
                                               launch, under the dispatch packet's 32-bit count) */
+#define SHADOWTOPO_OPT_PRUNE_PENDANT 16   /* CSR rows of an undirected graph: 1 (default) = relax without the
+                                              pendant trees that hold no attached vertex (peeled non-attached
+                                              vertices with one neighbour; they lie on no attached-pair path);
+                                              0 = every vertex. Results are identical. */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
                                               engine may take (default 1000); engines sharing one device split it */
 
@@ -161,6 +165,7 @@ typedef struct shadowtopo_stats {
                                 (the reference's selfPathTotalTime, topology.c:1608-1617) */
     int64_t self_paths;      /* attached vertices the self-path rule ran for */
     int64_t pruned_deltas;   /* dense: delta launches in the locality order with chunk bounds (OPT_DENSE_PRUNE) */
+    int64_t pruned_vertices; /* CSR: vertices the relaxation view leaves out (OPT_PRUNE_PENDANT) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -2567,6 +2567,15 @@ struct shadowtopo_engine {
     int32_t device = 0;
     GraphDev g{};
     std::vector<void*> graph_allocs;
+    // Relaxation view for compute_rows (OPT_PRUNE_PENDANT): the in-CSR without the pendant
+    // trees that hold no attached vertex (undirected CSR graphs), rebuilt when the attached
+    // set changes; `rg` is the graph the relax rounds and compose use (g for sssp)
+    GraphDev gp{};
+    const GraphDev* rg = nullptr;
+    std::vector<void*> prune_allocs;
+    bool prune_ready = false;
+    int32_t opt_prune = 1;
+    int64_t pruned_vertices = 0;
     // host mirrors for shadowtopo_get_eid, copied from the device on its first call
     std::once_flag mirrors_once;
     int mirrors_rc = 0;
@@ -2872,7 +2881,7 @@ dim3 grid_of(const shadowtopo_engine* eng, int64_t n) {
 // relax rounds for the batch slots [0, nbg) until no vertex changes
 int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = eng->V;
-    const GraphDev& g = eng->g;
+    const GraphDev& g = eng->rg ? *eng->rg : eng->g;
     const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
     if (fused_seed) {
         hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / KL, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
@@ -3323,12 +3332,128 @@ bool is_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
+// Pendant trees (the attached-pair matrix never needs them).  In an
+// undirected graph a non-attached vertex with at most one neighbour lies on no shortest
+// path between two other vertices (entering and leaving it would repeat its neighbour; every
+// latency is > 0), so peeling such vertices repeatedly leaves every attached-pair path, its
+// distance, predecessor chain, hops and reliability as they were.  The relaxation view gp is
+// the in-CSR restricted to the remaining vertices (rows of peeled vertices empty, arcs from
+// them dropped, row order kept): their state is never activated, read or written.  Ties the
+// peeled vertices could raise are the degenerate d(u) == d(v) kind at their attachment
+// vertex, which igraph resolves in favour of the core (the attachment vertex is popped
+// first), so only flags that were conservative disappear; the heap-exact replay keeps the
+// full graph.  C5: 24 % of the vertices, 11 % of the arcs.
+int ensure_mirrors(shadowtopo_engine* eng);
+
+int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
+    if (eng->prune_ready || !eng->opt_prune || eng->dense || (eng->flags & SHADOWTOPO_F_DIRECTED) ||
+        (eng->flags & SHADOWTOPO_F_COMPLETE) || eng->n_arcs == 0)
+        return SHADOWTOPO_OK;
+    int rc;
+    if ((rc = ensure_mirrors(eng))) return rc;
+    const int32_t V = eng->V;
+    const int64_t M = eng->n_arcs;
+    const std::vector<int64_t>& ptr = eng->h_in_ptr;
+    const std::vector<int32_t>& src = eng->h_in_src;
+    // peel: degree = distinct neighbours (the in-CSR merges parallel edges and drops loops)
+    std::vector<uint8_t> keep((size_t)V, 1), att((size_t)V, 0);
+    for (int32_t a : eng->h_attached) att[a] = 1;
+    std::vector<int32_t> deg((size_t)V), stack;
+    for (int32_t v = 0; v < V; ++v) {
+        deg[v] = (int32_t)(ptr[v + 1] - ptr[v]);
+        if (deg[v] <= 1 && !att[v]) stack.push_back(v);
+    }
+    int64_t peeled = 0;
+    while (!stack.empty()) {
+        const int32_t x = stack.back();
+        stack.pop_back();
+        if (!keep[x]) continue;
+        keep[x] = 0;
+        ++peeled;
+        for (int64_t e = ptr[x]; e < ptr[x + 1]; ++e) {
+            const int32_t y = src[e];
+            if (keep[y] && --deg[y] <= 1 && !att[y]) stack.push_back(y);
+        }
+    }
+    eng->pruned_vertices = peeled;
+    if (peeled == 0) {  // nothing to drop: relax over g (and do not peel again for this set)
+        eng->gp = eng->g;
+        eng->prune_ready = true;
+        return SHADOWTOPO_OK;
+    }
+    // the filtered arrays, row order kept, with the builder's padding arcs at the end
+    std::vector<double> w((size_t)M), r((size_t)M);
+    std::vector<float> w32((size_t)M);
+    HIP_TRY(hipMemcpy(w.data(), eng->g.in_w, 8 * (size_t)M, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(w32.data(), eng->g.in_w32, 4 * (size_t)M, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(r.data(), eng->g.in_r, 8 * (size_t)M, hipMemcpyDeviceToHost));
+    std::vector<int64_t> nptr((size_t)V + 1, 0);
+    std::vector<int32_t> nsrc, neid;
+    std::vector<double> nw, nr;
+    std::vector<float> nw32;
+    nsrc.reserve((size_t)M);
+    for (int32_t v = 0; v < V; ++v) {
+        if (keep[v])
+            for (int64_t e = ptr[v]; e < ptr[v + 1]; ++e)
+                if (keep[src[e]]) {
+                    nsrc.push_back(src[e]);
+                    nw.push_back(w[e]);
+                    nw32.push_back(w32[e]);
+                    nr.push_back(r[e]);
+                    neid.push_back(eng->h_in_eid[e]);
+                }
+        nptr[v + 1] = (int64_t)nsrc.size();
+    }
+    for (int k = 0; k < CSR_PAD; ++k) {  // graph_build's k_pad
+        nsrc.push_back(0);
+        nw.push_back(std::numeric_limits<double>::infinity());
+        nw32.push_back(std::numeric_limits<float>::infinity());
+        nr.push_back(0.0);
+        neid.push_back(-1);
+    }
+    for (void* p : eng->prune_allocs) (void)hipFree(p);
+    eng->prune_allocs.clear();
+    GraphDev gp = eng->g;
+    int64_t* d_ptr = nullptr;
+    int32_t *d_src = nullptr, *d_eid = nullptr;
+    double *d_w = nullptr, *d_r = nullptr;
+    float* d_w32 = nullptr;
+    const size_t na = nsrc.size();
+    if ((rc = dev_alloc(eng->prune_allocs, (void**)&d_ptr, 8 * ((size_t)V + 1))) ||
+        (rc = dev_alloc(eng->prune_allocs, (void**)&d_src, 4 * na)) ||
+        (rc = dev_alloc(eng->prune_allocs, (void**)&d_eid, 4 * na)) ||
+        (rc = dev_alloc(eng->prune_allocs, (void**)&d_w, 8 * na)) ||
+        (rc = dev_alloc(eng->prune_allocs, (void**)&d_r, 8 * na)) ||
+        (rc = dev_alloc(eng->prune_allocs, (void**)&d_w32, 4 * na)))
+        return rc;
+    HIP_TRY(hipMemcpy(d_ptr, nptr.data(), 8 * ((size_t)V + 1), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_src, nsrc.data(), 4 * na, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_eid, neid.data(), 4 * na, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_w, nw.data(), 8 * na, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_r, nr.data(), 8 * na, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_w32, nw32.data(), 4 * na, hipMemcpyHostToDevice));
+    gp.in_ptr = d_ptr;
+    gp.in_src = d_src;
+    gp.in_eid = d_eid;
+    gp.in_w = d_w;
+    gp.in_r = d_r;
+    gp.in_w32 = d_w32;
+    gp.out_ptr = d_ptr;  // undirected: out-neighbours = in-neighbours
+    gp.out_dst = d_src;
+    eng->gp = gp;
+    eng->prune_ready = true;
+    (void)s;
+    return SHADOWTOPO_OK;
+}
+
 int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
                       uint32_t* hops, uint8_t* kind, int32_t mem, hipStream_t s) {
     const int32_t A = eng->A;
     const bool complete = (eng->flags & SHADOWTOPO_F_COMPLETE) != 0;
     int rc;
     if ((rc = ensure_self(eng, s))) return rc;
+    if ((rc = ensure_pruned(eng, s))) return rc;
+    eng->rg = eng->prune_ready ? &eng->gp : &eng->g;  // back to g for sssp (shadowtopo_sssp)
     const int32_t nb = default_nb(eng, row_end - row_begin);
     if ((rc = ensure_batches(eng, nb))) return rc;
     const int32_t group = nb * KL;
@@ -3407,7 +3532,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         }
         auto t0 = std::chrono::steady_clock::now();
         if (A > 0) {
-            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(256), 0, s, eng->g, eng->pools,
+            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(256), 0, s, *eng->rg, eng->pools,
                                eng->d_attached, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
                                eng->d_self_kind, dl, dr, dh, dk, row_base);
             HIP_TRY(hipGetLastError());
@@ -3679,6 +3804,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->own_stream) (void)hipStreamSynchronize(eng->own_stream);
     free_batches(eng);
     for (void* p : eng->graph_allocs) (void)hipFree(p);
+    for (void* p : eng->prune_allocs) (void)hipFree(p);
     for (void* p : eng->rp_allocs) (void)hipFree(p);
     if (eng->d_attached) (void)hipFree(eng->d_attached);
     if (eng->d_self_lat) (void)hipFree(eng->d_self_lat);
@@ -3713,6 +3839,12 @@ int shadowtopo_set_attached(shadowtopo_engine* eng, const int32_t* attached, int
         if (attached[i] < 0 || attached[i] >= eng->V) return fail(SHADOWTOPO_EINVAL, "attached[%d] out of range", i);
     HIP_TRY(hipSetDevice(eng->device));
     HIP_TRY(hipStreamSynchronize(eng->own_stream));
+    // the same list again (the shim sets it before every computation): keep the self paths,
+    // the source order and the relaxation view
+    if (eng->d_attached && count == eng->A && std::equal(attached, attached + count, eng->h_attached.begin()))
+        return SHADOWTOPO_OK;
+    eng->prune_ready = false;
+    eng->rg = nullptr;
     if (eng->d_attached) (void)hipFree(eng->d_attached);
     if (eng->d_self_lat) (void)hipFree(eng->d_self_lat);
     if (eng->d_self_rel) (void)hipFree(eng->d_self_rel);
@@ -3791,6 +3923,14 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");
             eng->opt_dense_seed = (int32_t)value;
             return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_PRUNE_PENDANT:
+            if (value < 0 || value > 1) return fail(SHADOWTOPO_EINVAL, "prune must be 0 or 1");
+            if (eng->opt_prune != (int32_t)value) {
+                eng->opt_prune = (int32_t)value;
+                eng->prune_ready = false;
+                eng->rg = nullptr;
+            }
+            return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_GRID_X:
             if (value < 8 || value % 8 || value > ((int64_t)1 << 23))
                 return fail(SHADOWTOPO_EINVAL, "grid x limit must be a multiple of 8 in [8, 2^23]");
@@ -3858,6 +3998,7 @@ int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_so
             rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
             break;
         }
+        eng->rg = &eng->g;  // full rows: every vertex, the unpruned graph
         if ((rc = run_rounds(eng, 1, s))) break;
         hipLaunchKernelGGL(k_extract, dim3((eng->V + 255) / 256, n), dim3(256), 0, s, eng->g, eng->pools, n,
                            d_dist, d_pred, d_hops, d_tie);
@@ -3897,6 +4038,7 @@ void shadowtopo_host_free(void* p) {
 int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out) {
     if (!eng || !out) return fail(SHADOWTOPO_EINVAL, "NULL argument");
     *out = eng->st;
+    out->pruned_vertices = eng->prune_ready ? eng->pruned_vertices : 0;
     return SHADOWTOPO_OK;
 }
 

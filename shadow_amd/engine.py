@@ -44,6 +44,7 @@ OPT_DENSE_PRUNE = 12
 OPT_HBM_SHARE = 13
 OPT_WORKLIST = 14
 OPT_GRID_X = 15
+OPT_PRUNE_PENDANT = 16
 CSR_DELTA = 0  # fold changed in-neighbours into the recorded state, f64 (cross-check)
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (cross-check)
 CSR_FILTERED = 2  # changed tails only: round-stamped f32 keys, f64 settle (k_relax_st)
@@ -76,6 +77,7 @@ class Stats(ctypes.Structure):
         ("full_batches", ctypes.c_int64), ("full_changes", ctypes.c_int64), ("relax_batches", ctypes.c_int64),
         ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double), ("sparse_deltas", ctypes.c_int64),
         ("self_ms", ctypes.c_double), ("self_paths", ctypes.c_int64), ("pruned_deltas", ctypes.c_int64),
+        ("pruned_vertices", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -131,3 +131,40 @@ def test_source_order_same_matrix(case):
         assert visits[1] < 0.6 * visits[0], visits
     st = compare(g, layout="csr")  # default order against the oracle
     assert st["dense"] == 0
+
+
+@pytest.mark.parametrize("case", ["sparse", "tree_heavy", "vloss_prefer", "int_ties", "chung_lu"])
+def test_pendant_tree_pruning_same_results(case):
+    """OPT_PRUNE_PENDANT (default): the relaxation view without the pendant trees that hold
+    no attached vertex gives bit-identical attached-pair matrices (latency, reliability,
+    hops, kind) to the full graph, and the oracle's; full sssp rows still cover every
+    vertex"""
+    if case == "sparse":
+        g = synth.random_sparse(V=500, avg_deg=2.5, seed=61, A=120)
+    elif case == "tree_heavy":
+        g = synth.random_sparse(V=700, avg_deg=2.1, seed=62, A=90, loops=False)
+    elif case == "vloss_prefer":
+        rng = np.random.default_rng(8)
+        g = synth.random_sparse(V=400, avg_deg=2.5, seed=63, A=100, vloss=np.where(rng.random(400) < 0.5, 0.03, np.nan))
+        g.prefer_direct = True
+    elif case == "int_ties":
+        g = synth.random_sparse(V=450, avg_deg=2.4, seed=64, A=110, int_lat=True)
+    else:
+        g = synth.chung_lu(V=20_000, A=700)
+    mats = []
+    for prune in (0, 1):
+        eng = E.Engine.from_synth(g, layout="csr")
+        eng.set_option(E.OPT_PRUNE_PENDANT, prune)
+        eng.set_attached(g.attached)
+        mats.append(eng.compute_rows(want_kind=True))
+        st = eng.stats()
+        assert (st["pruned_vertices"] > 0) == bool(prune), st["pruned_vertices"]
+        if prune:
+            d, _, _, _ = eng.sssp(np.asarray(g.attached[:3], np.int32))
+            assert np.isfinite(d).sum() > 0
+        eng.close()
+    for x, y in zip(*mats):
+        assert np.array_equal(x.view(np.uint8) if x.dtype == np.float64 else x,
+                              y.view(np.uint8) if y.dtype == np.float64 else y)
+    if case != "chung_lu":
+        compare(g, layout="csr")
