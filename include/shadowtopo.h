@@ -106,6 +106,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               pendant trees that hold no attached vertex (peeled non-attached
                                               vertices with one neighbour; they lie on no attached-pair path);
                                               0 = every vertex. Results are identical. */
+#define SHADOWTOPO_OPT_DEVICE_ROUNDS 17   /* CSR FULL worklist rounds: 1 (default) = driven from the device (item
+                                              counts read back once per 8 rounds) when batches x vertices <= 4 Mi,
+                                              2 = always, 0 = never (one host read-back per round). Results are
+                                              identical. */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
                                               engine may take (default 1000); engines sharing one device split it */
 

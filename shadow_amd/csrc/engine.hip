@@ -516,6 +516,72 @@ __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in
     if (lane == 0) B.act(parity)[v] = 0;
 }
 
+// Device-driven worklist rounds (graphs whose batches x vertices fit OPT_DEVICE_ROUNDS'
+// bound, e.g. C3): the round's item count never visits the host.  k_scan_wl turns the
+// per-batch counts of k_compact into the prefix the worklist kernel reads, and logs the
+// total per round (tlog[round]: the host reads a block of rounds at once and stops at the
+// first empty one, which is convergence: no change, no activation).
+__global__ __launch_bounds__(256) void k_scan_wl(const uint32_t* __restrict__ wlcnt, int32_t nb,
+                                                 int64_t* __restrict__ prefix, int64_t* __restrict__ tlog,
+                                                 int32_t round) {
+    __shared__ int64_t sc[256];
+    constexpr int PER = 4;  // nb <= 1024
+    int64_t v[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int32_t b = threadIdx.x * PER + k;
+        v[k] = b < nb ? (int64_t)wlcnt[b] : 0;
+        sum += v[k];
+    }
+    sc[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const int64_t add = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0;
+        __syncthreads();
+        sc[threadIdx.x] += add;
+        __syncthreads();
+    }
+    int64_t run = sc[threadIdx.x] - sum;  // items before this thread's batches
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int32_t b = threadIdx.x * PER + k;
+        if (b < nb) prefix[b] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 255) {
+        prefix[nb] = sc[255];
+        tlog[round] = sc[255];
+    }
+}
+
+// k_relax_wl with a fixed grid (G blocks, G / 8 per XCD) that loops over the round's items:
+// XCD x (block % 8) takes the slice [x*S, (x+1)*S) of the batch-major list, S = ceil(T / 8),
+// its waves striding through it; an empty round's blocks exit at once
+__global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                   const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                                   const int64_t* __restrict__ out_ptr,
+                                                   const int32_t* __restrict__ out_dst, Pools pools, int32_t parity,
+                                                   const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
+                                                   int32_t nb, int32_t* __restrict__ cnt,
+                                                   unsigned long long* __restrict__ prof) {
+    const int64_t T = prefix[nb];
+    if (T == 0) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t S = (T + 7) / 8;
+    const int64_t x = blockIdx.x & 7;
+    const int64_t waves_per_xcd = (int64_t)(gridDim.x >> 3) * 4;
+    for (int64_t j = (int64_t)(blockIdx.x >> 3) * 4 + wave; j < S; j += waves_per_xcd) {
+        const int64_t i = x * S + j;
+        if (i >= T) break;
+        const int32_t b = __builtin_amdgcn_readfirstlane(wl_batch(prefix, nb, i, lane));
+        const int32_t v = __builtin_amdgcn_readfirstlane(wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x);
+        const BatchDev B = batch_view(pools, b);
+        relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+        if (lane == 0) B.act(parity)[v] = 0;
+    }
+}
+
 // CSR delta round (default for sparse graphs).  Same pull schedule as k_relax (one wave per
 // active destination v, in-arcs in chunks of 8), but a lane only looks at in-neighbours u
 // whose state changed for ITS source in the previous round (chm: per-vertex 64-bit lane
@@ -2609,6 +2675,11 @@ struct shadowtopo_engine {
     uint32_t* h_wlcnt = nullptr;  // pinned [nb]
     int64_t* d_wlpre = nullptr;   // [nb + 1] item prefix, uploaded per round
     int64_t* h_wlpre = nullptr;   // pinned
+    int64_t* d_tlog = nullptr;    // device-driven rounds: items per round [max rounds + 1]
+    int64_t* h_tlog = nullptr;    // pinned copy of a block of rounds
+    int64_t tlog_n = 0;
+    int32_t opt_device_rounds = 1;  // 0 never, 1 when batches x vertices <= dev_rounds_max, 2 always
+    int64_t dev_rounds_max = (int64_t)4 << 20;
     // staging for host outputs
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -2641,6 +2712,7 @@ struct shadowtopo_engine {
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
+    std::vector<hipEvent_t> ev_dev;  // device-driven rounds: one pair per round of a block
     shadowtopo_stats st{};
 };
 
@@ -2925,6 +2997,80 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const bool masked = !eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_MASKED && eng->pools.cm && eng->d_wl;
     const bool use_wl = masked || (!eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL && eng->opt_worklist && eng->d_wl);
     const int32_t ncb = (V + WL_SPAN - 1) / WL_SPAN;
+    // small graphs (C3: 110 batches x 7000 vertices): rounds driven from the device, the
+    // host reading the per-round item counts once per block of DEV_K rounds instead of
+    // synchronising on every round (a round of C3 is 0.1 ms of kernel and ~0.05 ms of
+    // launch + read-back otherwise)
+    const bool dev_rounds = !masked && use_wl && eng->opt_worklist == 1 && nbg <= 1024 &&
+                            (eng->opt_device_rounds == 2 ||
+                             (eng->opt_device_rounds == 1 && (int64_t)nbg * V <= eng->dev_rounds_max));
+    if (dev_rounds) {
+        constexpr int DEV_K = 8;
+        const int64_t cap = max_rounds + DEV_K + 2;
+        if (eng->tlog_n < cap) {
+            if (eng->d_tlog) (void)hipFree(eng->d_tlog);
+            if (eng->h_tlog) (void)hipHostFree(eng->h_tlog);
+            eng->d_tlog = nullptr;
+            eng->h_tlog = nullptr;
+            eng->tlog_n = 0;
+            HIP_TRY(hipMalloc((void**)&eng->d_tlog, sizeof(int64_t) * cap));
+            HIP_TRY(hipHostMalloc((void**)&eng->h_tlog, sizeof(int64_t) * cap, hipHostMallocDefault));
+            eng->tlog_n = cap;
+        }
+        if (eng->opt_timing && eng->ev_dev.empty()) {
+            eng->ev_dev.resize(2 * DEV_K);
+            for (auto& e : eng->ev_dev) HIP_TRY(hipEventCreate(&e));
+        }
+        const uint32_t G = 8 * 256;  // fixed grid: 8192 waves, the chip at occupancy 8
+        HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
+        hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, 0, eng->d_wl,
+                           eng->d_wlcnt, g.in_ptr);
+        hipLaunchKernelGGL(k_scan_wl, dim3(1), dim3(256), 0, s, eng->d_wlcnt, nbg, eng->d_wlpre, eng->d_tlog, 0);
+        HIP_TRY(hipGetLastError());
+        for (int64_t r0 = 0;; r0 += DEV_K) {
+            if (r0 > max_rounds)
+                return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds", (long long)max_rounds);
+            for (int64_t round = r0; round < r0 + DEV_K; ++round) {
+                int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;  // written, not read back
+                if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0)], s));
+                hipLaunchKernelGGL(k_relax_wlp, dim3(G), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r, g.out_ptr,
+                                   g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl, eng->d_wlpre, nbg, cnt_cur,
+                                   eng->d_prof);
+                if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0) + 1], s));
+                HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
+                hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
+                                   (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);
+                hipLaunchKernelGGL(k_scan_wl, dim3(1), dim3(256), 0, s, eng->d_wlcnt, nbg, eng->d_wlpre, eng->d_tlog,
+                                   (int32_t)(round + 1));
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipMemcpyAsync(eng->h_tlog + r0, eng->d_tlog + r0, sizeof(int64_t) * (DEV_K + 1),
+                                   hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            bool done = false;
+            for (int64_t round = r0; round < r0 + DEV_K; ++round) {
+                const int64_t T = eng->h_tlog[round];
+                if (T == 0) {  // nothing active: converged (the rest of the block were no-ops)
+                    done = true;
+                    break;
+                }
+                eng->st.rounds++;
+                eng->st.relax_launches++;
+                eng->st.wl_launches++;
+                eng->st.relax_batches += nbg;
+                float ms = 0;
+                if (eng->opt_timing) {
+                    HIP_TRY(hipEventElapsedTime(&ms, eng->ev_dev[2 * (round - r0)], eng->ev_dev[2 * (round - r0) + 1]));
+                    eng->st.relax_ms += ms;
+                    eng->st.wl_ms += ms;
+                }
+                if (eng->trace_rounds)
+                    fprintf(stderr, "[shadowtopo] round %lld batches %d items %lld (device-driven) %.3f ms\n",
+                            (long long)round, nbg, (long long)T, ms);
+            }
+            if (done) break;
+        }
+    } else {
     if (use_wl) {
         HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
         hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, 0, eng->d_wl,
@@ -3109,6 +3255,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         if (eng->dense && eng->opt_profile) eng->st.changes += changed;  // changed (vertex, source) pairs
         if (changed == 0) break;
     }
+    }  // host-driven rounds
     if (eng->d_prof) {
         std::vector<unsigned long long> h((size_t)16 * nbg);
         HIP_TRY(hipMemcpy(h.data(), eng->d_prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
@@ -3802,6 +3949,9 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->device);
     if (eng->own_stream) (void)hipStreamSynchronize(eng->own_stream);
+    if (eng->d_tlog) (void)hipFree(eng->d_tlog);
+    if (eng->h_tlog) (void)hipHostFree(eng->h_tlog);
+    for (auto e : eng->ev_dev) (void)hipEventDestroy(e);
     free_batches(eng);
     for (void* p : eng->graph_allocs) (void)hipFree(p);
     for (void* p : eng->prune_allocs) (void)hipFree(p);
@@ -3922,6 +4072,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_SEED:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense seed must be 0 or 1");
             eng->opt_dense_seed = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DEVICE_ROUNDS:
+            if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "device rounds must be 0, 1 or 2");
+            eng->opt_device_rounds = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_PRUNE_PENDANT:
             if (value < 0 || value > 1) return fail(SHADOWTOPO_EINVAL, "prune must be 0 or 1");

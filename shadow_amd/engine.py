@@ -45,6 +45,7 @@ OPT_HBM_SHARE = 13
 OPT_WORKLIST = 14
 OPT_GRID_X = 15
 OPT_PRUNE_PENDANT = 16
+OPT_DEVICE_ROUNDS = 17
 CSR_DELTA = 0  # fold changed in-neighbours into the recorded state, f64 (cross-check)
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (cross-check)
 CSR_FILTERED = 2  # changed tails only: round-stamped f32 keys, f64 settle (k_relax_st)

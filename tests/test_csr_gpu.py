@@ -168,3 +168,14 @@ def test_pendant_tree_pruning_same_results(case):
                               y.view(np.uint8) if y.dtype == np.float64 else y)
     if case != "chung_lu":
         compare(g, layout="csr")
+
+
+@pytest.mark.parametrize("case", ["sparse", "directed", "ties", "vloss_prefer", "multigraph"])
+def test_device_driven_rounds_same_results(case):
+    """OPT_DEVICE_ROUNDS: worklist rounds driven from the device (item counts read back once
+    per block of rounds, k_scan_wl / k_relax_wlp) against host-driven rounds (one read-back
+    per round) and the oracle, with several batch groups"""
+    g = _case(case)
+    st1 = compare(g, layout="csr", csr_variant=E.CSR_FULL, device_rounds=2, batches_in_flight=2)
+    st0 = compare(g, layout="csr", csr_variant=E.CSR_FULL, device_rounds=0, batches_in_flight=2)
+    assert st1["rounds"] == st0["rounds"] and st1["wl_launches"] == st1["relax_launches"]
