@@ -1661,11 +1661,12 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
 }
 
 // Dense round 0 in one pass: the state k_init + k_seed + k_seed_dense would leave, with
-// every (v, source) entry written once.  A block owns 64 destinations [v0, v0+64) of one
-// batch; the batch's source rows W[s][v0..v0+63] are loaded coalesced (lane = v), staged in
+// every (v, source) entry written once.  A block owns 32 destinations [v0, v0+32) of one
+// batch; the batch's source rows W[s][v0..v0+31] are loaded coalesced (256-byte segments), staged in
 // LDS and read back transposed (lane = source), so the state rows [v][64] are written
 // coalesced too.  Pad rows v >= V get the unreached state.
-constexpr int SEED_ST = KL + 1;  // LDS row stride: the transposed reads spread over the banks
+constexpr int SEED_T = 32;             // destinations per block (64 needed 50 KB of LDS: 3 blocks per CU)
+constexpr int SEED_ST = SEED_T + 1;    // LDS row stride: the transposed reads spread over the banks
 __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__ W, const int32_t* __restrict__ WI,
                                                       int32_t Vp, const double* __restrict__ in_r,
                                                       const double* __restrict__ vfac, Pools pools, int32_t V) {
@@ -1674,22 +1675,24 @@ __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int32_t v0 = blockIdx.x * KL;
-    for (int j = wave; j < KL; j += 4) {
+    const int32_t v0 = blockIdx.x * SEED_T;
+    // the 64 sources' rows over this block's destinations: 32-element (256-byte) segments
+    for (int e = threadIdx.x; e < KL * SEED_T; e += 256) {
+        const int j = e / SEED_T, x = e % SEED_T;
         const int32_t s = B.srcv[j];
         double w = dinf();
         int32_t a = -1;
-        if (s >= 0 && v0 + lane < V) {
-            w = W[(size_t)s * Vp + v0 + lane];
-            a = WI[(size_t)s * Vp + v0 + lane];
+        if (s >= 0 && v0 + x < V) {
+            w = W[(size_t)s * Vp + v0 + x];
+            a = WI[(size_t)s * Vp + v0 + x];
         }
-        sw[j * SEED_ST + lane] = w;
-        si[j * SEED_ST + lane] = a;
+        sw[j * SEED_ST + x] = w;
+        si[j * SEED_ST + x] = a;
     }
     __syncthreads();
     const int32_t sv = B.srcv[lane];
     const double rs = sv >= 0 ? vfac[sv] : 0.0;  // R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445)
-    for (int x = wave; x < KL; x += 4) {
+    for (int x = wave; x < SEED_T; x += 4) {
         const int32_t v = v0 + x;
         const double w = sw[lane * SEED_ST + x];
         const int32_t arc = si[lane * SEED_ST + x];
@@ -2959,7 +2962,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const GraphDev& g = eng->rg ? *eng->rg : eng->g;
     const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
     if (fused_seed) {
-        hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / KL, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
+        hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / SEED_T, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
                            g.in_r, g.vfac, eng->pools, V);
         HIP_TRY(hipGetLastError());
     } else {
