@@ -51,9 +51,9 @@ def main():
     n = int(round((bench["warmup"] + bench["steps"]) * rf["launches_per_step"]))
     # label-correcting rounds read values that other waves of the same round may already have
     # updated, so a step can converge a round earlier or later from one run to the next: each
-    # pass averages over its own last dispatches (at most n; one short of n is accepted)
+    # pass averages over its own last dispatches (at most n; up to a tenth fewer is accepted)
     f, w, s = (dispatches(d, kre)[-n:] for d in (fdir, wdir, sdir))
-    if min(len(f), len(w), len(s)) < max(1, n - max(2, n // 40)):
+    if min(len(f), len(w), len(s)) < max(1, n - max(2, n // 10)):
         raise SystemExit(f"expected {n} dispatches matching {kre}, found {len(f)}/{len(w)}/{len(s)}")
     fetch = sum(v["FETCH_SIZE"] for v in f) * 1024 * 2 / len(f)
     write = sum(v["WRITE_SIZE"] for v in w) * 1024 / len(w)
