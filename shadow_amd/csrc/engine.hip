@@ -2327,7 +2327,10 @@ __device__ void walk_tree(const GraphDev& g, const BatchDev& B, int lane, int32_
     o.rel = rel;
 }
 
-__global__ __launch_bounds__(256) void k_compose(GraphDev g, Pools pools,
+// 512 threads: 8 targets per wave instead of 16 (the per-lane pair values live in registers
+// until the transposes: 132 VGPRs at 16, occupancy 3)
+constexpr int COMPOSE_T = 512;
+__global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
                                                  const int32_t* __restrict__ attached, int32_t A,
                                                  const double* __restrict__ self_lat,
                                                  const double* __restrict__ self_rel,
@@ -2340,13 +2343,14 @@ __global__ __launch_bounds__(256) void k_compose(GraphDev g, Pools pools,
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int32_t t0 = blockIdx.x * 64;
     const int32_t s = B.srcv[lane];
-    double vl[16], vr[16];
-    uint32_t vh[16];
-    uint8_t vk[16];
+    constexpr int PT = 64 / (COMPOSE_T / 64);  // targets per wave
+    double vl[PT], vr[PT];
+    uint32_t vh[PT];
+    uint8_t vk[PT];
     bool taint_any = false;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int32_t ti = t0 + wave * 16 + i;
+    for (int i = 0; i < PT; ++i) {
+        const int32_t ti = t0 + wave * PT + i;
         PairOut o;
         o.lat = -1.0;
         o.rel = -1.0;
@@ -2382,18 +2386,18 @@ __global__ __launch_bounds__(256) void k_compose(GraphDev g, Pools pools,
     const int32_t nrow = 64;
     // lat
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sd[lane * 65 + wave * 16 + i] = vl[i];
+    for (int i = 0; i < PT; ++i) sd[lane * 65 + wave * PT + i] = vl[i];
     __syncthreads();
-    for (int k = threadIdx.x; k < nrow * 64; k += 256) {
+    for (int k = threadIdx.x; k < nrow * 64; k += COMPOSE_T) {
         const int j = k >> 6, tl = k & 63;
         const int32_t r = B.row[j], ti = t0 + tl;
         if (r >= 0 && ti < A) out_lat[(size_t)(r - row_base) * A + ti] = sd[j * 65 + tl];
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sd[lane * 65 + wave * 16 + i] = vr[i];
+    for (int i = 0; i < PT; ++i) sd[lane * 65 + wave * PT + i] = vr[i];
     __syncthreads();
-    for (int k = threadIdx.x; k < nrow * 64; k += 256) {
+    for (int k = threadIdx.x; k < nrow * 64; k += COMPOSE_T) {
         const int j = k >> 6, tl = k & 63;
         const int32_t r = B.row[j], ti = t0 + tl;
         if (r >= 0 && ti < A) out_rel[(size_t)(r - row_base) * A + ti] = sd[j * 65 + tl];
@@ -2401,12 +2405,12 @@ __global__ __launch_bounds__(256) void k_compose(GraphDev g, Pools pools,
     __syncthreads();
     uint32_t* su = reinterpret_cast<uint32_t*>(sd);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        su[lane * 65 + wave * 16 + i] = vh[i];
-        su[64 * 65 + lane * 65 + wave * 16 + i] = vk[i];
+    for (int i = 0; i < PT; ++i) {
+        su[lane * 65 + wave * PT + i] = vh[i];
+        su[64 * 65 + lane * 65 + wave * PT + i] = vk[i];
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < nrow * 64; k += 256) {
+    for (int k = threadIdx.x; k < nrow * 64; k += COMPOSE_T) {
         const int j = k >> 6, tl = k & 63;
         const int32_t r = B.row[j], ti = t0 + tl;
         if (r >= 0 && ti < A) {
@@ -3685,7 +3689,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         }
         auto t0 = std::chrono::steady_clock::now();
         if (A > 0) {
-            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(256), 0, s, *eng->rg, eng->pools,
+            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(COMPOSE_T), 0, s, *eng->rg, eng->pools,
                                eng->d_attached, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
                                eng->d_self_kind, dl, dr, dh, dk, row_base);
             HIP_TRY(hipGetLastError());
