@@ -1929,7 +1929,8 @@ __global__ __launch_bounds__(256) void k_live_chunks(Pools pools, int32_t V, int
 // per load, cost 1.6x this kernel's time: one texture-address cycle per lane.)
 constexpr int SWS = KL + 4;              // LDS row stride (floats) of the staged W32 slab and the thresholds:
                                          // rows r != r' (mod 16) on distinct bank quads
-constexpr int RING_S = KL * (KL / DW);   // one chunk's changed pairs of one wave, at most
+constexpr int RING_S = 512;  // ring segment (int16 entries): a chunk's pairs of one wave (at most 64 x 16) are
+                             // listed and drained 512 at a time -- 46 -> 40 KB of LDS, 4 blocks per CU
 
 constexpr int PR_CHUNKS = 640;  // pruned delta: live-chunk list capacity (dense mode keeps Vp <= 38 730: 606 chunks)
 
@@ -1959,8 +1960,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     constexpr int PF = KL * KL / 4 / (64 * DW);  // float4 of one W32 slab per thread
     __shared__ __attribute__((aligned(16))) float sT[KL * SWS];  // [s][v] thresholds
     __shared__ __attribute__((aligned(16))) float sW[KL * SWS];
-    __shared__ int32_t sP[DW][RING_S];  // (row in chunk << 6) | s
-    __shared__ unsigned long long sM[DW][KL];
+    __shared__ int16_t sP[DW][RING_S];  // (row in chunk << 6) | s
     __shared__ int16_t sL[PR ? PR_CHUNKS : 1];  // PR: the block's live chunks, ascending
     __shared__ int32_t sNL;
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1989,7 +1989,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     const gfloat* W32g = (const gfloat*)W32;
     const bool vok = v < V;
     const double inf = dinf();
-    int32_t* ring = sP[wave];
+    int16_t* ring = sP[wave];
     unsigned long long mine = 0;
 
     if (PR) {
@@ -2137,14 +2137,18 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         pma = chp + (PR ? (more ? urow_n : 0) : un + lane);
         mnext = *pma;
         if (more) fetch(un);
-        if (tot) {
+        for (int base = 0; base < tot; base += RING_S) {  // usually one segment (C2: ~40 pairs)
             unsigned long long mm = m;
+            int q = pos;
             while (mm) {
-                ring[pos++] = (lane << 6) | __builtin_ctzll(mm);
+                if (q >= base && q < base + RING_S) ring[q - base] = (int16_t)((lane << 6) | __builtin_ctzll(mm));
+                ++q;
                 mm &= mm - 1;
             }
             __builtin_amdgcn_wave_barrier();
-            for (int h = 0; h < tot; h += KL) drain(u0, urow, h, tot - h < KL ? tot - h : KL);
+            const int seg = tot - base < RING_S ? tot - base : RING_S;
+            for (int h = 0; h < seg; h += KL) drain(u0, urow, h, seg - h < KL ? seg - h : KL);
+            __builtin_amdgcn_wave_barrier();  // the segment is drained before the next overwrites it
         }
         hold();
         __syncthreads();  // every wave is done with this slab
@@ -2153,6 +2157,10 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         urow = PR ? urow_n : un + lane;
         urow_n = urow_nn;
     }
+    // the waves' change masks, in the thresholds' LDS (every wave is past the walk's last
+    // barrier: nobody reads sT any more)
+    unsigned long long (*sM)[KL] = reinterpret_cast<unsigned long long (*)[KL]>(sT);
+    __syncthreads();
     sM[wave][lane] = mine;
     __syncthreads();
     if (wave == 0) {
