@@ -1660,17 +1660,34 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
     }
 }
 
+// WR[i] = in_r[WI[i]]: the dense reliability factors (0 where there is no arc)
+__global__ __launch_bounds__(256) void k_dense_wr(const int32_t* __restrict__ WI, const double* __restrict__ in_r,
+                                                  double* __restrict__ WR, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int32_t a = WI[i];
+        WR[i] = a >= 0 ? in_r[a] : 0.0;
+    }
+}
+
 // Dense round 0 in one pass: the state k_init + k_seed + k_seed_dense would leave, with
 // every (v, source) entry written once.  A block owns 32 destinations [v0, v0+32) of one
 // batch; the batch's source rows W[s][v0..v0+31] are loaded coalesced (256-byte segments), staged in
 // LDS and read back transposed (lane = source), so the state rows [v][64] are written
 // coalesced too.  Pad rows v >= V get the unreached state.
-constexpr int SEED_T = 32;             // destinations per block (64 needed 50 KB of LDS: 3 blocks per CU)
+// The arcs' reliability factors come from the dense WR table (in_r[WI], built once with the
+// tables): gathered from in_r by arc id they cost one scattered line per (v, source) and
+// C2's seed 0.17 ms per launch against 0.07 ms without them.
+#ifndef SEED_T_EXP
+constexpr int SEED_T = 16;             // destinations per block: 22 KB of LDS, 7 blocks per CU
+#else
+constexpr int SEED_T = SEED_T_EXP;
+#endif
 constexpr int SEED_ST = SEED_T + 1;    // LDS row stride: the transposed reads spread over the banks
 __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__ W, const int32_t* __restrict__ WI,
-                                                      int32_t Vp, const double* __restrict__ in_r,
+                                                      int32_t Vp, const double* __restrict__ WR,
                                                       const double* __restrict__ vfac, Pools pools, int32_t V) {
     __shared__ double sw[KL * SEED_ST];
+    __shared__ double sr[KL * SEED_ST];
     __shared__ int32_t si[KL * SEED_ST];
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int lane = threadIdx.x & 63;
@@ -1680,13 +1697,15 @@ __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__
     for (int e = threadIdx.x; e < KL * SEED_T; e += 256) {
         const int j = e / SEED_T, x = e % SEED_T;
         const int32_t s = B.srcv[j];
-        double w = dinf();
+        double w = dinf(), r = 0.0;
         int32_t a = -1;
         if (s >= 0 && v0 + x < V) {
             w = W[(size_t)s * Vp + v0 + x];
             a = WI[(size_t)s * Vp + v0 + x];
+            r = WR[(size_t)s * Vp + v0 + x];
         }
         sw[j * SEED_ST + x] = w;
+        sr[j * SEED_ST + x] = r;
         si[j * SEED_ST + x] = a;
     }
     __syncthreads();
@@ -1696,6 +1715,7 @@ __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__
         const int32_t v = v0 + x;
         const double w = sw[lane * SEED_ST + x];
         const int32_t arc = si[lane * SEED_ST + x];
+        const double ra = sr[lane * SEED_ST + x];
         const bool own = (v == sv);
         const bool seeded = sv >= 0 && !own && v < V && w < dinf();
         double d = dinf(), r = 0.0, bdu = dinf();
@@ -1709,7 +1729,7 @@ __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__
             d = 0.0 + w;
             d32 = f32_key(d);
             h = 1;
-            r = rs * in_r[arc];
+            r = rs * ra;
             p = arc;
             bdu = 0.0;
         }
@@ -2630,6 +2650,7 @@ struct shadowtopo_engine {
     int32_t dense = 0;
     const double* d_W = nullptr;    // dense mode: [Vp][Vp] arc latency, +inf if none
     const int32_t* d_WI = nullptr;  // dense mode: [Vp][Vp] in-arc index, -1 if none
+    const double* d_WR = nullptr;   // dense mode: [Vp][Vp] in_r of that arc (the seed's reliability factors)
     const float* d_W32 = nullptr;   // dense mode: [Vp][Vp] arc latency rounded down to f32, NaN if none
     uint32_t* d_hitlog = nullptr;   // dense full sweep: per wave, per batch, per 32-row chunk: rows to settle in f64
     size_t hitlog_n = 0;
@@ -2972,10 +2993,10 @@ dim3 grid_of(const shadowtopo_engine* eng, int64_t n) {
 int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = eng->V;
     const GraphDev& g = eng->rg ? *eng->rg : eng->g;
-    const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
+    const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->d_WR && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
     if (fused_seed) {
         hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / SEED_T, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
-                           g.in_r, g.vfac, eng->pools, V);
+                           eng->d_WR, g.vfac, eng->pools, V);
         HIP_TRY(hipGetLastError());
     } else {
         const size_t total = (size_t)eng->Vp * KL;
@@ -3873,7 +3894,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->Vp = (V + 63) / 64 * 64;  // dense tiles of 64 destinations, 32-row LDS chunks
     {
         const double VV = (double)V * (double)V;
-        const bool fits = (double)eng->Vp * eng->Vp * 16.0 <= 24.0e9;
+        const bool fits = (double)eng->Vp * eng->Vp * 24.0 <= 36.0e9;  // W, WR, WI, W32
         if (flags & SHADOWTOPO_F_FORCE_DENSE)
             eng->dense = fits ? 1 : 0;
         else if (flags & SHADOWTOPO_F_FORCE_CSR)
@@ -3908,7 +3929,9 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         double* W = nullptr;
         int32_t* WI = nullptr;
         float* W32 = nullptr;
+        double* WR = nullptr;
         if ((rc = dev_alloc(eng->graph_allocs, (void**)&W, Vp * Vp * sizeof(double))) ||
+            (rc = dev_alloc(eng->graph_allocs, (void**)&WR, Vp * Vp * sizeof(double))) ||
             (rc = dev_alloc(eng->graph_allocs, (void**)&WI, Vp * Vp * sizeof(int32_t))) ||
             (rc = dev_alloc(eng->graph_allocs, (void**)&W32, Vp * Vp * sizeof(float)))) {
             shadowtopo_destroy(eng);
@@ -3917,6 +3940,11 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         hipStream_t bs = nullptr;
         hipError_t e = hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
         if (e == hipSuccess) e = graph_build::build_dense(eng->Vp, gb, W, WI, W32, bs);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_dense_wr, dim3(4096), dim3(256), 0, bs, WI, gb.in_r, WR, Vp * Vp);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamSynchronize(bs);
+        }
         if (bs) (void)hipStreamDestroy(bs);
         if (e != hipSuccess) {
             shadowtopo_destroy(eng);
@@ -3924,6 +3952,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         }
         eng->d_W = W;
         eng->d_WI = WI;
+        eng->d_WR = WR;
         eng->d_W32 = W32;
     }
     // the arc heads were needed only for the dense tables
