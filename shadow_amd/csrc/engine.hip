@@ -2745,6 +2745,7 @@ struct shadowtopo_engine {
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
+    int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
     int32_t* d_nlive = nullptr;        // [nb_cap]
@@ -3640,7 +3641,28 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     if ((rc = ensure_self(eng, s))) return rc;
     if ((rc = ensure_pruned(eng, s))) return rc;
     eng->rg = eng->prune_ready ? &eng->gp : &eng->g;  // back to g for sssp (shadowtopo_sssp)
-    const int32_t nb = default_nb(eng, row_end - row_begin);
+    // host destinations: rows are composed into device staging and copied out per group;
+    // into pinned (page-locked) host memory -- shadowtopo_host_alloc, as the topology shim
+    // allocates its matrix -- the copy of group g runs on the copy stream behind group
+    // g + 1's relaxation (two staging slots), into pageable memory it is a synchronous copy
+    const bool pinned_out = mem == SHADOWTOPO_MEM_HOST && is_pinned(lat) && is_pinned(rel) &&
+                            (!hops || is_pinned(hops)) && (!kind || is_pinned(kind));
+    int32_t nb = default_nb(eng, row_end - row_begin);
+    {
+        // a computation that fits one group would copy all its rows after its last round.
+        // Where the copy outweighs the relaxation it is cut into opt_host_split groups, so
+        // every group's copy but the last runs behind the next group's rounds.  The test is a
+        // row's bytes against the graph's arcs (what a source's rounds walk), calibrated on one
+        // MI355X: C3 (7000 x 17 B per row, 139 k arcs: 0.86 B per arc; 833 MB, 15 ms of PCIe
+        // against 8 ms of rounds) 22.4 -> 19.5 ms in 4 groups (8: 26.4); C4 (0.21 B per arc)
+        // 186 -> 207 ms in 4 groups, its smaller groups' rounds cost more than the copy
+        const int32_t need = (row_end - row_begin + KL - 1) / KL;
+        const double row_bytes = (double)A * (16 + (hops ? 4 : 0) + (kind ? 1 : 0));
+        const double bytes = row_bytes * (row_end - row_begin);
+        if (pinned_out && eng->opt_host_split > 1 && nb >= need && bytes >= 64.0e6 &&
+            row_bytes >= 0.5 * (double)eng->n_arcs)
+            nb = std::max(1, (need + eng->opt_host_split - 1) / eng->opt_host_split);
+    }
     if ((rc = ensure_batches(eng, nb))) return rc;
     const int32_t group = nb * KL;
     if ((rc = ensure_vperm(eng, s))) return rc;
@@ -3655,12 +3677,6 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     double *dl = lat, *dr = rel;
     uint32_t* dh = hops;
     uint8_t* dk = kind;
-    // host destinations: rows are composed into device staging and copied out per group;
-    // into pinned (page-locked) host memory -- shadowtopo_host_alloc, as the topology shim
-    // allocates its matrix -- the copy of group g runs on the copy stream behind group
-    // g + 1's relaxation (two staging slots), into pageable memory it is a synchronous copy
-    const bool pinned_out = mem == SHADOWTOPO_MEM_HOST && is_pinned(lat) && is_pinned(rel) &&
-                            (!hops || is_pinned(hops)) && (!kind || is_pinned(kind));
     const int nslots = pinned_out && row_end - row_begin > group ? 2 : 1;
     const size_t slot_bytes = ((size_t)group * A * (8 + 8 + (hops ? 4 : 0) + (kind ? 1 : 0)) + 255) & ~(size_t)255;
     if (mem == SHADOWTOPO_MEM_HOST) {
@@ -3981,6 +3997,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (dl && dl[0] >= '0' && dl[0] <= '2') eng->opt_delta_live = dl[0] - '0';
         const char* dd = getenv("SHADOWTOPO_DELTA_LIVE_DIV");
         if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
+        const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
+        if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
     }
     eng->st.n_vertices = V;
     eng->st.n_edges = n_edges;

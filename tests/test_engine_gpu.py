@@ -352,6 +352,31 @@ def test_pinned_host_rows_pipelined(layout):
     assert_bitexact("hops", hops, hops_o[100:A - 30])
 
 
+def test_pinned_host_rows_split_into_groups():
+    """A computation that fits one batch group but whose rows outweigh its relaxation (row
+    bytes >= half the graph's arcs, past 64 MB) is cut into host groups
+    (opt_host_split = 4), so its copies overlap the later groups' rounds: 2200 sources of a
+    k-NN graph (82 MB of rows, 35 batches -> 4 groups).  Bit-identical to the pageable path,
+    which computes in one group (fewer rounds)."""
+    g = synth.knn_geographic(V=2200, k=8, seed=12)
+    eng = E.Engine.from_synth(g, layout="csr")
+    eng.set_attached(g.attached)
+    A = len(g.attached)
+    lat = E.pinned_empty((A, A), np.float64)
+    rel = E.pinned_empty((A, A), np.float64)
+    kind = E.pinned_empty((A, A), np.uint8)
+    r0 = eng.stats()["rounds"]
+    eng.compute_rows_into(0, A, lat, rel, None, kind)
+    r1 = eng.stats()["rounds"]
+    pl, pr, _, pk = eng.compute_rows(0, A, want_kind=True)
+    r2 = eng.stats()["rounds"]
+    eng.close()
+    assert r1 - r0 > r2 - r1, (r1 - r0, r2 - r1)
+    assert_bitexact("latency", lat, pl)
+    assert_bitexact("reliability", rel, pr)
+    assert_bitexact("kind", kind, pk)
+
+
 def test_row_exchange_with_engine_device_rows():
     """bench.py's step (shard.RowExchange) with the engine's device rows (compute_rows_device
     on torch's stream) in two row chunks, world size 1: the assembled matrix equals the
