@@ -520,8 +520,9 @@ __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in
 // bound, e.g. C3): the round's item count never visits the host.  k_scan_wl turns the
 // per-batch counts of k_compact into the prefix the worklist kernel reads, and logs the
 // total per round (tlog[round]: the host reads a block of rounds at once and stops at the
-// first empty one, which is convergence: no change, no activation).
-__global__ __launch_bounds__(256) void k_scan_wl(const uint32_t* __restrict__ wlcnt, int32_t nb,
+// first empty one, which is convergence: no change, no activation).  It also zeroes the
+// counts for the next round's k_compact (one memset launch fewer per round).
+__global__ __launch_bounds__(256) void k_scan_wl(uint32_t* __restrict__ wlcnt, int32_t nb,
                                                  int64_t* __restrict__ prefix, int64_t* __restrict__ tlog,
                                                  int32_t round) {
     __shared__ int64_t sc[256];
@@ -530,7 +531,11 @@ __global__ __launch_bounds__(256) void k_scan_wl(const uint32_t* __restrict__ wl
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int32_t b = threadIdx.x * PER + k;
-        v[k] = b < nb ? (int64_t)wlcnt[b] : 0;
+        v[k] = 0;
+        if (b < nb) {
+            v[k] = (int64_t)wlcnt[b];
+            wlcnt[b] = 0u;
+        }
         sum += v[k];
     }
     sc[threadIdx.x] = sum;
@@ -3077,7 +3082,6 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                                    g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl, eng->d_wlpre, nbg, cnt_cur,
                                    eng->d_prof);
                 if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0) + 1], s));
-                HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
                 hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
                                    (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);
                 hipLaunchKernelGGL(k_scan_wl, dim3(1), dim3(256), 0, s, eng->d_wlcnt, nbg, eng->d_wlpre, eng->d_tlog,
