@@ -2213,27 +2213,39 @@ __global__ __launch_bounds__(256) void k_min_w64(const float* __restrict__ W32p,
 
 // minDc[b][c][lane] = min D32 over the CHANGED pairs (previous round's change masks) of the
 // rows perm[c*64 .. c*64+64) of batch b; NaN when the chunk has none for the lane (a dead
-// chunk for that source whatever the thresholds).  One wave per (chunk, batch).
+// chunk for that source whatever the thresholds).  One block per (chunk, batch): each wave
+// takes 16 of the rows with all their loads in flight (one wave walking the 64 rows in turn
+// took 69 us per C2 delta round, latency-bound), the four minima meet in LDS.
 __global__ __launch_bounds__(256) void k_min_d32c(Pools pools, const int32_t* __restrict__ perm, int32_t V,
                                                   int32_t nvc, int32_t parity, const int32_t* __restrict__ cnt_prev,
                                                   int32_t thresh, float* __restrict__ minDc) {
+    __shared__ float sm[4][KL];
+    constexpr int RW = KL / 4;  // rows per wave
     const int32_t b = blockIdx.y;
-    const int32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int32_t c = blockIdx.x;
+    const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    if (c >= nvc) return;
     const BatchDev B = batch_view(pools, b);
-    const unsigned long long* chp = B.chm(parity ^ 1);
     float m = __int_as_float(0x7f800000);
     const int32_t cp = cnt_prev[b];
-    if (cp > 0 && cp <= thresh) {
-        for (int r = 0; r < KL; ++r) {
-            const int32_t u = perm[c * KL + r];
-            if (u >= V) continue;
-            const unsigned long long mk = chp[u];
-            if ((mk >> lane) & 1ull) m = fminf(m, B.D32[(size_t)u * KL + lane]);
-        }
+    if (cp > 0 && cp <= thresh) {  // block-uniform
+        const unsigned long long* chp = B.chm(parity ^ 1);
+        int32_t u[RW];
+        unsigned long long mk[RW];
+#pragma unroll
+        for (int i = 0; i < RW; ++i) u[i] = perm[c * KL + wave * RW + i];
+#pragma unroll
+        for (int i = 0; i < RW; ++i) mk[i] = u[i] < V ? chp[u[i]] : 0ull;
+#pragma unroll
+        for (int i = 0; i < RW; ++i)
+            if ((mk[i] >> lane) & 1ull) m = fminf(m, B.D32[(size_t)u[i] * KL + lane]);
     }
-    minDc[((size_t)b * nvc + c) * KL + lane] = m < __int_as_float(0x7f800000) ? m : __int_as_float(0x7fc00000);
+    sm[wave][lane] = m;
+    __syncthreads();
+    if (wave == 0) {
+        m = fminf(fminf(sm[0][lane], sm[1][lane]), fminf(sm[2][lane], sm[3][lane]));
+        minDc[((size_t)b * nvc + c) * KL + lane] = m < __int_as_float(0x7f800000) ? m : __int_as_float(0x7fc00000);
+    }
 }
 
 // ---------------------------------------------------------------- self pairs
@@ -3187,7 +3199,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                         HIP_TRY(hipMalloc((void**)&eng->d_minDc, need * sizeof(float)));
                         eng->minDc_n = need;
                     }
-                    hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)((nvc + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
+                    hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, nbg), dim3(256), 0, s, eng->pools,
                                        eng->d_perm, V, nvc, par, cnt_prev, thresh, eng->d_minDc);
                     hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
