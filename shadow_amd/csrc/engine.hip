@@ -2769,6 +2769,7 @@ struct shadowtopo_engine {
     unsigned long long* d_prof = nullptr;  // = prof_buf when OPT_PROFILE is on, else NULL
     unsigned long long* prof_buf = nullptr; // [nb][8 shards][visits, changes]
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
+    hipEvent_t ev_spin = nullptr;  // round_sync
     std::vector<hipEvent_t> ev_dev;  // device-driven rounds: one pair per round of a block
     shadowtopo_stats st{};
 };
@@ -2901,6 +2902,19 @@ int ensure_replay(shadowtopo_engine* eng) {
 // batch slots in flight: enough for every requested row when HBM allows.  Sparse rounds
 // cost a launch + a flag read-back each, so more batches per round means fewer rounds in
 // total; the budget is 40 % of the free HBM (MI355X: 288 GB) beside the resident graph.
+// The host's wait between rounds (a round's counts decide the next launch): polls an event
+// for up to 200 us before falling back to a blocking wait.  A blocking synchronisation
+// sleeps, and its wake-up added tens of microseconds to each of a C2 step's 4 waits.
+hipError_t round_sync(shadowtopo_engine* eng, hipStream_t s) {
+    hipError_t e = hipEventRecord(eng->ev_spin, s);
+    if (e != hipSuccess) return e;
+    const auto t0 = std::chrono::steady_clock::now();
+    while ((e = hipEventQuery(eng->ev_spin)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) return hipEventSynchronize(eng->ev_spin);
+    }
+    return e;
+}
+
 int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
@@ -3102,7 +3116,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             }
             HIP_TRY(hipMemcpyAsync(eng->h_tlog + r0, eng->d_tlog + r0, sizeof(int64_t) * (DEV_K + 1),
                                    hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(round_sync(eng, s));
             bool done = false;
             for (int64_t round = r0; round < r0 + DEV_K; ++round) {
                 const int64_t T = eng->h_tlog[round];
@@ -3133,7 +3147,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                            eng->d_wlcnt, g.in_ptr);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(round_sync(eng, s));
     }
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
@@ -3273,7 +3287,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
         }
         HIP_TRY(hipMemcpyAsync(eng->h_cnt, cnt_cur, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(round_sync(eng, s));
         eng->st.relax_launches++;
         eng->st.rounds++;
         if (eng->opt_timing) {
@@ -3759,7 +3773,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         std::vector<unsigned long long> masks(nbg);
         HIP_TRY(hipMemcpyAsync(masks.data(), eng->pools.mask, sizeof(unsigned long long) * nbg,
                                hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(round_sync(eng, s));
         eng->st.compose_ms +=
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         std::vector<std::pair<int32_t, int32_t>> jobs;  // (vertex, row)
@@ -4002,7 +4016,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     }
     if (hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess ||
-        hipEventCreate(&eng->evm) != hipSuccess || hipEventCreate(&eng->evm2) != hipSuccess) {
+        hipEventCreate(&eng->evm) != hipSuccess || hipEventCreate(&eng->evm2) != hipSuccess ||
+        hipEventCreateWithFlags(&eng->ev_spin, hipEventDisableTiming) != hipSuccess) {
         shadowtopo_destroy(eng);
         return fail(SHADOWTOPO_EDEVICE, "stream/event create failed");
     }
@@ -4054,6 +4069,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->ev1) (void)hipEventDestroy(eng->ev1);
     if (eng->evm) (void)hipEventDestroy(eng->evm);
     if (eng->evm2) (void)hipEventDestroy(eng->evm2);
+    if (eng->ev_spin) (void)hipEventDestroy(eng->ev_spin);
     if (eng->copy_stream) (void)hipStreamSynchronize(eng->copy_stream);
     for (int k = 0; k < 2; ++k) {
         if (eng->ev_comp[k]) (void)hipEventDestroy(eng->ev_comp[k]);
