@@ -188,7 +188,8 @@ typedef struct {
     int cur_dom;         /* GML_NODE / GML_EDGE / GML_GRAPH of the element owning <data> */
     int64_t cur_idx;
     int in_data;
-    char* data_key;
+    sbuf data_key;       /* key of the open <data> (reused buffer) */
+    sbuf tagbuf;         /* the current tag's attribute names and values (reused buffer) */
     int in_key;          /* index into keys while inside <key> */
     int in_default;
     sbuf text;
@@ -210,22 +211,18 @@ static const char* local_name(const char* n) {
     return c ? c + 1 : n;
 }
 
+/* A parsed tag.  Attribute names and decoded values live in the parser's reusable tag
+ * buffer (NUL-separated), so a tag costs no allocation: the file's ~3e7 attributes of a
+ * C5-sized topology took two mallocs and two frees each when every string was its own
+ * allocation. */
 typedef struct {
     char name[64];
     int nattr;
-    char* an[16];
-    char* av[16];
+    const char* an[16];
+    const char* av[16];
     int self_close;
     int is_end;
 } tag;
-
-static void tag_free(tag* t) {
-    for (int i = 0; i < t->nattr; i++) {
-        free(t->an[i]);
-        free(t->av[i]);
-    }
-    t->nattr = 0;
-}
 
 static const char* tag_get(const tag* t, const char* name) {
     for (int i = 0; i < t->nattr; i++)
@@ -235,7 +232,12 @@ static const char* tag_get(const tag* t, const char* name) {
 
 /* parse a tag starting after '<'; s->p points at the name (or '/') */
 static int parse_tag(pstate* s, tag* t) {
-    memset(t, 0, sizeof *t);
+    t->nattr = 0;
+    t->self_close = 0;
+    t->is_end = 0;
+    sbuf* tb = &s->tagbuf;
+    tb->n = 0;
+    size_t aoff[16], voff[16];
     const char* p = s->p;
     if (p < s->end && *p == '/') {
         t->is_end = 1;
@@ -272,16 +274,20 @@ static int parse_tag(pstate* s, tag* t) {
         while (p < s->end && *p != q) p++;
         if (p >= s->end) return perr(s, "unterminated attribute value in <%s", t->name);
         if (t->nattr < 16) {
-            sbuf b = {0};
-            if (sb_add_decoded(&b, av, (size_t)(p - av))) {
-                free(b.s);
-                return perr(s, "out of memory");
-            }
-            t->an[t->nattr] = strndup(an, anl);
-            t->av[t->nattr] = b.s ? b.s : strdup("");
+            /* name NUL value NUL, as offsets: the buffer may move while it grows */
+            aoff[t->nattr] = tb->n;
+            if (sb_add(tb, an, anl)) return perr(s, "out of memory");
+            tb->n++;
+            voff[t->nattr] = tb->n;
+            if (sb_add_decoded(tb, av, (size_t)(p - av)) || sb_add(tb, "", 0)) return perr(s, "out of memory");
+            tb->n++;
             t->nattr++;
         }
         p++;
+    }
+    for (int i = 0; i < t->nattr; i++) {
+        t->an[i] = tb->s + aoff[i];
+        t->av[i] = tb->s + voff[i];
     }
     s->p = p;
     return 0;
@@ -381,9 +387,10 @@ static int vertex_of(pstate* s, const char* name, int32_t* out) {
 
 static int store_data(pstate* s) {
     const char* txt = s->text.s ? s->text.s : "";
+    const char* dk = s->data_key.s ? s->data_key.s : "";
     for (int i = 0; i < s->g->nattr; i++) {
         gml_attr* a = &s->g->attrs[i];
-        if (a->domain != s->cur_dom || strcmp(a->key_id, s->data_key)) continue;
+        if (a->domain != s->cur_dom || strcmp(a->key_id, dk)) continue;
         int64_t idx = s->cur_dom == GML_GRAPH ? 0 : s->cur_idx;
         if (attr_reserve(a, idx + 1)) return perr(s, "out of memory");
         if (a->type == GML_STRING) {
@@ -511,8 +518,8 @@ static int handle_start(pstate* s, tag* t) {
     }
     if (!strcmp(n, "data")) {
         const char* k = tag_get(t, "key");
-        free(s->data_key);
-        s->data_key = strdup(k ? k : "");
+        s->data_key.n = 0;
+        if (sb_add(&s->data_key, k ? k : "", k ? strlen(k) : 0)) return perr(s, "out of memory");
         s->text.n = 0;
         if (s->text.s) s->text.s[0] = 0;
         if (t->self_close) return store_data(s);
@@ -601,11 +608,11 @@ int gml_parse_buffer(const char* buf, size_t len, gml_graph** out, char* err, si
                 if (!strcmp(local_name(t.name), "graph") && !t.is_end) saw_graph = 1;
                 rc = t.is_end ? handle_end(&s, t.name) : handle_start(&s, &t);
             }
-            tag_free(&t);
         }
     }
     free(s.text.s);
-    free(s.data_key);
+    free(s.data_key.s);
+    free(s.tagbuf.s);
     for (int i = 0; i < s.nkeys; i++) {
         free(s.keys[i].id);
         free(s.keys[i].name);
