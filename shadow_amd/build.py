@@ -16,6 +16,7 @@ ARCH = os.environ.get("SHADOWTOPO_ARCH", "gfx950")
 
 HIP_SOURCES = ["engine.hip", "graph_build.hip"]
 C_SOURCES = ["graphml.c", "topology_hip.c", "shadow_hooks.c"]  # C host shim
+CXX_SOURCES = ["numparse.cpp"]  # the GraphML reader's number conversion (std::from_chars)
 
 
 def _hipcc():
@@ -43,15 +44,20 @@ def build(verbose=False, force=False):
     inc = os.path.join(ROOT, "include")
     hip_srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
     c_srcs = [os.path.join(CSRC, s) for s in C_SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    cxx_srcs = [os.path.join(CSRC, s) for s in CXX_SOURCES]
     headers = [os.path.join(inc, h) for h in os.listdir(inc)] + [
         os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    if not force and not _stale(LIB, hip_srcs + c_srcs + headers):
+    if not force and not _stale(LIB, hip_srcs + c_srcs + cxx_srcs + headers):
         return LIB
     objs = []
     for s in c_srcs:
         o = os.path.join(OUT, os.path.basename(s) + ".o")
         _run(["gcc", "-O2", "-fPIC", "-std=gnu11", "-Wall", "-Wextra", "-pthread", "-ffp-contract=off",
               "-I", inc, "-I", CSRC, "-c", s, "-o", o], verbose)
+        objs.append(o)
+    for s in cxx_srcs:
+        o = os.path.join(OUT, os.path.basename(s) + ".o")
+        _run(["g++", "-O2", "-fPIC", "-std=c++17", "-Wall", "-Wextra", "-ffp-contract=off", "-c", s, "-o", o], verbose)
         objs.append(o)
     hipcc = _hipcc()
     for s in hip_srcs:

@@ -19,6 +19,7 @@
 typedef struct {
     char** keys;
     int32_t* vals;
+    uint64_t* hs;  /* each key's hash: probes compare it before the string (one miss, not two) */
     size_t cap;
     size_t n;
 } strhash;
@@ -36,45 +37,56 @@ static int sh_grow(strhash* h) {
     size_t ncap = h->cap ? h->cap * 2 : 1024;
     char** nk = (char**)calloc(ncap, sizeof(char*));
     int32_t* nv = (int32_t*)calloc(ncap, sizeof(int32_t));
-    if (!nk || !nv) {
+    uint64_t* nh = (uint64_t*)calloc(ncap, sizeof(uint64_t));
+    if (!nk || !nv || !nh) {
         free(nk);
         free(nv);
+        free(nh);
         return -1;
     }
     for (size_t i = 0; i < h->cap; i++) {
         if (!h->keys[i]) continue;
-        size_t j = fnv1a(h->keys[i], strlen(h->keys[i])) & (ncap - 1);
+        size_t j = h->hs[i] & (ncap - 1);
         while (nk[j]) j = (j + 1) & (ncap - 1);
         nk[j] = h->keys[i];
         nv[j] = h->vals[i];
+        nh[j] = h->hs[i];
     }
     free(h->keys);
     free(h->vals);
+    free(h->hs);
     h->keys = nk;
     h->vals = nv;
+    h->hs = nh;
     h->cap = ncap;
     return 0;
 }
 
-/* returns the id for key s (inserting `next` if absent); *inserted set accordingly */
-static int sh_intern(strhash* h, const char* s, int32_t next, int32_t* out, int* inserted) {
+/* returns the id for key s (inserting `next` if absent); *inserted set accordingly, and
+ * *key the table's own copy of the string */
+static int sh_intern(strhash* h, const char* s, int32_t next, int32_t* out, int* inserted, char** key) {
     if ((h->n + 1) * 2 > h->cap && sh_grow(h)) return -1;
-    size_t len = strlen(s);
-    size_t j = fnv1a(s, len) & (h->cap - 1);
+    const size_t len = strlen(s);
+    const uint64_t hv = fnv1a(s, len);
+    size_t j = hv & (h->cap - 1);
     while (h->keys[j]) {
-        if (strcmp(h->keys[j], s) == 0) {
+        if (h->hs[j] == hv && strcmp(h->keys[j], s) == 0) {
             *out = h->vals[j];
             *inserted = 0;
+            *key = h->keys[j];
             return 0;
         }
         j = (j + 1) & (h->cap - 1);
     }
-    h->keys[j] = strdup(s);
+    h->keys[j] = (char*)malloc(len + 1);
     if (!h->keys[j]) return -1;
+    memcpy(h->keys[j], s, len + 1);
     h->vals[j] = next;
+    h->hs[j] = hv;
     h->n++;
     *out = next;
     *inserted = 1;
+    *key = h->keys[j];
     return 0;
 }
 
@@ -82,6 +94,7 @@ static void sh_free(strhash* h) {
     /* keys are owned by node_ids */
     free(h->keys);
     free(h->vals);
+    free(h->hs);
 }
 
 /* ------------------------------------------------------------ growable text */
@@ -293,15 +306,14 @@ static int parse_tag(pstate* s, tag* t) {
     return 0;
 }
 
+int gml_strtod(const char* s, double* out); /* numparse.cpp: strtod's value, faster */
+
 static double parse_num(const char* txt, double def) {
     if (!txt) return def;
     while (*txt && isspace((unsigned char)*txt)) txt++;
     if (!*txt) return def;
-    char* endp = NULL;
-    errno = 0;
-    double v = strtod(txt, &endp);
-    if (endp == txt) return def;
-    return v;
+    double v;
+    return gml_strtod(txt, &v) ? v : def;
 }
 
 static int parse_bool(const char* txt, double def) {
@@ -366,7 +378,8 @@ static int finish_key(pstate* s, int ki) {
 static int vertex_of(pstate* s, const char* name, int32_t* out) {
     gml_graph* g = s->g;
     int ins = 0;
-    if (sh_intern(&s->ids, name, g->n, out, &ins)) return perr(s, "out of memory");
+    char* key = NULL;
+    if (sh_intern(&s->ids, name, g->n, out, &ins, &key)) return perr(s, "out of memory");
     if (ins) {
         if (g->n >= s->ids_cap) {
             int64_t nc = s->ids_cap ? s->ids_cap * 2 : 1024;
@@ -376,10 +389,7 @@ static int vertex_of(pstate* s, const char* name, int32_t* out) {
             s->ids_cap = nc;
         }
         /* the hash owns one copy; node_ids shares it */
-        size_t len = strlen(name);
-        size_t j = fnv1a(name, len) & (s->ids.cap - 1);
-        while (strcmp(s->ids.keys[j], name)) j = (j + 1) & (s->ids.cap - 1);
-        g->node_ids[g->n] = s->ids.keys[j];
+        g->node_ids[g->n] = key;
         g->n++;
     }
     return 0;

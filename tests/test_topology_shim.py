@@ -91,6 +91,32 @@ def test_graphml_ingest_matches_reference_reader(tmp_path, gen):
     top.free()
 
 
+def test_graphml_numbers_convert_as_strtod(tmp_path):
+    """numparse.cpp (std::from_chars, strtod fallback) gives libc strtod's value for every
+    spelling a topology file may hold: signs, hex floats, 17+ significant digits, bare
+    exponents, leading blanks"""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.strtod.restype = ctypes.c_double
+    libc.strtod.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    spellings = ["+5", "0x1p3", "0X1.8p1", "1e2", ".5", "5.", " 7", "1e", "2.5e-3", "12345678901234567890",
+                 "0.12345678901234567890123", "1.7976931348623157e308", "4.9406564584124654e-300", "3E+2",
+                 "1.2451401810445306", "0.1"]
+    g = synth.random_sparse(V=60, avg_deg=3, seed=9)
+    text = synth.to_graphml(g)
+    key = re.search(r'<key attr.name="latency"[^>]*id="(\w+)"', text)
+    key = key.group(1) if key else re.search(r'id="(\w+)"[^>]*attr.name="latency"', text).group(1)
+    it = iter(spellings)
+    text = re.sub(r'(<data key="%s">)[^<]*(</data>)' % key,
+                  lambda m: m.group(1) + next(it) + m.group(2), text, count=len(spellings))
+    top = T.Topology.new(write(tmp_path, "n.xml", text))
+    assert top is not None
+    _, _, lat, _, _ = top.edges()
+    want = np.array([libc.strtod(x.encode(), None) for x in spellings])
+    assert np.array_equal(lat[:len(spellings)].view(np.uint64), want.view(np.uint64)), (lat[:len(spellings)], want)
+    top.free()
+
+
 def test_example_config_graph_and_quirks(tmp_path):
     # CDATA, entities, comments, node declared after use, for="all" key with default
     text = """<?xml version="1.0"?>
