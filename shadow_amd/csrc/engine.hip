@@ -1221,7 +1221,7 @@ constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FT
 // (the kernel wants 82, i.e. 5 waves); waves_per_eu(6) spills 3 dwords outside the chunk
 // loop and buys a sixth wave: 3.89 -> 3.68 ms on C2 together with the unrolls below.
 template <int TDT, int XR, int TB, bool PR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6 : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
                                                        int32_t nb, int32_t ntb, int32_t parity, int32_t thresh,
