@@ -2919,12 +2919,15 @@ int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
     const double per_batch = (double)eng->Vp * KL * state_bytes(eng) + 18.0 * eng->Vp + (eng->dense ? 0.0 : 36.0 * eng->Vp);
+    const double cap = eng->dense ? 16.0 : 256.0;
+    // the budget below is never under 24 GB (times the share): when that floor already holds
+    // every batch, the answer is `need` without the driver's free-memory query (per step)
+    if (std::min(cap, std::floor(24.0e9 * eng->opt_hbm_share / 1000.0 / per_batch)) >= (double)need) return need;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
     // engines sharing one device (SHADOWTOPO_DEVICES listing it twice) split the budget
     const double budget = std::max(24.0e9, 0.55 * ((double)free_b + held)) * eng->opt_hbm_share / 1000.0;
-    const double cap = eng->dense ? 16.0 : 256.0;
     const int32_t nb = (int32_t)std::max(1.0, std::min(cap, std::floor(budget / per_batch)));
     return std::min(nb, need);
 }
