@@ -188,42 +188,143 @@ def roofline_of(st, g, config, scale, world, rows, steps, csr_variant=1, dense_v
     return roofline
 
 
-def north_star_c4(device, steps=5, warmup=1):
+def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, on_timed_start=None,
+                on_timed_end=None, on_first_step=None):
+    """One sharded attached-pair matrix build per step: this rank's contiguous
+    row block computed by `compute(a, z, lat, rel, hops)` into packed row chunks, each chunk
+    all-gathered (shard.RowExchange).  `warmup` untimed steps, then exactly `steps` bracketed
+    by a barrier and a device synchronisation on both sides, max over ranks; at N > 1 the
+    all-gather alone is timed the same way afterwards.  `device` may be a CPU device (the gloo
+    tests drive this with the oracle as the compute stand-in)."""
+    import torch
+    from shadow_amd import shard
+    cuda = device.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize(device)
+
+    def timed(fn, n):
+        sync()
+        if dist is not None:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        sync()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([el], dtype=torch.float64, device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el
+
+    ex = shard.RowExchange(dist, A, world, rank, device, chunks)
+    for i in range(max(1, warmup)):
+        ex.step(compute)
+        if i == 0 and on_first_step:
+            sync()
+            on_first_step()
+    if on_timed_start:
+        on_timed_start()
+    elapsed = timed(lambda: ex.step(compute), steps)
+    if on_timed_end:
+        on_timed_end()
+    out = {"exchange": ex, "elapsed_s": elapsed, "timed": timed}
+    if world > 1:
+        def gather_only():
+            works = [dist.all_gather_into_tensor(ex.gathered[c], ex.packs[c], async_op=True)
+                     for c in range(len(ex.bounds))]
+            for w in works:
+                w.wait()
+        out["allgather_s"] = timed(gather_only, steps)
+        out["allgather_bytes"] = sum(p.numel() for p in ex.packs) * world
+    return out
+
+
+def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=1, project=True):
     """The north-star workload (BASELINE.json configs[3], SURVEY.md 8d C4: a 10^5-vertex
-    Barabasi-Albert graph, 10^4 attached hosts) on this one GPU, timed like the headline
-    (inputs resident, rows into HBM, synchronize around exactly `steps` matrix builds), so
-    the driver's own run carries it beside the configs[1] line."""
+    Barabasi-Albert graph, 10^4 attached hosts) on every rank, timed like the headline
+    (inputs resident, rows into HBM, barrier + synchronize around exactly `steps` matrix
+    builds, max over ranks), so the driver's own run carries it beside the configs[1] line
+    at every GPU count: the A sources are sharded over the ranks in contiguous row blocks
+    (shard.shard_rows) and one RCCL all-gather per row chunk gives every rank the whole
+    10^4 x 10^4 latency / reliability / hop matrix (shard.RowExchange).
+
+    At one GPU it also times rank 0's and the last rank's row share of an N-GPU run
+    (N = 2, 4, 8) on this GPU: the per-GPU half of the N-GPU figure (the all-gather over
+    xGMI is the other half, measured only by an N-GPU run)."""
     import torch
     from shadow_amd import engine as E
-    g, _per, desc = build_workload("C4", 1, 1.0)
+    from shadow_amd import shard
+    g, _per, desc = build_workload("C4", world, 1.0)
     A = len(g.attached)
     eng = E.Engine.from_synth(g, device=device.index or 0)
     try:
         eng.set_attached(g.attached)
         eng.set_option(E.OPT_TIMING, 1)
-        lat = torch.empty((A, A), dtype=torch.float64, device=device)
-        rel = torch.empty((A, A), dtype=torch.float64, device=device)
-        hops = torch.empty((A, A), dtype=torch.int32, device=device)
 
-        def step():
+        def compute(a, z, lat, rel, hops):
             stream = torch.cuda.current_stream(device).cuda_stream
-            eng.compute_rows_device(0, A, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
+            eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
 
-        for _ in range(max(1, warmup)):
-            step()
-        torch.cuda.synchronize(device)
-        eng.reset_stats()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
-        torch.cuda.synchronize(device)
-        elapsed = time.perf_counter() - t0
-        st = eng.stats()
-        return {"workload": desc, "n_vertices": g.n, "n_arcs": st["n_arcs"], "attached": A,
-                "steps": steps, "warmup": warmup, "matrix_build_ms": elapsed / steps * 1e3,
-                "value": A * steps / elapsed, "unit": "source-paths/s",
-                "rounds_per_step": st["rounds"] / steps,
-                "roofline": roofline_of(st, g, "C4", 1.0, 1, A, steps)}
+        eng_stats = {}
+
+        def reset():
+            eng.reset_stats()
+
+        def collect():
+            eng_stats.update(eng.stats())
+
+        run = run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks,
+                          on_timed_start=reset, on_timed_end=collect)
+        ex, elapsed, st = run["exchange"], run["elapsed_s"], eng_stats
+        timed = run["timed"]
+        rec = {"workload": desc, "n_gpus": world, "n_vertices": g.n, "n_arcs": st["n_arcs"], "attached": A,
+               "steps": steps, "warmup": warmup, "matrix_build_ms": elapsed / steps * 1e3,
+               "value": A * steps / elapsed, "unit": "source-paths/s",
+               "parallelism": f"{A} sources sharded x{world} (rows [{ex.r0},{ex.r1}) on rank {rank})"
+                              + (f" + RCCL all-gather ({len(ex.bounds)} chunks)" if world > 1 else ""),
+               "rounds_per_step": st["rounds"] / steps,
+               "roofline": roofline_of(st, g, "C4", 1.0, world, ex.rows, steps)}
+        if world > 1:
+            rec["allgather_ms"] = run["allgather_s"] / steps * 1e3
+            rec["allgather_bytes_per_rank"] = run["allgather_bytes"]
+            rec["allgather_GBps_per_rank"] = run["allgather_bytes"] * (world - 1) / world / (run["allgather_s"] / steps) / 1e9
+        target = {"matrix_build_ms_under": 1000.0, "hbm_frac_at_least": 0.5, "on_gpus": 8,
+                  "time_met": rec["matrix_build_ms"] < 1000.0,
+                  "frac_compulsory": rec["roofline"]["frac"],
+                  "frac_measured_traffic": (rec["roofline"]["measured_hbm_gbs"] / HBM_PEAK_GBS
+                                            if rec["roofline"].get("measured_hbm_gbs") else None)}
+        rec["target"] = target
+        if project and world == 1:
+            proj = {}
+            lat = torch.empty((A, A), dtype=torch.float64, device=device)
+            rel = torch.empty((A, A), dtype=torch.float64, device=device)
+            hops = torch.empty((A, A), dtype=torch.int32, device=device)
+            for W in (2, 4, 8):
+                shares = []
+                for r in sorted({0, W - 1}):
+                    a, z, _ = shard.shard_rows(A, W, r)
+                    compute(a, z, lat, rel, hops)
+                    eng.reset_stats()
+                    el = timed(lambda: compute(a, z, lat, rel, hops), steps)
+                    sst = eng.stats()
+                    rf = roofline_of(sst, g, "C4", 1.0, W, z - a, steps)
+                    shares.append({"rank": r, "rows": z - a, "ms": el / steps * 1e3,
+                                   "relax_ms": sst["relax_ms"] / steps, "roofline_frac": rf["frac"],
+                                   "rounds": sst["rounds"] / steps})
+                slow = max(shares, key=lambda x: x["ms"])
+                proj[str(W)] = {"per_gpu_ms": slow["ms"], "ranks_timed": shares,
+                                "allgather_bytes_per_gpu": 20 * A * A * (W - 1) // W,
+                                "note": "one rank's row share computed on this GPU; the all-gather over xGMI "
+                                        "is not included (measured only by an N-GPU run)"}
+            rec["projection"] = proj
+            del lat, rel, hops
+        return rec
     finally:
         eng.close()
 
@@ -239,7 +340,7 @@ def main():
     ap.add_argument("--no-host-rate", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
     ap.add_argument("--cpu-sources", type=int, default=12)
     ap.add_argument("--no-north-star", action="store_true",
-                    help="skip the C4 north-star record the default (C2, 1 GPU) run adds to its line")
+                    help="skip the C4 north-star record (sharded over the ranks) the default C2 run adds to its line")
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
@@ -315,37 +416,19 @@ def main():
     # (measured at N=1: 2 chunks cost +0.9 ms of per-chunk overhead, so overlap pays only
     # where the exchange is long: 8 ranks move ~1.1 GB into every GPU per step)
     chunks = args.chunks or (2 if world >= 8 else 1)
-    ex = shard.RowExchange(dist, A, world, rank, dev, chunks)
 
     def compute(a, z, lat, rel, hops):
         stream = torch.cuda.current_stream(dev).cuda_stream
         eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=stream)
 
-    def step():
-        ex.step(compute)
-
-    for i in range(max(1, args.warmup)):
-        step()
-        if i == 0:  # engine creation -> first finished matrix rows on the device
-            torch.cuda.synchronize(dev)
-            cold_start_ms = (time.perf_counter() - t_cold) * 1e3
-    torch.cuda.synchronize(dev)
-    eng.reset_stats()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    st = eng.stats()
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    cold = {}
+    st = {}
+    run = run_sharded(dist, world, rank, dev, A, compute, args.steps, args.warmup, chunks,
+                      on_timed_start=eng.reset_stats, on_timed_end=lambda: st.update(eng.stats()),
+                      # engine creation -> first finished matrix rows on the device
+                      on_first_step=lambda: cold.update(ms=(time.perf_counter() - t_cold) * 1e3))
+    cold_start_ms = cold["ms"]
+    elapsed = run["elapsed_s"]
     total_sources = A if world > 1 else rows  # every rank's rows per step
     value = total_sources * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -375,14 +458,16 @@ def main():
         host_pageable_ms = (time.perf_counter() - h0) * 1e3
         del outs
 
+    # the north-star record (C4 sharded over every rank + all-gather) at every GPU count: all
+    # ranks take part (barriers, all-gather), rank 0 reports
     north = None
-    if rank == 0 and world == 1 and args.config == "C2" and args.scale == 1.0 and not args.no_north_star:
+    if args.config == "C2" and args.scale == 1.0 and not args.no_north_star:
         eng.close()
         eng = None
         try:
-            north = north_star_c4(dev)
+            north = north_star_c4(dev, dist, world, rank, chunks=chunks)
         except Exception as e:  # report, never fake
-            north = {"error": str(e)}
+            north = {"error": f"{type(e).__name__}: {e}"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

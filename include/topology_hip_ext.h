@@ -36,6 +36,10 @@ typedef struct topology_hip_info {
     int64_t self_path_count;  /* _topology_computeShortestPathToSelf calls */
     int64_t cached_paths;     /* Paths in the cache */
     double self_seconds;      /* engine time of the self-path rule */
+    /* IP -> vertex table read by the per-packet lookups with no lock (topology_hip.c iptab) */
+    int64_t ip_table_slots;     /* slots of the live table */
+    int64_t ip_tables_retired;  /* tables replaced by growth / tombstone rehash (freed with the topology) */
+    int64_t ip_retired_bytes;   /* their bytes */
 } topology_hip_info;
 
 /* HIP device the engine uses (default: $SHADOWTOPO_DEVICE or 0); before the first query */

@@ -319,8 +319,14 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
                                               uint32_t curH, double curR, int32_t curP) {
     const size_t idx = (size_t)v * KL + lane;
     const size_t uidx = (size_t)u * KL + lane;
+#ifdef EXP_NO_PRED_GATHER
+    const uint32_t hu = 0u;
+    const double ru = 1.0;
+    (void)uidx;
+#else
     const uint32_t hu = B.H[uidx];
     const double ru = B.R[uidx];
+#endif
     // local tie: two candidates share (fl(d(u)+w), d(u)), or the degenerate d(u) == d(v)
     const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? (TAINT | LTIE) : 0u);
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
@@ -1245,7 +1251,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
     __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
     int32_t grp, vt;
+#ifdef EXP_DENSE_TILE_MAJOR
+    if (!xcd_tile(blockIdx.x, ntb, (nb + TB - 1) / TB, vt, grp)) return;
+#else
     if (!xcd_tile(blockIdx.x, (nb + TB - 1) / TB, ntb, grp, vt)) return;  // block-uniform exits only (barriers below)
+#endif
     const int32_t b0 = grp * TB;  // this block's TB batches
     bool live[TB];
     int32_t first = -1;
@@ -1788,8 +1798,14 @@ __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, in
     if (du == c) lt = LTIE;  // degenerate d(u) == d(v): the reference order is heap-dependent
     const int32_t arc = WI[(size_t)u * Vp + v];
     const size_t uidx = (size_t)u * KL + s;
+#ifdef EXP_NO_PRED_GATHER
+    const uint32_t hu = 0u;
+    const double ru = 1.0;
+    (void)uidx;
+#else
     const uint32_t hu = B.H[uidx];
     const double ru = B.R[uidx];
+#endif
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
     const double r = ru * in_r[arc];
     B.BDU[idx] = du;
@@ -2758,6 +2774,7 @@ struct shadowtopo_engine {
     int32_t opt_dense_tb = 1;       // batches per wave in the f32-filtered full sweep (1, 2 or 4)
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
+    bool floor_ok = false;             // default_nb: the 24 GB budget floor was found free once
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
@@ -2901,7 +2918,9 @@ int ensure_replay(shadowtopo_engine* eng) {
 
 // batch slots in flight: enough for every requested row when HBM allows.  Sparse rounds
 // cost a launch + a flag read-back each, so more batches per round means fewer rounds in
-// total; the budget is 40 % of the free HBM (MI355X: 288 GB) beside the resident graph.
+// total; the budget is 55 % of the free HBM (MI355X: 288 GB) beside the resident graph, never
+// under 24 GB (times the share) -- a floor that holds every requested batch skips the query
+// only when it is itself within the device's capacity.
 // The host's wait between rounds (a round's counts decide the next launch): polls an event
 // for up to 200 us before falling back to a blocking wait.  A blocking synchronisation
 // sleeps, and its wake-up added tens of microseconds to each of a C2 step's 4 waits.
@@ -2915,19 +2934,23 @@ hipError_t round_sync(shadowtopo_engine* eng, hipStream_t s) {
     return e;
 }
 
-int32_t default_nb(const shadowtopo_engine* eng, int32_t rows) {
+int32_t default_nb(shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
     const double per_batch = (double)eng->Vp * KL * state_bytes(eng) + 18.0 * eng->Vp + (eng->dense ? 0.0 : 36.0 * eng->Vp);
     const double cap = eng->dense ? 16.0 : 256.0;
-    // the budget below is never under 24 GB (times the share): when that floor already holds
-    // every batch, the answer is `need` without the driver's free-memory query (per step)
-    if (std::min(cap, std::floor(24.0e9 * eng->opt_hbm_share / 1000.0 / per_batch)) >= (double)need) return need;
+    // the budget is never under a 24 GB floor (times the share) once one free-memory query of
+    // this engine found the floor free: when it already holds every batch, later calls (one
+    // per step) answer without the driver's query
+    const double floor_b = 24.0e9 * eng->opt_hbm_share / 1000.0;
+    if (eng->floor_ok && std::min(cap, std::floor(floor_b / per_batch)) >= (double)need) return need;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
+    if ((double)free_b + held >= floor_b) eng->floor_ok = true;
     // engines sharing one device (SHADOWTOPO_DEVICES listing it twice) split the budget
-    const double budget = std::max(24.0e9, 0.55 * ((double)free_b + held)) * eng->opt_hbm_share / 1000.0;
+    const double budget = std::max(eng->floor_ok ? floor_b : 0.0,
+                                   0.55 * ((double)free_b + held) * eng->opt_hbm_share / 1000.0);
     const int32_t nb = (int32_t)std::max(1.0, std::min(cap, std::floor(budget / per_batch)));
     return std::min(nb, need);
 }
@@ -3840,11 +3863,16 @@ int ensure_mirrors(shadowtopo_engine* eng) {
         eng->h_in_src.resize(M);
         eng->h_in_eid.resize(M);
         eng->h_loop_eid.resize(V);
+        // on the calling thread's device setting: restored below (shadowtopo_get_eid runs
+        // on Shadow's worker threads, and the process may drive other devices)
+        int prev = -1;
+        (void)hipGetDevice(&prev);
         const bool ok = hipSetDevice(eng->device) == hipSuccess &&
                         hipMemcpy(eng->h_in_ptr.data(), eng->g.in_ptr, 8 * (V + 1), hipMemcpyDeviceToHost) == hipSuccess &&
                         (M == 0 || hipMemcpy(eng->h_in_src.data(), eng->g.in_src, 4 * M, hipMemcpyDeviceToHost) == hipSuccess) &&
                         (M == 0 || hipMemcpy(eng->h_in_eid.data(), eng->g.in_eid, 4 * M, hipMemcpyDeviceToHost) == hipSuccess) &&
                         hipMemcpy(eng->h_loop_eid.data(), eng->g.loop_eid, 4 * V, hipMemcpyDeviceToHost) == hipSuccess;
+        if (prev >= 0) (void)hipSetDevice(prev);
         eng->mirrors_rc = ok ? 0 : fail(SHADOWTOPO_EDEVICE, "get_eid host mirrors");
     });
     return eng->mirrors_rc;

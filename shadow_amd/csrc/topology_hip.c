@@ -47,90 +47,110 @@ extern void worker_updateMinTimeJump(double minPathLatency);
 #define TOPO_MAGIC 0x70B01060u
 #define SHADOWTOPO_MAX_DEVICES 64
 
-/* ------------------------------------------------------------ IP -> vertex table */
-typedef struct {
-    uint32_t* keys;
-    int32_t* vals;
-    uint8_t* state; /* 0 empty, 1 used, 2 deleted */
-    size_t cap, used, live;
-} iptable;
+/* ------------------------------------------------------------ IP -> vertex table
+ * virtualIP (topology.c:42-47, 1388-1405), read by the per-packet lookups with no lock
+ * (SURVEY.md 8(f)3).  Every slot is ONE 64-bit word, ip << 32 | tag (tag 0: empty;
+ * vertex + 1: live; IPT_DEAD: deleted), written by attach / detach under ip_lock (writer)
+ * with a release store and read with an acquire load, so a lookup never sees a torn entry
+ * and a detach costs one store (no rebuild).  Growth, and the rehash that drops tombstones,
+ * builds a new table, publishes it with a release store and retires the old one, which a
+ * lookup that loaded the old pointer may still be probing: retired tables are freed with the
+ * topology.  What they hold is bounded: a table retired by growth is half the size of its
+ * successor (all of them together < the live table), and a rehash at the same size needs
+ * cap / 4 detaches since the last one (at most 32 bytes retained per detach). */
+#define IPT_DEAD 0xFFFFFFFFu
+
+typedef struct iptab {
+    size_t cap;          /* slots, a power of two */
+    size_t used, live;   /* writer-side counts (ip_lock): non-empty slots, live entries */
+    struct iptab* next;  /* retired tables */
+    _Atomic uint64_t slot[];
+} iptab;
 
 static size_t ip_slot(uint32_t ip, size_t cap) {
     uint64_t h = (uint64_t)ip * 0x9E3779B97F4A7C15ULL;
     return (size_t)(h >> 20) & (cap - 1);
 }
 
-static int ipt_grow(iptable* t) {
-    size_t ncap = t->cap ? t->cap * 2 : 256;
-    uint32_t* nk = calloc(ncap, sizeof(uint32_t));
-    int32_t* nv = calloc(ncap, sizeof(int32_t));
-    uint8_t* ns = calloc(ncap, 1);
-    if (!nk || !nv || !ns) {
-        free(nk);
-        free(nv);
-        free(ns);
-        return -1;
-    }
-    for (size_t i = 0; i < t->cap; i++) {
-        if (t->state[i] != 1) continue;
-        size_t j = ip_slot(t->keys[i], ncap);
-        while (ns[j]) j = (j + 1) & (ncap - 1);
-        nk[j] = t->keys[i];
-        nv[j] = t->vals[i];
-        ns[j] = 1;
-    }
-    free(t->keys);
-    free(t->vals);
-    free(t->state);
-    t->keys = nk;
-    t->vals = nv;
-    t->state = ns;
-    t->cap = ncap;
-    t->used = t->live;
-    return 0;
+static iptab* ipt_alloc(size_t cap) {
+    iptab* t = calloc(1, sizeof(iptab) + cap * sizeof(uint64_t));
+    if (t) t->cap = cap;
+    return t;
 }
 
-static int32_t ipt_get(const iptable* t, uint32_t ip) {
-    if (!t->cap) return -1;
-    size_t j = ip_slot(ip, t->cap);
-    while (t->state[j]) {
-        if (t->state[j] == 1 && t->keys[j] == ip) return t->vals[j];
-        j = (j + 1) & (t->cap - 1);
+/* lookups (any thread, no lock) */
+static int32_t ipt_get(const iptab* t, uint32_t ip) {
+    if (!t) return -1;
+    for (size_t j = ip_slot(ip, t->cap);; j = (j + 1) & (t->cap - 1)) {
+        const uint64_t w = atomic_load_explicit(&t->slot[j], memory_order_acquire);
+        if (w == 0) return -1;
+        const uint32_t tag = (uint32_t)w;
+        if ((uint32_t)(w >> 32) == ip && tag != IPT_DEAD) return (int32_t)(tag - 1);
     }
-    return -1;
 }
 
-static int ipt_put(iptable* t, uint32_t ip, int32_t v) { /* g_hash_table_replace */
-    if ((t->used + 1) * 2 > t->cap && ipt_grow(t)) return -1;
-    size_t j = ip_slot(ip, t->cap);
-    size_t tomb = (size_t)-1;
-    while (t->state[j]) {
-        if (t->state[j] == 1 && t->keys[j] == ip) {
-            t->vals[j] = v;
+/* writers hold ip_lock.  A table with room for one more entry (at most half its slots
+ * non-empty): the current one, or a fresh one (twice the size when the live entries need
+ * it) that replaces it */
+static iptab* ipt_room(_Atomic(iptab*)* live, iptab** retired, size_t* nretired) {
+    iptab* t = atomic_load_explicit(live, memory_order_relaxed);
+    if (t && (t->used + 1) * 2 <= t->cap) return t;
+    size_t cap = t ? t->cap : 256;
+    while ((t ? t->live + 1 : 1) * 4 > cap) cap *= 2;
+    iptab* n = ipt_alloc(cap);
+    if (!n) return NULL;
+    for (size_t i = 0; t && i < t->cap; i++) {
+        const uint64_t w = atomic_load_explicit(&t->slot[i], memory_order_relaxed);
+        if (w == 0 || (uint32_t)w == IPT_DEAD) continue;
+        size_t j = ip_slot((uint32_t)(w >> 32), cap);
+        while (atomic_load_explicit(&n->slot[j], memory_order_relaxed)) j = (j + 1) & (cap - 1);
+        atomic_store_explicit(&n->slot[j], w, memory_order_relaxed);
+        n->used++;
+        n->live++;
+    }
+    atomic_store_explicit(live, n, memory_order_release);
+    if (t) {
+        t->next = *retired;
+        *retired = t;
+        (*nretired)++;
+    }
+    return n;
+}
+
+static int ipt_put(_Atomic(iptab*)* live, iptab** retired, size_t* nretired, uint32_t ip, int32_t v) {
+    /* g_hash_table_replace */
+    iptab* t = ipt_room(live, retired, nretired);
+    if (!t) return -1;
+    const uint64_t want = ((uint64_t)ip << 32) | (uint32_t)(v + 1);
+    size_t tomb = (size_t)-1, j = ip_slot(ip, t->cap);
+    for (;; j = (j + 1) & (t->cap - 1)) {
+        const uint64_t w = atomic_load_explicit(&t->slot[j], memory_order_relaxed);
+        if (w == 0) break;
+        if ((uint32_t)w == IPT_DEAD) {
+            if (tomb == (size_t)-1) tomb = j;
+        } else if ((uint32_t)(w >> 32) == ip) {
+            atomic_store_explicit(&t->slot[j], want, memory_order_release);
             return 0;
         }
-        if (t->state[j] == 2 && tomb == (size_t)-1) tomb = j;
-        j = (j + 1) & (t->cap - 1);
     }
     if (tomb != (size_t)-1) j = tomb;
     else t->used++;
-    t->keys[j] = ip;
-    t->vals[j] = v;
-    t->state[j] = 1;
+    atomic_store_explicit(&t->slot[j], want, memory_order_release);
     t->live++;
     return 0;
 }
 
-static void ipt_del(iptable* t, uint32_t ip) {
-    if (!t->cap) return;
-    size_t j = ip_slot(ip, t->cap);
-    while (t->state[j]) {
-        if (t->state[j] == 1 && t->keys[j] == ip) {
-            t->state[j] = 2;
+static void ipt_del(_Atomic(iptab*)* live, uint32_t ip) {
+    iptab* t = atomic_load_explicit(live, memory_order_relaxed);
+    if (!t) return;
+    for (size_t j = ip_slot(ip, t->cap);; j = (j + 1) & (t->cap - 1)) {
+        const uint64_t w = atomic_load_explicit(&t->slot[j], memory_order_relaxed);
+        if (w == 0) return;
+        if ((uint32_t)w != IPT_DEAD && (uint32_t)(w >> 32) == ip) {
+            atomic_store_explicit(&t->slot[j], ((uint64_t)ip << 32) | IPT_DEAD, memory_order_release);
             t->live--;
             return;
         }
-        j = (j + 1) & (t->cap - 1);
     }
 }
 
@@ -146,18 +166,11 @@ typedef struct matrix {
     double* rel;
     uint8_t* kind;
     /* undirected late attach: rows [0, partial) hold the reverse-direction entries in
-     * columns >= partial until an old source's own row is needed (fill_old_rows) */
-    int32_t partial;
+     * columns >= partial until an old source's own row is needed (fill_old_rows rewrites
+     * them in place, then stores 0 here with release order) */
+    _Atomic int32_t partial;
     struct matrix* next; /* retired matrices (readers may still hold them) */
 } matrix;
-
-/* immutable IP -> vertex snapshot for the per-packet lookups: published
- * with a release store on the first query after an attach / detach, read with no lock */
-typedef struct ip_snap {
-    uint64_t version;
-    iptable t;
-    struct ip_snap* next; /* retired snapshots (readers may still hold them) */
-} ip_snap;
 
 /* ascending vertex list of one attach queue and how many of its vertices carry a usable IP */
 typedef struct {
@@ -207,12 +220,10 @@ struct _Topology {
     double* eloss; /* edge packetloss */
     double* vloss; /* vertex packetloss, NaN = absent */
     const gml_attr *a_ip, *a_city, *a_country, *a_geo, *a_type, *a_bwdown, *a_bwup, *a_asn, *a_vloss;
-    pthread_rwlock_t ip_lock; /* writers: attach / detach; readers: snapshot builds */
-    iptable ips;
-    _Atomic uint64_t ip_version; /* bumped by every attach / detach */
-    _Atomic(ip_snap*) snap;
-    ip_snap* snap_retired;
-    pthread_mutex_t snap_lock;
+    pthread_rwlock_t ip_lock; /* writers: attach / detach; readers: the attached list */
+    _Atomic(iptab*) ips;      /* read with no lock (ipt_get) */
+    iptab* ips_retired;
+    size_t ips_nretired;
     _Atomic int32_t* att_index; /* [V] attached index or -1 (verticesWithAttachedHosts) */
     int32_t* attached;
     int32_t n_att, cap_att;
@@ -236,14 +247,18 @@ struct _Topology {
     /* the reference's path cache as a set of attached pairs (cache_resolve): bit j % 64 of
      * word i % 64 in the 64 x 64 tile (i / 64, j / 64), allocated on first store */
     _Atomic(_Atomic(uint64_t*)*)* srow;
-    pthread_mutex_t cache_lock; /* misses (the reference's pathCacheLock writer side) */
+    /* per attached source: the matrix size its Dijkstra store loop last ran for (one loop
+     * per source and target list: concurrent misses on the same source claim their own pair
+     * instead of repeating the O(A) loop) */
+    _Atomic int32_t* src_loop;
+    pthread_mutex_t min_lock; /* minimumPathLatency (the reference's pathCacheLock writer side) */
     int self_rule;
     double min_latency;
     double compute_s;
-    int64_t compute_count;   /* source rows computed on the GPU */
-    int64_t dijkstra_runs;   /* _topology_computeSourcePaths calls the reference would make */
-    int64_t self_count;      /* _topology_computeShortestPathToSelf calls */
-    int64_t cached_paths;    /* Paths in the emulated cache */
+    int64_t compute_count;          /* source rows computed on the GPU */
+    _Atomic int64_t dijkstra_runs;  /* _topology_computeSourcePaths calls the reference would make */
+    _Atomic int64_t self_count;     /* _topology_computeShortestPathToSelf calls */
+    _Atomic int64_t cached_paths;   /* Paths in the emulated cache */
 };
 /* ------------------------------------------------------------ attribute helpers
  * _topology_find{Vertex,Edge,Graph}Attribute{String,Double} (topology.c:284-369): a value
@@ -707,14 +722,6 @@ static void free_index(attach_index* x) {
     free(x);
 }
 
-static void free_snap(ip_snap* s) {
-    if (!s) return;
-    free(s->t.keys);
-    free(s->t.vals);
-    free(s->t.state);
-    free(s);
-}
-
 /* tile (ti, tj) of `words` u64 in a rows -> tiles table, allocated on first touch with a
  * compare-and-swap (no lock); NULL when out of range or out of memory */
 static uint64_t* tile_get(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd, int32_t ti, int32_t tj, size_t words) {
@@ -791,12 +798,78 @@ static uint64_t counter_peek(const Topology* top, int32_t i, int32_t j) {
                 : 0;
 }
 
-/* is the Path of attached pair (i, j) -- this direction -- in the emulated cache */
-static int stored_test(const Topology* top, int32_t i, int32_t j) {
-    uint64_t* tile = tile_peek(top->srow, top->ctd, i / CTILE, j / CTILE);
-    return tile && ((atomic_load_explicit((_Atomic uint64_t*)&tile[i % CTILE], memory_order_acquire) >>
-                     (j % CTILE)) & 1u);
+/* The emulated path cache's stored set (cache_resolve).  Directed graphs: one bit per
+ * ordered pair, bit j % 64 of word i % 64 of tile (i / 64, j / 64).  Undirected graphs: one
+ * 2-bit cell per unordered pair {a <= b} -- bit 0: (a, b) is cached, bit 1: (b, a) -- in
+ * tile (a / 64, b / 64), word 2 (a % 64) + (b % 64) / 32, so the direction that holds a
+ * pair is decided by ONE compare-and-swap: _topology_shouldStorePath's "neither direction
+ * cached yet" (topology.c:1309-1318) as an atomic claim, with no lock on the store path. */
+#define STILE_WORDS(top) ((top)->directed ? CTILE : 2 * CTILE)
+
+static _Atomic uint64_t* cell_word(const Topology* top, int32_t a, int32_t b, int alloc, int* shift) {
+    uint64_t* tile = alloc ? tile_get(top->srow, top->ctd, a / CTILE, b / CTILE, STILE_WORDS(top))
+                           : tile_peek(top->srow, top->ctd, a / CTILE, b / CTILE);
+    if (!tile) return NULL;
+    if (top->directed) {
+        *shift = b % CTILE;
+        return (_Atomic uint64_t*)&tile[a % CTILE];
+    }
+    *shift = 2 * (b % 32);
+    return (_Atomic uint64_t*)&tile[2 * (a % CTILE) + (b % CTILE) / 32];
 }
+
+/* which direction of attached pair (i, j) is cached: 1 = (i, j), 2 = (j, i) (undirected
+ * graphs only), 0 = neither */
+static int cached_dir(const Topology* top, int32_t i, int32_t j) {
+    int sh;
+    if (top->directed) {
+        _Atomic uint64_t* w = cell_word(top, i, j, 0, &sh);
+        return w && ((atomic_load_explicit(w, memory_order_acquire) >> sh) & 1u) ? 1 : 0;
+    }
+    const int32_t a = i < j ? i : j, b = i < j ? j : i;
+    _Atomic uint64_t* w = cell_word(top, a, b, 0, &sh);
+    const unsigned c = w ? (unsigned)((atomic_load_explicit(w, memory_order_acquire) >> sh) & 3u) : 0u;
+    if (!c) return 0;
+    if (i == j) return 1;
+    /* bit 0 holds (a, b): the forward direction when i < j */
+    return ((c & 1u) != 0) == (i < j) ? 1 : 2;
+}
+
+/* cache (i, j) unless the pair is cached already in either direction (undirected) or in
+ * this direction (directed: the drop-in keeps both directions); 1 when this
+ * call stored it */
+static int cache_claim(Topology* top, int32_t i, int32_t j) {
+    int sh;
+    if (top->directed) {
+        _Atomic uint64_t* w = cell_word(top, i, j, 1, &sh);
+        if (!w) return 0;
+        return !((atomic_fetch_or_explicit(w, 1ull << sh, memory_order_acq_rel) >> sh) & 1u);
+    }
+    const int32_t a = i < j ? i : j, b = i < j ? j : i;
+    _Atomic uint64_t* w = cell_word(top, a, b, 1, &sh);
+    if (!w) return 0;
+    const uint64_t bit = (i <= j ? 1ull : 2ull) << sh;
+    uint64_t cur = atomic_load_explicit(w, memory_order_acquire);
+    while (!((cur >> sh) & 3u))
+        if (atomic_compare_exchange_weak_explicit(w, &cur, cur | bit, memory_order_acq_rel, memory_order_acquire))
+            return 1;
+    return 0;
+}
+
+/* matrix cells are read by the getters while a late attach's fill_old_rows rewrites
+ * others: relaxed atomic accesses (plain moves on x86-64) */
+static inline double cell_d(const double* p) {
+    uint64_t u = __atomic_load_n((const uint64_t*)p, __ATOMIC_RELAXED);
+    double d;
+    memcpy(&d, &u, sizeof d);
+    return d;
+}
+static inline void cell_d_store(double* p, double d) {
+    uint64_t u;
+    memcpy(&u, &d, sizeof u);
+    __atomic_store_n((uint64_t*)p, u, __ATOMIC_RELAXED);
+}
+static inline uint8_t cell_k(const uint8_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 
 static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix* m, int32_t i, int32_t j,
                          uint64_t count, char* buf, size_t len) {
@@ -804,8 +877,8 @@ static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix
     size_t o = (size_t)i * m->A + j;
     snprintf(buf, len,
              "SourceIndex=%ld DestinationIndex=%ld Latency=%f Reliability=%f PacketCount=%lu isDirect=%s", (long)s,
-             (long)t, m->lat[o], m->rel[o], (unsigned long)count,
-             m->kind[o] == SHADOWTOPO_KIND_DIRECT ? "True" : "False");
+             (long)t, cell_d(&m->lat[o]), cell_d(&m->rel[o]), (unsigned long)count,
+             cell_k(&m->kind[o]) == SHADOWTOPO_KIND_DIRECT ? "True" : "False");
     (void)top;
     return buf;
 }
@@ -821,9 +894,18 @@ void topology_free(Topology* top) {
             for (int32_t tj = 0; tj < top->ctd; tj++) {
                 uint64_t* tile = tile_peek(top->srow, top->ctd, ti, tj);
                 if (!tile) continue;
-                for (int32_t a = 0; a < CTILE; a++) {
-                    for (uint64_t w = tile[a]; w; w &= w - 1) {
-                        int32_t i = ti * CTILE + a, j = tj * CTILE + __builtin_ctzll(w);
+                for (int32_t x = 0; x < STILE_WORDS(top); x++) {
+                    for (uint64_t w = tile[x]; w; w &= w - 1) {
+                        const int bit = __builtin_ctzll(w);
+                        int32_t i, j;
+                        if (top->directed) {
+                            i = ti * CTILE + x;
+                            j = tj * CTILE + bit;
+                        } else {  /* cell (a, b): bit 0 -> (a, b) cached, bit 1 -> (b, a) */
+                            const int32_t a = ti * CTILE + x / 2, b = tj * CTILE + (x % 2) * 32 + bit / 2;
+                            i = (bit & 1) ? b : a;
+                            j = (bit & 1) ? a : b;
+                        }
                         if (i >= m->A || j >= m->A) continue;
                         uint64_t c = counter_peek(top, i, j);
                         int32_t s = top->attached[i], t = top->attached[j];
@@ -842,7 +924,8 @@ void topology_free(Topology* top) {
         if (top->engs[k] && shadowtopo_get_stats(top->engs[k], &est) == SHADOWTOPO_OK) self_s += est.self_ms * 1e-3;
     st_message("path cache cleared, spent %f seconds computing %u shortest paths with dijkstra, "
                "and %f seconds computing %u shortest self paths",
-               top->compute_s, (unsigned)top->dijkstra_runs, self_s, (unsigned)top->self_count);
+               top->compute_s, (unsigned)atomic_load(&top->dijkstra_runs), self_s,
+               (unsigned)atomic_load(&top->self_count));
     free_matrix(m);
     for (matrix* r = top->retired; r;) {
         matrix* n = r->next;
@@ -851,19 +934,16 @@ void topology_free(Topology* top) {
     }
     tiles_free(top->crow, top->ctd);
     tiles_free(top->srow, top->ctd);
-    free_snap(atomic_load(&top->snap));
-    for (ip_snap* r = top->snap_retired; r;) {
-        ip_snap* n = r->next;
-        free_snap(r);
+    free(atomic_load(&top->ips));
+    for (iptab* r = top->ips_retired; r;) {
+        iptab* n = r->next;
+        free(r);
         r = n;
     }
     free_index(top->aidx);
     for (int32_t k = 0; k < top->ndev; k++)
         if (top->engs[k]) shadowtopo_destroy(top->engs[k]);
     top->eng = NULL;
-    free(top->ips.keys);
-    free(top->ips.vals);
-    free(top->ips.state);
     free((void*)top->att_index);
     free(top->attached);
     free(top->elat);
@@ -872,9 +952,9 @@ void topology_free(Topology* top) {
     gml_free(top->gml);
     pthread_rwlock_destroy(&top->ip_lock);
     pthread_mutex_destroy(&top->compute_lock);
-    pthread_mutex_destroy(&top->snap_lock);
     pthread_mutex_destroy(&top->idx_lock);
-    pthread_mutex_destroy(&top->cache_lock);
+    pthread_mutex_destroy(&top->min_lock);
+    free((void*)top->src_loop);
     top->magic = 0;
     free(top);
 }
@@ -894,11 +974,9 @@ Topology* topology_new(const char* graphPath) {
     top->magic = TOPO_MAGIC;
     pthread_rwlock_init(&top->ip_lock, NULL);
     pthread_mutex_init(&top->compute_lock, NULL);
-    pthread_mutex_init(&top->snap_lock, NULL);
     pthread_mutex_init(&top->idx_lock, NULL);
-    pthread_mutex_init(&top->cache_lock, NULL);
-    atomic_store(&top->ip_version, 1);
-    atomic_store(&top->snap, NULL);
+    pthread_mutex_init(&top->min_lock, NULL);
+    atomic_store(&top->ips, NULL);
     const char* dev = getenv("SHADOWTOPO_DEVICE");
     top->device = dev ? atoi(dev) : 0;
     top->ndev = 1;
@@ -957,6 +1035,8 @@ Topology* topology_new(const char* graphPath) {
     }
     top->att_index = malloc(sizeof(*top->att_index) * (size_t)(top->V > 0 ? top->V : 1));
     for (int32_t v = 0; v < top->V; v++) atomic_init(&top->att_index[v], -1);
+    top->src_loop = malloc(sizeof(*top->src_loop) * (size_t)(top->V > 0 ? top->V : 1));
+    for (int32_t v = 0; v < top->V; v++) atomic_init(&top->src_loop[v], 0);
     top->ctd = (top->V + CTILE - 1) / CTILE;
     top->crow = calloc((size_t)(top->ctd > 0 ? top->ctd : 1), sizeof(*top->crow));
     top->srow = calloc((size_t)(top->ctd > 0 ? top->ctd : 1), sizeof(*top->srow));
@@ -1256,7 +1336,8 @@ void topology_attach(Topology* top, Address* address, Random* randomSourcePool, 
         return;
     }
     pthread_rwlock_wrlock(&top->ip_lock);
-    ipt_put(&top->ips, node_ip, v);
+    if (ipt_put(&top->ips, &top->ips_retired, &top->ips_nretired, node_ip, v))
+        st_critical("out of memory for the IP table; address '%s' stays unconnected", address_toHostIPString(address));
     if (atomic_load_explicit(&top->att_index[v], memory_order_relaxed) < 0) {
         if (top->n_att == top->cap_att) {
             top->cap_att = top->cap_att ? top->cap_att * 2 : 256;
@@ -1266,7 +1347,6 @@ void topology_attach(Topology* top, Address* address, Random* randomSourcePool, 
         atomic_store_explicit(&top->att_index[v], top->n_att, memory_order_release);
         top->n_att++;
     }
-    atomic_fetch_add_explicit(&top->ip_version, 1, memory_order_release);
     pthread_rwlock_unlock(&top->ip_lock);
     double x;
     if (bwUpOut) *bwUpOut = vnum(top->a_bwup, v, &x) ? (uint64_t)x : 0;
@@ -1290,8 +1370,7 @@ void topology_detach(Topology* top, Address* address) {
     if (!top || !address) return;
     uint32_t ip = address_toNetworkIP(address);
     pthread_rwlock_wrlock(&top->ip_lock);
-    ipt_del(&top->ips, ip);
-    atomic_fetch_add_explicit(&top->ip_version, 1, memory_order_release);
+    ipt_del(&top->ips, ip);  /* one tombstone store: lookups see it at once, nothing is rebuilt */
     pthread_rwlock_unlock(&top->ip_lock);
 }
 /* ------------------------------------------------------------ eager computation */
@@ -1447,7 +1526,7 @@ static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A,
             m->kind[o] = m->kind[r];
         }
     }
-    m->partial = A0;
+    atomic_store_explicit(&m->partial, A0, memory_order_release);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     top->compute_count += A - A0;
@@ -1497,56 +1576,64 @@ static matrix* current_matrix(Topology* top, int32_t need) {
 
 /* Rows [0, m->partial) of an undirected late-attach matrix with their own entries for the
  * columns the late attach added (compute_matrix copied the reverse direction there):
- * needed once an old source's paths enter the cache (the reference reruns that source's
- * Dijkstra against the grown target list).  Only entries that differ are written, so a
- * reader of a cached entry never sees a store.  Caller holds cache_lock. */
+ * needed once an old source's entry for a new target is read (the reference reruns that
+ * source's Dijkstra against the grown target list).  In place, under compute_lock (once per
+ * matrix: a thread that waited finds partial == 0), with relaxed atomic cell stores; then
+ * partial = 0 with release order.  No reader reads those cells before: cache_resolve fills
+ * before it returns such an entry, and every (i, t) it caches is claimed after the fill. */
 static int fill_old_rows(Topology* top, matrix* m) {
-    const int32_t P = m->partial, A = m->A;
-    if (P <= 0) return 0;
+    if (atomic_load_explicit(&m->partial, memory_order_acquire) <= 0) return 0;
     pthread_mutex_lock(&top->compute_lock);
-    int rc = -1;
-    int32_t* att = malloc(sizeof(int32_t) * (size_t)A);
-    matrix tmp;
-    memset(&tmp, 0, sizeof tmp);
-    tmp.A = A;
-    tmp.lat = malloc(sizeof(double) * (size_t)P * (size_t)A);
-    tmp.rel = malloc(sizeof(double) * (size_t)P * (size_t)A);
-    tmp.kind = malloc((size_t)P * (size_t)A);
-    if (att && tmp.lat && tmp.rel && tmp.kind) {
-        pthread_rwlock_rdlock(&top->ip_lock);
-        memcpy(att, top->attached, sizeof(int32_t) * (size_t)A);  /* attach order: a stable prefix */
-        pthread_rwlock_unlock(&top->ip_lock);
-        struct timespec t0, t1;
-        clock_gettime(CLOCK_MONOTONIC, &t0);
-        if (ensure_engine(top) == 0 && compute_rows_sharded(top, att, A, 0, P, &tmp) == 0) {
-            for (size_t o = 0; o < (size_t)P * (size_t)A; o++) {
-                if (memcmp(&m->lat[o], &tmp.lat[o], sizeof(double))) m->lat[o] = tmp.lat[o];
-                if (memcmp(&m->rel[o], &tmp.rel[o], sizeof(double))) m->rel[o] = tmp.rel[o];
-                if (m->kind[o] != tmp.kind[o]) m->kind[o] = tmp.kind[o];
+    const int32_t P = atomic_load_explicit(&m->partial, memory_order_acquire), A = m->A;
+    int rc = P <= 0 ? 0 : -1;
+    if (P > 0) {
+        int32_t* att = malloc(sizeof(int32_t) * (size_t)A);
+        matrix tmp;
+        memset(&tmp, 0, sizeof tmp);
+        tmp.A = A;
+        tmp.lat = malloc(sizeof(double) * (size_t)P * (size_t)A);
+        tmp.rel = malloc(sizeof(double) * (size_t)P * (size_t)A);
+        tmp.kind = malloc((size_t)P * (size_t)A);
+        if (att && tmp.lat && tmp.rel && tmp.kind) {
+            pthread_rwlock_rdlock(&top->ip_lock);
+            memcpy(att, top->attached, sizeof(int32_t) * (size_t)A);  /* attach order: a stable prefix */
+            pthread_rwlock_unlock(&top->ip_lock);
+            struct timespec t0, t1;
+            clock_gettime(CLOCK_MONOTONIC, &t0);
+            if (ensure_engine(top) == 0 && compute_rows_sharded(top, att, A, 0, P, &tmp) == 0) {
+                for (int32_t i = 0; i < P; i++)
+                    for (int32_t t = P; t < A; t++) {
+                        const size_t o = (size_t)i * (size_t)A + (size_t)t;
+                        cell_d_store(&m->lat[o], tmp.lat[o]);
+                        cell_d_store(&m->rel[o], tmp.rel[o]);
+                        __atomic_store_n(&m->kind[o], tmp.kind[o], __ATOMIC_RELAXED);
+                    }
+                atomic_store_explicit(&m->partial, 0, memory_order_release);
+                top->compute_count += P;
+                rc = 0;
             }
-            m->partial = 0;
-            top->compute_count += P;
-            rc = 0;
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
         }
-        clock_gettime(CLOCK_MONOTONIC, &t1);
-        top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        free(att);
+        free(tmp.lat);
+        free(tmp.rel);
+        free(tmp.kind);
     }
-    free(att);
-    free(tmp.lat);
-    free(tmp.rel);
-    free(tmp.kind);
     pthread_mutex_unlock(&top->compute_lock);
     if (rc) st_critical("recomputing the rows of hosts attached before a late attach failed");
     return rc;
 }
 
-/* _topology_storePathInCache (topology.c:1336-1386) for attached pair (i, j) of m, whose
- * _topology_shouldStorePath checks the caller made; returns the stored latency */
-static double cache_store(Topology* top, const matrix* m, int32_t i, int32_t j) {
-    uint64_t* tile = tile_get(top->srow, top->ctd, i / CTILE, j / CTILE, CTILE);
-    if (tile) atomic_fetch_or_explicit((_Atomic uint64_t*)&tile[i % CTILE], 1ull << (j % CTILE), memory_order_release);
-    top->cached_paths++;
-    return m->lat[(size_t)i * m->A + j];
+/* the running minimum (topology.c:1374-1385: `minimumPathLatency == 0 || lower`), and the
+ * upcall after the lock is released, as the reference makes it */
+static void note_min_latency(Topology* top, double mn) {
+    pthread_mutex_lock(&top->min_lock);
+    const int upd = top->min_latency == 0 || mn < top->min_latency;
+    if (upd) top->min_latency = mn;
+    const double cur = top->min_latency;
+    pthread_mutex_unlock(&top->min_lock);
+    if (upd) worker_updateMinTimeJump(cur);
 }
 
 /* The reference's path cache over the eager matrix.  Every value is computed up front; what
@@ -1564,117 +1651,83 @@ static double cache_store(Topology* top, const matrix* m, int32_t i, int32_t j) 
  *                _topology_shouldStorePath accepts (:1309-1334: neither direction cached
  *                yet; not a non-direct path where the graph prefers an existing direct
  *                edge), t' = s included with the configured self value.
- * Returns the cached direction in (si, sj), or -1 when the pair has no path. */
+ * No lock: each store is an atomic claim of its pair (cache_claim), so concurrent misses
+ * serialise per pair exactly as some order of the reference's would; the O(A) store loop
+ * runs once per source and target list (src_loop), a concurrent miss on the same source
+ * claiming just its own pair.  Returns the cached direction in (si, sj), or -1 when the
+ * pair has no path. */
 static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32_t* si, int32_t* sj) {
     matrix* m = *mp;
-    if (stored_test(top, i, j)) goto fwd;
-    if (!top->directed && stored_test(top, j, i)) goto rev;
-    pthread_mutex_lock(&top->cache_lock);
-    if (stored_test(top, i, j)) {
-        pthread_mutex_unlock(&top->cache_lock);
-        goto fwd;
-    }
-    if (!top->directed && stored_test(top, j, i)) {
-        pthread_mutex_unlock(&top->cache_lock);
-        goto rev;
-    }
-    /* a late attach may have published a larger matrix meanwhile: its target list is the
-     * one the reference's Dijkstra would use now */
-    matrix* cur = atomic_load_explicit(&top->mat, memory_order_acquire);
-    if (cur && cur->A > (i > j ? i : j)) *mp = m = cur;
-    const int32_t A = m->A;
-    const uint8_t k = m->kind[(size_t)i * A + j];
-    double mn = 0.0;
-    int stored = 0;
-    if (k == SHADOWTOPO_KIND_DIRECT || top->complete) {
-        if (k == SHADOWTOPO_KIND_DIRECT) {  /* a complete graph without the edge: get_eid fails */
-            mn = cache_store(top, m, i, j);
-            stored = 1;
-        }
-    } else if (i == j) {
-        top->self_count++;
-        if (k != SHADOWTOPO_KIND_NONE) {
-            mn = cache_store(top, m, i, i);
-            stored = 1;
-        }
-    } else {
-        top->dijkstra_runs++;
-        if (i < m->partial && fill_old_rows(top, m)) {
-            pthread_mutex_unlock(&top->cache_lock);
-            return -1;
-        }
-        const uint8_t* kr = m->kind + (size_t)i * A;
-        for (int32_t t = 0; t < A; t++) {
-            /* reachable targets only (an empty igraph path is never stored); a pair whose
-             * rule is the direct edge is not stored from a Dijkstra run */
-            if (kr[t] == SHADOWTOPO_KIND_NONE || kr[t] == SHADOWTOPO_KIND_DIRECT) continue;
-            if (stored_test(top, i, t) || (!top->directed && stored_test(top, t, i))) continue;
-            const double l = cache_store(top, m, i, t);
-            if (!stored || l < mn) mn = l;
-            stored = 1;
-        }
-    }
-    /* the running minimum (topology.c:1374-1385: `minimumPathLatency == 0 || lower`) */
-    if (stored && (top->min_latency == 0 || mn < top->min_latency)) {
-        top->min_latency = mn;
-        worker_updateMinTimeJump(top->min_latency);
-    }
-    const int fwd_ok = stored_test(top, i, j), rev_ok = !top->directed && stored_test(top, j, i);
-    pthread_mutex_unlock(&top->cache_lock);
-    if (fwd_ok) goto fwd;
-    if (rev_ok) goto rev;
-    return -1;
-fwd:
-    *si = i;
-    *sj = j;
-    return 0;
-rev:
-    *si = j;
-    *sj = i;
-    return 0;
-}
-
-/* IP -> vertex snapshot for the per-packet path: rebuilt (under snap_lock) only when an
- * attach / detach bumped the version since the last one; lookups then take no lock */
-static const ip_snap* query_snap(Topology* top) {
-    ip_snap* s = atomic_load_explicit(&top->snap, memory_order_acquire);
-    if (s && s->version == atomic_load_explicit(&top->ip_version, memory_order_acquire)) return s;
-    pthread_mutex_lock(&top->snap_lock);
-    s = atomic_load_explicit(&top->snap, memory_order_acquire);
-    if (!s || s->version != atomic_load_explicit(&top->ip_version, memory_order_acquire)) {
-        ip_snap* n = calloc(1, sizeof(ip_snap));
-        if (n) {
-            pthread_rwlock_rdlock(&top->ip_lock);
-            n->version = atomic_load_explicit(&top->ip_version, memory_order_acquire);
-            n->t = top->ips;
-            size_t cap = top->ips.cap;
-            n->t.keys = cap ? malloc(sizeof(uint32_t) * cap) : NULL;
-            n->t.vals = cap ? malloc(sizeof(int32_t) * cap) : NULL;
-            n->t.state = cap ? malloc(cap) : NULL;
-            if (cap && n->t.keys && n->t.vals && n->t.state) {
-                memcpy(n->t.keys, top->ips.keys, sizeof(uint32_t) * cap);
-                memcpy(n->t.vals, top->ips.vals, sizeof(int32_t) * cap);
-                memcpy(n->t.state, top->ips.state, cap);
-            } else if (cap) {
-                n->t.cap = 0;
+    int d = cached_dir(top, i, j);
+    if (!d) {
+        /* a late attach may have published a larger matrix meanwhile: its target list is the
+         * one the reference's Dijkstra would use now */
+        matrix* cur = atomic_load_explicit(&top->mat, memory_order_acquire);
+        if (cur && cur->A > (i > j ? i : j)) *mp = m = cur;
+        const int32_t A = m->A;
+        /* an old source's own entries before any of them is cached (or, below, read) */
+        if (i < atomic_load_explicit(&m->partial, memory_order_acquire) && fill_old_rows(top, m)) return -1;
+        const uint8_t k = cell_k(&m->kind[(size_t)i * A + j]);
+        double mn = 0.0;
+        int64_t stored = 0;
+        if (k == SHADOWTOPO_KIND_DIRECT || top->complete) {
+            /* a complete graph without the edge: get_eid fails, nothing is stored */
+            if (k == SHADOWTOPO_KIND_DIRECT && cache_claim(top, i, j)) {
+                mn = cell_d(&m->lat[(size_t)i * A + j]);
+                stored = 1;
             }
-            pthread_rwlock_unlock(&top->ip_lock);
-            if (s) {
-                s->next = top->snap_retired;
-                top->snap_retired = s;
+        } else if (i == j) {
+            atomic_fetch_add_explicit(&top->self_count, 1, memory_order_relaxed);
+            if (k != SHADOWTOPO_KIND_NONE && cache_claim(top, i, i)) {
+                mn = cell_d(&m->lat[(size_t)i * A + i]);
+                stored = 1;
             }
-            atomic_store_explicit(&top->snap, n, memory_order_release);
-            s = n;
+        } else {
+            atomic_fetch_add_explicit(&top->dijkstra_runs, 1, memory_order_relaxed);
+            int32_t ran = atomic_load_explicit(&top->src_loop[i], memory_order_acquire);
+            int mine = 0;
+            while (ran < A && !(mine = atomic_compare_exchange_weak_explicit(&top->src_loop[i], &ran, A,
+                                                                             memory_order_acq_rel,
+                                                                             memory_order_acquire))) {
+            }
+            const uint8_t* kr = m->kind + (size_t)i * A;
+            const int32_t t0 = mine ? 0 : j, t1 = mine ? A : j + 1;
+            for (int32_t t = t0; t < t1; t++) {
+                /* reachable targets only (an empty igraph path is never stored); a pair whose
+                 * rule is the direct edge is not stored from a Dijkstra run */
+                const uint8_t kt = cell_k(&kr[t]);
+                if (kt == SHADOWTOPO_KIND_NONE || kt == SHADOWTOPO_KIND_DIRECT) continue;
+                if (!cache_claim(top, i, t)) continue;
+                const double l = cell_d(&m->lat[(size_t)i * A + t]);
+                if (!stored || l < mn) mn = l;
+                stored++;
+            }
         }
+        if (stored) {
+            atomic_fetch_add_explicit(&top->cached_paths, stored, memory_order_relaxed);
+            note_min_latency(top, mn);
+        }
+        d = cached_dir(top, i, j);
+        if (!d) return -1;
     }
-    pthread_mutex_unlock(&top->snap_lock);
-    return s;
+    *si = d == 1 ? i : j;
+    *sj = d == 1 ? j : i;
+    /* the entry's own row: a matrix whose rows [0, partial) still hold reverse copies in the
+     * late attach's columns is swapped for the current one (filled before any of those
+     * entries was cached) or filled now (an entry cached before the late attach) */
+    int32_t p = atomic_load_explicit(&m->partial, memory_order_acquire);
+    if (*si < p && *sj >= p) {
+        matrix* cur = atomic_load_explicit(&top->mat, memory_order_acquire);
+        if (cur && cur->A > (*si > *sj ? *si : *sj)) *mp = m = cur;
+        p = atomic_load_explicit(&m->partial, memory_order_acquire);
+        if (*si < p && *sj >= p && fill_old_rows(top, m)) return -1;
+    }
+    return 0;
 }
 
 static int32_t connected_vertex(Topology* top, Address* a) {
-    /* _topology_getConnectedVertexIndex, topology.c:1388-1405, on the lock-free snapshot */
-    const ip_snap* s = query_snap(top);
-    int32_t v = s ? ipt_get(&s->t, address_toNetworkIP(a)) : -1;
+    /* _topology_getConnectedVertexIndex, topology.c:1388-1405, with no lock (ipt_get) */
+    int32_t v = ipt_get(atomic_load_explicit(&top->ips, memory_order_acquire), address_toNetworkIP(a));
     if (v < 0) st_warning("address %s is not connected to the topology", address_toHostIPString(a));
     return v;
 }
@@ -1711,13 +1764,13 @@ static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off
 double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress) {
     size_t o;
     matrix* m = path_entry(top, srcAddress, dstAddress, &o, NULL, NULL);
-    return m ? m->lat[o] : -1.0;
+    return m ? cell_d(&m->lat[o]) : -1.0;
 }
 
 double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress) {
     size_t o;
     matrix* m = path_entry(top, srcAddress, dstAddress, &o, NULL, NULL);
-    return m ? m->rel[o] : -1.0;
+    return m ? cell_d(&m->rel[o]) : -1.0;
 }
 
 int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress) {
@@ -1786,17 +1839,25 @@ int topology_hip_get_info(Topology* top, topology_hip_info* out) {
     out->computed_for = m ? m->A : 0;
     out->device = top->device;
     out->n_devices = top->ndev;
+    pthread_mutex_lock(&top->min_lock);
     out->min_path_latency = top->min_latency;
+    pthread_mutex_unlock(&top->min_lock);
     out->compute_seconds = top->compute_s;
     out->compute_count = top->compute_count;
-    out->dijkstra_runs = top->dijkstra_runs;
-    out->self_path_count = top->self_count;
-    out->cached_paths = top->cached_paths;
+    out->dijkstra_runs = atomic_load(&top->dijkstra_runs);
+    out->self_path_count = atomic_load(&top->self_count);
+    out->cached_paths = atomic_load(&top->cached_paths);
     shadowtopo_stats est;
     for (int32_t k = 0; k < top->ndev; k++)
         if (top->engs[k] && shadowtopo_get_stats(top->engs[k], &est) == SHADOWTOPO_OK)
             out->self_seconds += est.self_ms * 1e-3;
     out->compute_failed = top->compute_failed;
+    pthread_rwlock_rdlock(&top->ip_lock);
+    const iptab* it = atomic_load(&top->ips);
+    out->ip_table_slots = it ? (int64_t)it->cap : 0;
+    out->ip_tables_retired = (int64_t)top->ips_nretired;
+    for (const iptab* r = top->ips_retired; r; r = r->next) out->ip_retired_bytes += (int64_t)(sizeof(iptab) + r->cap * 8);
+    pthread_rwlock_unlock(&top->ip_lock);
     return 0;
 }
 
@@ -1809,9 +1870,7 @@ int32_t topology_hip_attached(Topology* top, int32_t* out, int32_t cap) {
 
 int32_t topology_hip_vertex_of_ip(Topology* top, uint32_t ip) {
     if (!top) return -1;
-    pthread_rwlock_rdlock(&top->ip_lock);
-    int32_t v = ipt_get(&top->ips, ip);
-    pthread_rwlock_unlock(&top->ip_lock);
+    int32_t v = ipt_get(atomic_load_explicit(&top->ips, memory_order_acquire), ip);
     return v;
 }
 

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libshadowtopo_hip.so")
+LIB_PATH = os.environ.get("SHADOWTOPO_EXP_LIB") or os.path.join(HERE, "_build", "libshadowtopo_hip.so")
 
 F_DIRECTED = 0x1
 F_COMPLETE = 0x2

@@ -36,8 +36,11 @@ def chunk_rows(per: int, chunks: int):
 
 
 def packed_bytes(rows: int, A: int) -> int:
-    """one chunk's lat (f64) + rel (f64) + hops (i32) rows in one buffer"""
-    return rows * A * 20
+    """one chunk's lat (f64) + rel (f64) + hops (i32) rows in one buffer, padded to a multiple
+    of 256 bytes: rank r's part of the all-gathered buffer starts at r * packed_bytes, and its
+    f64 views need 8-byte alignment (rows * A odd would otherwise leave ranks >= 1 at an offset
+    of 4 mod 8)"""
+    return -(-rows * A * 20 // 256) * 256
 
 
 def pack_views(buf, rows: int, A: int):

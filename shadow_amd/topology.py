@@ -37,6 +37,7 @@ class Info(ctypes.Structure):
         ("compute_count", ctypes.c_int64), ("n_devices", ctypes.c_int32), ("compute_failed", ctypes.c_int32),
         ("dijkstra_runs", ctypes.c_int64), ("self_path_count", ctypes.c_int64), ("cached_paths", ctypes.c_int64),
         ("self_seconds", ctypes.c_double),
+        ("ip_table_slots", ctypes.c_int64), ("ip_tables_retired", ctypes.c_int64), ("ip_retired_bytes", ctypes.c_int64),
     ]
 
     def as_dict(self):

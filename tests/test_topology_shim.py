@@ -360,3 +360,56 @@ def test_c_harness_ingest_and_attach(tmp_path, mode):
     res = run_harness(build_harness(tmp_path), path, 500, 1, 0, mode)
     assert res["vertices"] == 300 and res["hosts"] == 500
     assert 0 < res["attached"] <= 300
+
+
+def test_ip_table_lookups_through_attach_detach_churn(tmp_path):
+    """The per-packet IP -> vertex table (topology_hip.c iptab, read with no lock): lookups of
+    stable hosts from several threads stay right while another thread attaches and detaches
+    other hosts (table growth and tombstone rehashes replace the table under the readers),
+    and the memory the retired tables keep stays bounded by the churn (one full
+    snapshot per detach before)."""
+    import threading
+    g, text, _ = attach_graph(n=200, seed=13)
+    top = T.Topology.new(write(tmp_path, "ipt.xml", text))
+    rnd = T.Random(9)
+    stable = [T.Address(f"12.0.{k // 200}.{k % 200 + 1}") for k in range(300)]
+    for a in stable:
+        top.attach(a, rnd)
+    want = {a.ip: top.vertex_of_ip(a.ip) for a in stable}
+    assert all(v >= 0 for v in want.values())
+    stop = threading.Event()
+    bad = []
+
+    def reader(seed):
+        rng = np.random.default_rng(seed)
+        n = 0
+        while not stop.is_set() or n < 2000:
+            a = stable[rng.integers(0, len(stable))]
+            if top.vertex_of_ip(a.ip) != want[a.ip]:
+                bad.append(a.ip)
+            n += 1
+
+    threads = [threading.Thread(target=reader, args=(s,)) for s in range(4)]
+    for t in threads:
+        t.start()
+    churn = [T.Address(f"13.{k // 60000}.{(k // 250) % 240}.{k % 250 + 1}") for k in range(2500)]
+    detaches = 0
+    for rnd_i in range(2):
+        for a in churn:
+            top.attach(a, rnd)
+        for a in churn[: 2000]:
+            top.detach(a)
+            detaches += 1
+            assert top.vertex_of_ip(a.ip) == -1
+    stop.set()
+    for t in threads:
+        t.join()
+    assert not bad, f"{len(bad)} wrong lookups of stable hosts during churn"
+    for a in churn[2000:]:
+        assert top.vertex_of_ip(a.ip) >= 0
+    inf = top.info()
+    assert inf["ip_table_slots"] >= 2 * (len(stable) + 500) and inf["ip_tables_retired"] >= 2
+    # growth retires tables half the size of their successor; tombstone rehashes need
+    # cap / 4 detaches each: bounded by the live table plus 32 bytes per detach
+    assert inf["ip_retired_bytes"] <= 8 * inf["ip_table_slots"] + 32 * detaches + 4096 * inf["ip_tables_retired"]
+    top.free()
