@@ -136,7 +136,7 @@ def cpu_baseline(g, n_sources, budget_s=20.0, all_cores=16):
     return out
 
 
-def roofline_of(st, g, config, scale, world, rows, steps, csr_variant=1, dense_variant=0):
+def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0):
     """Roofline of the dominant kernel, timed with HIP events on the engine's stream around
     every launch: the f32 dense full sweep (k_relax_dense_f) on complete-ish graphs, the CSR
     relax rounds (k_relax, with the k_relax_wl worklist rounds) otherwise.  achieved = that
@@ -151,7 +151,7 @@ def roofline_of(st, g, config, scale, world, rows, steps, csr_variant=1, dense_v
     else:
         # every relax round of the step (grid and worklist launches alike): achieved = the
         # step's compulsory bytes / the relax kernels' time in the step
-        kname = {0: "k_relax_delta", 1: "k_relax", 2: "k_relax_st", 3: "k_relax_cm"}[csr_variant]
+        kname = "k_relax"
         launches, kms = max(1, st["relax_launches"]), st["relax_ms"]
         bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * steps / launches
         batches_per_launch = st["relax_batches"] / launches
@@ -178,7 +178,7 @@ def roofline_of(st, g, config, scale, world, rows, steps, csr_variant=1, dense_v
                             "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
                             "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
                                     "waves / SQ_WAVES; peak = one wave64 VALU issue per 2 cycles per SIMD-32 at 2.4 GHz"}
-    if not st["dense"] and st["wl_launches"] and csr_variant == 1:
+    if not st["dense"] and st["wl_launches"]:
         roofline["worklist_kernel"] = {"kernel": "k_relax_wl", "avg_launch_ms": st["wl_ms"] / st["wl_launches"],
                                        "launches_per_step": st["wl_launches"] / steps}
     if st["dense"] and st["delta_sweeps"]:
@@ -329,6 +329,54 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
         eng.close()
 
 
+def shim_host_matrix(ndev, config="C4", hosts=10_000):
+    """The drop-in's own multi-GPU path, as Shadow runs it (one process): topology_new on the
+    config's GraphML, `hosts` host attaches (no hints: the reference's random vertex pick,
+    topology.c:2327-2333), then topology_hip_prepare with one engine per device
+    (topology_hip_set_devices: device k computes a contiguous block of source rows on its
+    own host thread straight into the shim's page-locked lat / rel / kind matrix,
+    topology_hip.c compute_rows_sharded).  The prepare time is the whole one-shot build a
+    Shadow run pays: engines (graph upload + device build), locality keys, rounds, compose
+    and the PCIe copies into host memory."""
+    import tempfile
+    from shadow_amd import synth
+    from shadow_amd import topology as T
+    g, _per, desc = build_workload(config, 1, 1.0)
+    T.set_log_level(1)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "topology.graphml.xml")
+        with open(path, "w") as f:
+            f.write(synth.to_graphml(g))
+        t0 = time.perf_counter()
+        top = T.Topology.new(path)
+        ingest_s = time.perf_counter() - t0
+    if top is None:
+        return {"error": "topology_new failed"}
+    try:
+        rnd = T.Random(12345)
+        addrs = [T.Address(f"11.{k >> 16 & 255}.{k >> 8 & 255}.{(k & 255) or 1}" if k & 255 else
+                           f"12.{k >> 16 & 255}.{k >> 8 & 255}.1") for k in range(hosts)]
+        t0 = time.perf_counter()
+        for a in addrs:
+            top.attach(a, rnd)
+        attach_s = time.perf_counter() - t0
+        top.set_devices(list(range(ndev)))
+        t0 = time.perf_counter()
+        rc = top.prepare()
+        prep = time.perf_counter() - t0
+        inf = top.info()
+        A = inf["computed_for"]
+        return {"workload": desc + f" (GraphML through topology_new, {hosts} hosts attached with no hints)",
+                "devices": ndev, "attached": inf["n_attached"], "rc": rc,
+                "ingest_s": ingest_s, "attach_s": attach_s, "prepare_ms": prep * 1e3,
+                "compute_ms": inf["compute_seconds"] * 1e3,
+                "host_matrix_bytes": A * A * 17, "host_matrix_GBps": A * A * 17 / prep / 1e9 if prep > 0 else None,
+                "note": "host-side (page-locked) matrix build time of the drop-in, PCIe included; "
+                        "cold: engine creation on every device included"}
+    finally:
+        top.free()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -341,6 +389,8 @@ def main():
     ap.add_argument("--cpu-sources", type=int, default=12)
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the C4 north-star record (sharded over the ranks) the default C2 run adds to its line")
+    ap.add_argument("--no-shim", action="store_true",
+                    help="skip the drop-in's in-process multi-GPU host-matrix build (C4 through topology_new)")
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
@@ -350,9 +400,6 @@ def main():
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists when under half the pairs are active (1, default), "
                          "always (2), or the full grid (0)")
-    ap.add_argument("--csr-variant", type=int, default=1,
-                    help="3 = changed (tail, source) pairs over worklists, 1 = full recomputation, "
-                         "2 = changed tails with stamped f32 keys, 0 = f64 delta rounds")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -402,7 +449,6 @@ def main():
     if args.dense_tb:
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
-    eng.set_option(E.OPT_CSR_VARIANT, args.csr_variant)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
@@ -435,8 +481,7 @@ def main():
 
     # roofline of the dominant kernel, timed with HIP events on the engine's stream around
     # every launch
-    roofline = roofline_of(st, g, args.config, args.scale, world, rows, args.steps, args.csr_variant,
-                           args.dense_variant)
+    roofline = roofline_of(st, g, args.config, args.scale, world, rows, args.steps, args.dense_variant)
 
     # the drop-in boundary hands host buffers over (topology_hip.c: MEM_HOST); its
     # PCIe-inclusive rate, measured once outside the timed region (never `value`)
@@ -469,6 +514,19 @@ def main():
         except Exception as e:  # report, never fake
             north = {"error": f"{type(e).__name__}: {e}"}
 
+    # the drop-in's in-process multi-GPU path (one engine per device, rows straight into the
+    # shim's page-locked host matrix): rank 0 drives every GPU of the node while the other
+    # ranks wait at the barrier
+    shim = None
+    if args.config == "C2" and args.scale == 1.0 and not args.no_north_star and not args.no_shim:
+        if rank == 0:
+            try:
+                shim = shim_host_matrix(world)
+            except Exception as e:  # report, never fake
+                shim = {"error": f"{type(e).__name__}: {e}"}
+        if world > 1:
+            dist.barrier()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -497,6 +555,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "north_star": north,
+            "shim_host_matrix": shim,
             "engine": {"rounds_per_step": st["rounds"] / args.steps, "replayed_sources": st["replayed_sources"],
                        "relax_ms_per_step": st["relax_ms"] / args.steps,
                        "compose_ms_per_step": st["compose_ms"] / args.steps, "dense": st["dense"],

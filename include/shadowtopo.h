@@ -78,7 +78,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
                                               (vertex, source) pairs gets a change-mask delta round instead of a full
                                               sweep (default 125; 0 = always full sweeps) */
-#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default), _MASKED, _FILTERED or _DELTA */
+#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (the only one) */
 #define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
 #define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Hilbert
                                               order of the top two principal axes of the distances to eight
@@ -113,24 +113,12 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (55 % of free HBM, at least 24 GB) this
                                               engine may take (default 1000); engines sharing one device split it */
 
-/* sparse (CSR) relaxation rounds (all exact, same fixed point):
- *   FULL (default): recompute every active vertex's minimum over all its in-arcs' 512-byte
- *     distance rows (k_relax; rounds with few active pairs run over frontier worklists);
- *   MASKED: over frontier worklists, fold only the (in-neighbour, source) pairs whose state
- *     changed, found through per-vertex round-stamped change records; the wave compacts the
- *     changed in-arcs with a ballot and loads their distance rows masked to the changed
- *     lanes; the vertex's own state is read only for lanes with a candidate (k_relax_cm);
- *   FILTERED: fold only the in-neighbours whose state changed, found through round stamps
- *     in 256-byte f32 key rows, settling the f32-filter survivors in f64 (k_relax_st);
- *   DELTA: fold only changed in-neighbours, found through 64-bit change masks, in f64,
- *     over the whole grid.
- * MASKED, FILTERED and DELTA read fewer rows but issue more instructions: on C4 MASKED
- * fetches 12 % fewer bytes at 2.2x the VALU instructions and runs 1.3x longer than FULL
- * (DESIGN.md 4); they are kept as cross-checks. */
-#define SHADOWTOPO_CSR_DELTA 0
+/* sparse (CSR) relaxation rounds: every active vertex's minimum is recomputed over all its
+ * in-arcs' 512-byte distance rows (k_relax; rounds with few active pairs run over frontier
+ * worklists, k_relax_wl / k_relax_wlp).  Changed-tail variants (masked, stamped-key, delta)
+ * read fewer rows but issued more instructions and were slower on every config;
+ * they were removed in r03. */
 #define SHADOWTOPO_CSR_FULL 1
-#define SHADOWTOPO_CSR_FILTERED 2
-#define SHADOWTOPO_CSR_MASKED 3
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;

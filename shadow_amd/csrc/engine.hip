@@ -101,16 +101,6 @@ typedef __attribute__((address_space(1))) uint32_t guint;
 typedef __attribute__((address_space(1))) int32_t gint;
 typedef __attribute__((address_space(1))) uint8_t gbyte;
 
-// Change record of one vertex in one batch, for the CSR masked rounds (k_relax_cm): the
-// lanes (sources) whose state changed in round rd[p], one record per round parity p.  A
-// reader in round r takes the records stamped r - 1 or r; a record from an older round is
-// stale and ignored, so nothing is ever cleared between rounds.
-struct alignas(32) CMask {
-    unsigned long long m[2];
-    uint32_t rd[2];
-    uint32_t pad_[2];
-};
-
 struct Pools {
     double* D;          // [slot][Vp][64] distance
     uint32_t* H;        // [slot][Vp][64] hops | TAINT
@@ -122,8 +112,7 @@ struct Pools {
     unsigned long long* mask;  // [slot] lanes whose rows need the heap-exact replay
     double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
     unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
-    float* D32;         // [slot][Vp][64] f32 filter key (dense: distance rounded down; CSR: stamped, see stamp_key)
-    CMask* cm;          // CSR masked rounds: [slot][Vp] change records
+    float* D32;         // dense mode: [slot][Vp][64] f32 filter key (distance rounded down, NaN unreached)
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -143,7 +132,6 @@ struct BatchDev {
     unsigned long long* chm0;
     unsigned long long* chm1;
     gfloat* D32;
-    CMask* cm;
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
     __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
@@ -164,7 +152,6 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.chm0 = p.chm ? p.chm + (size_t)b * 2 * p.Vp : nullptr;
     B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
     B.D32 = p.D32 ? (gfloat*)(p.D32 + o) : nullptr;
-    B.cm = p.cm ? p.cm + (size_t)b * p.Vp : nullptr;
     return B;
 }
 
@@ -285,7 +272,7 @@ __global__ void k_init(Pools pools, int32_t V, int32_t tree) {
 }
 
 // sources: d(s) = 0, R(s) = 1*(1-loss_v(s)) (topology.c:1441-1445); activate out-neighbours
-__global__ void k_seed(GraphDev g, Pools pools, int32_t src_key_zero) {
+__global__ void k_seed(GraphDev g, Pools pools) {
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int j = blockIdx.x;
     const int32_t s = B.srcv[j];
@@ -296,17 +283,11 @@ __global__ void k_seed(GraphDev g, Pools pools, int32_t src_key_zero) {
         B.H[idx] = 0;
         B.R[idx] = g.vfac[s];
         B.P[idx] = -1;
-        // f32 filter key: NaN for the dense sweeps (the source's own row never passes a
-        // dense filter: its seed candidate starts every lexicographic state,
-        // k_relax_dense_f); 0 for the CSR filtered rounds, where the source's row is the
-        // first candidate its out-neighbours see (k_relax_st)
-        if (B.D32) B.D32[idx] = src_key_zero ? 0.0f : __int_as_float(0x7fc00000);
-        // round 0 of the CSR delta rounds reads the change masks of a virtual round -1
+        // dense mode: f32 filter key NaN (the source's own row never passes a dense filter:
+        // its seed candidate starts every lexicographic state, k_relax_dense_f), and the
+        // first delta round reads the change masks of a virtual round -1
+        if (B.D32) B.D32[idx] = __int_as_float(0x7fc00000);
         if (B.chm1) atomicOr(&B.chm1[s], 1ull << j);
-        if (B.cm) {  // the masked rounds: the same, as a record stamped round -1
-            atomicOr(&B.cm[s].m[1], 1ull << j);
-            B.cm[s].rd[1] = 0xffffffffu;
-        }
     }
     for (int64_t x = g.out_ptr[s] + threadIdx.x; x < g.out_ptr[s + 1]; x += blockDim.x) B.act0[g.out_dst[x]] = 1;
 }
@@ -591,483 +572,6 @@ __global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ i
         relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
         if (lane == 0) B.act(parity)[v] = 0;
     }
-}
-
-// CSR delta round (default for sparse graphs).  Same pull schedule as k_relax (one wave per
-// active destination v, in-arcs in chunks of 8), but a lane only looks at in-neighbours u
-// whose state changed for ITS source in the previous round (chm: per-vertex 64-bit lane
-// masks), and folds those candidates into v's recorded lexicographic state (D, BDU = d(pred),
-// P, local-tie bit) with the rules of delta_candidate.  Unchanged (u, source) pairs were
-// folded in when they last changed, so the recorded state plus the changed candidates is
-// the full minimum.  The d(u) row loads are masked to the changed lanes: a row whose
-// single changed source shares one 64-byte line with 7 unchanged ones costs one line,
-// not 512 bytes.
-__global__ __launch_bounds__(256) void k_relax_delta(const int64_t* __restrict__ in_ptr,
-                                                     const int32_t* __restrict__ in_src,
-                                                     const double* __restrict__ in_w, const double* __restrict__ in_r,
-                                                     const int64_t* __restrict__ out_ptr,
-                                                     const int32_t* __restrict__ out_dst, Pools pools, int32_t V,
-                                                     int32_t nb, int32_t nvb, int32_t parity, int32_t* __restrict__ cnt,
-                                                     unsigned long long* __restrict__ prof) {
-    int32_t b, vt;
-    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
-    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int32_t v = vt * 4 + wave;
-    if (v >= V) return;
-    const int lane = threadIdx.x & 63;
-    const BatchDev B = batch_view(pools, b);
-    gbyte* act_cur = B.act(parity);
-    if (act_cur[v] == 0) {
-        if (lane == 0) B.chm(parity)[v] = 0ull;  // every (v, batch) has a wave: clear the stale mask
-        return;
-    }
-    if (lane == 0) act_cur[v] = 0;
-    const unsigned long long* chp = B.chm(parity ^ 1);
-    // masks written earlier in this same round too (Gauss-Seidel: a change made this round
-    // reaches v now instead of a round later; a mask seen twice re-offers an unchanged
-    // candidate, which the rules below leave as it is)
-    const unsigned long long* chc = B.chm(parity);
-    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
-    const int32_t sv = B.srcv[lane];
-    const size_t idx = (size_t)v * KL + lane;
-    const double D0 = B.D[idx];
-    const double B0 = B.BDU[idx];
-    const int32_t P0 = B.P[idx];
-    const uint32_t H0 = B.H[idx];
-    double d = D0, bdu = B0;
-    int32_t pa = P0;
-    int32_t pu = P0 >= 0 ? in_src[P0] : -1;
-    bool lt = (H0 & LTIE) != 0;
-    bool touched = false;
-    const gdouble* Dl = B.D + lane;
-    for (int32_t e = beg; e < end; e += 8) {
-        int32_t u[8];
-        double w[8];
-        unsigned long long m[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            u[k] = in_src[e + k];
-            w[k] = in_w[e + k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) m[k] = (e + k < end) ? (chp[u[k]] | chc[u[k]]) : 0ull;
-        double du[8];
-        bool on[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            on[k] = (m[k] >> lane) & 1ull;
-            du[k] = on[k] ? Dl[(size_t)u[k] * KL] : 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (!on[k]) continue;
-            const double c = du[k] + w[k];  // igraph: altdist = mindist + weights[edge]
-            // a same-round mask can become visible before the d(u) it announces (no fence):
-            // the stale d(u) is a weaker candidate, re-offered next round from chp; an
-            // unreached one (+inf) must not enter the equal-distance rules below
-            if (!(c < dinf())) continue;
-            if (c < d) {
-                d = c;
-                bdu = du[k];
-                pa = e + k;
-                pu = u[k];
-                lt = du[k] == c;  // degenerate d(u) == d(v): heap-order dependent
-                touched = true;
-            } else if (c == d) {
-                if (pu == u[k]) {  // the recorded predecessor refreshed
-                    lt = (du[k] == bdu && lt) || du[k] == c;
-                    bdu = du[k];
-                    touched = true;
-                } else if (du[k] < bdu) {
-                    bdu = du[k];
-                    pa = e + k;
-                    pu = u[k];
-                    lt = du[k] == c;
-                    touched = true;
-                } else if (du[k] == bdu) {
-                    lt = true;  // two predecessors at the same d(u): heap pop order decides
-                    touched = true;
-                }
-            }
-        }
-    }
-    bool ch = false;
-    if (touched && sv >= 0 && sv != v) {
-        const size_t uidx = (size_t)pu * KL + lane;
-        const uint32_t hu = B.H[uidx];
-        const double ru = B.R[uidx];
-        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
-        const double r = ru * in_r[pa];
-        const double R0 = B.R[idx];
-        ch = d != D0 || h != H0 || r != R0 || pa != P0;
-        if (ch) {
-            B.D[idx] = d;
-            B.H[idx] = h;
-            B.R[idx] = r;
-            B.P[idx] = pa;
-        }
-        if (bdu != B0) B.BDU[idx] = bdu;
-    }
-    const unsigned long long mask = __ballot(ch);
-    if (lane == 0) B.chm(parity)[v] = mask;
-    if (mask) {
-        gbyte* act_nxt = B.act(parity ^ 1);
-        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
-        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
-        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
-    }
-    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
-}
-
-
-// Round-stamped f32 keys for the CSR rounds (k_relax_st).  The key of a (vertex, source)
-// state is its distance rounded toward -inf in f32, lowered by at least 256 ulps and with
-// the low byte replaced by the round (mod 256) in which the state last changed:
-//   key <= round_down_f32(d) - 1 ulp <= d        (so the f32 filter stays exact)
-//   key >= round_down_f32(d) - 511 ulps           (so thr_of_key below bounds d from above)
-// 0 for d below 512 float ulps (the source itself: always eligible), NaN when unreached.
-// One coalesced 256-byte row load then tells every lane both whether the tail changed
-// recently (no separate change-mask loads) and a lower bound of its candidate.
-constexpr uint32_t KEY_NAN = 0x7fc00000u;
-__device__ __forceinline__ uint32_t stamp_key(double d, int32_t round) {
-    if (!(d < dinf())) return KEY_NAN;
-    const uint32_t kb = __float_as_uint(__double2float_rd(d));
-    if (kb < 512u) return 0u;
-    return ((kb - 256u) & ~0xFFu) | ((uint32_t)round & 0xFFu);
-}
-// an f32 upper bound of round_up(d) + 4 ulps from the key alone (the f32_thr of d or more)
-__device__ __forceinline__ float thr_of_key(uint32_t k) {
-    if (k == KEY_NAN) return __int_as_float(0x7f800000);
-    return k + 516u <= 0x7f7fffffu ? __uint_as_float(k + 516u) : __int_as_float(0x7f800000);
-}
-
-// Lexicographic state of one (destination, source) in the changed-tail CSR rounds
-// (k_relax_st): the recorded state (D0, B0, P0, H0, loaded lazily), the running one
-// (d, bdu = d(pred), pa / pu = predecessor arc / vertex, lt = local tie) and the threshold.
-struct MGState {
-    double D0, B0, d, bdu;
-    int32_t P0, pa, pu;
-    uint32_t H0;
-    float thr;
-    bool have, touched, lt;
-};
-
-__device__ __forceinline__ void mg_fold(MGState& S, double c, double du, int32_t e, int32_t u) {
-    if (!(c < dinf())) return;  // a key seen before its distance (same round): next round
-    if (c < S.d) {
-        S.d = c;
-        S.bdu = du;
-        S.pa = e;
-        S.pu = u;
-        S.lt = du == c;  // degenerate d(u) == d(v): heap-order dependent
-        S.touched = true;
-    } else if (c == S.d) {
-        if (S.pu == u) {  // the recorded predecessor refreshed
-            S.lt = (du == S.bdu && S.lt) || du == c;
-            S.bdu = du;
-            S.touched = true;
-        } else if (du < S.bdu) {
-            S.bdu = du;
-            S.pa = e;
-            S.pu = u;
-            S.lt = du == c;
-            S.touched = true;
-        } else if (du == S.bdu) {
-            S.lt = true;  // two predecessors at the same d(u): heap pop order decides
-            S.touched = true;
-        }
-    }
-}
-
-typedef __attribute__((address_space(1))) uint32_t gu32;
-
-// mg_fold with the recorded predecessor identified by its in-arc (one arc per tail in the
-// merged in-CSR), so the recorded state needs no tail lookup; S.pu is set whenever a
-// candidate is taken or refreshes the recorded predecessor
-__device__ __forceinline__ void mg_fold_arc(MGState& S, double c, double du, int32_t e, int32_t u) {
-    if (!(c < dinf())) return;  // a record seen before its distance (same round): next round
-    if (c < S.d) {
-        S.d = c;
-        S.bdu = du;
-        S.pa = e;
-        S.pu = u;
-        S.lt = du == c;  // degenerate d(u) == d(v): heap-order dependent
-        S.touched = true;
-    } else if (c == S.d) {
-        if (S.pa == e) {  // the recorded predecessor refreshed
-            S.lt = (du == S.bdu && S.lt) || du == c;
-            S.bdu = du;
-            S.pu = u;
-            S.touched = true;
-        } else if (du < S.bdu) {
-            S.bdu = du;
-            S.pa = e;
-            S.pu = u;
-            S.lt = du == c;
-            S.touched = true;
-        } else if (du == S.bdu) {
-            S.lt = true;  // two predecessors at the same d(u): heap pop order decides
-            S.touched = true;
-        }
-    }
-}
-
-
-// CSR round, changed tails only, stamped f32 keys (SHADOWTOPO_CSR_FILTERED).  One wave =
-// one destination v of one batch (lane = source).  Per chunk of 8 in-arcs: the tails' key
-// rows (256 B, coalesced: half of k_relax's f64 rows, and a working set the Infinity Cache
-// holds for the batches in flight) tell each lane whether the tail changed in the previous
-// or this round (key stamp) and give the f32 filter fl32(key + W32) <= thr(v) (thr_of_key:
-// an upper bound of v's running best, so the filter is exact); only passing lanes read the
-// exact f64 d(u) and fold (fl(d(u)+w), d(u)) into v's recorded lexicographic state with the
-// rules of k_relax_delta (mg_fold) -- that state is loaded lazily, for lanes with a passing
-// candidate only.  Unchanged tails were folded in when they last changed (every change
-// activates all out-neighbours for the next round, which sees its stamp), so the recorded
-// state plus the changed candidates is the full minimum: the same fixed point as k_relax,
-// bit for bit.  A stale stamp (256 rounds back) only re-offers an unchanged candidate,
-// which the rules leave as it is.
-__global__ __launch_bounds__(256) void k_relax_st(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
-                                                  const double* __restrict__ in_w, const float* __restrict__ in_w32,
-                                                  const double* __restrict__ in_r, const int64_t* __restrict__ out_ptr,
-                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t V,
-                                                  int32_t nb, int32_t nvb, int32_t parity, int32_t round,
-                                                  int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
-    int32_t b, vt;
-    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
-    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int32_t v = vt * 4 + wave;
-    if (v >= V) return;
-    const int lane = threadIdx.x & 63;
-    const BatchDev B = batch_view(pools, b);
-    gbyte* act_cur = B.act(parity);
-    if (act_cur[v] == 0) return;
-    if (lane == 0) act_cur[v] = 0;
-    const uint32_t kp = (uint32_t)(round - 1) & 0xFFu;
-    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
-    const int32_t sv = B.srcv[lane];
-    const size_t idx = (size_t)v * KL + lane;
-    const gu32* K = (const gu32*)B.D32;
-    const gu32* Kl = K + lane;
-    const gdouble* Dl = B.D + lane;
-    const bool live = sv >= 0 && sv != v;
-    // a dead lane gets a NaN threshold: nothing passes
-    const float thr = live ? thr_of_key(K[idx]) : __int_as_float(0x7fc00000);
-    MGState S;
-    S.have = S.touched = S.lt = false;
-    S.D0 = S.B0 = S.d = S.bdu = dinf();
-    S.P0 = S.pa = S.pu = -1;
-    S.H0 = 0;
-    for (int32_t e = beg; e < end; e += 8) {
-        int32_t u[8];
-        float w32[8];
-        uint32_t kk[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            u[k] = in_src[e + k];
-            w32[k] = in_w32[e + k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) kk[k] = e + k < end ? Kl[(size_t)u[k] * KL] : KEY_NAN;  // uniform guard
-        bool pass[8];
-        bool anyl = false;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            // changed in the previous round or this one; keys below 256 (the source) always
-            const bool elig = kk[k] < 256u || ((kk[k] - kp) & 0xFFu) <= 1u;
-            pass[k] = elig && __uint_as_float(kk[k]) + w32[k] <= thr;  // NaN never passes
-            anyl |= pass[k];
-        }
-        if (!__ballot(anyl)) continue;
-        if (anyl && !S.have) {  // the recorded state, only for lanes that have a candidate
-            S.D0 = B.D[idx];
-            S.B0 = B.BDU[idx];
-            S.P0 = B.P[idx];
-            S.H0 = B.H[idx];
-            S.d = S.D0;
-            S.bdu = S.B0;
-            S.pa = S.P0;
-            S.pu = S.P0 >= 0 ? in_src[S.P0] : -1;
-            S.lt = (S.H0 & LTIE) != 0;
-            S.have = true;
-        }
-        double du[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) du[k] = pass[k] ? Dl[(size_t)u[k] * KL] : 0.0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (pass[k]) mg_fold(S, du[k] + in_w[e + k], du[k], e + k, u[k]);  // altdist = mindist + weight
-    }
-    bool ch = false;
-    if (S.touched) {
-        const size_t uidx = (size_t)S.pu * KL + lane;
-        const uint32_t hu = B.H[uidx];
-        const double ru = B.R[uidx];
-        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (S.lt ? (TAINT | LTIE) : 0u);
-        const double r = ru * in_r[S.pa];
-        const double R0 = B.R[idx];
-        ch = S.d != S.D0 || h != S.H0 || r != R0 || S.pa != S.P0;
-        if (ch) {
-            B.D[idx] = S.d;
-            B.H[idx] = h;
-            B.R[idx] = r;
-            B.P[idx] = S.pa;
-            ((gu32*)B.D32)[idx] = stamp_key(S.d, round);
-        }
-        if (S.bdu != S.B0) B.BDU[idx] = S.bdu;
-    }
-    if (__ballot(ch)) {
-        gbyte* act_nxt = B.act(parity ^ 1);
-        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
-        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
-        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
-    }
-    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
-}
-
-// CSR masked round (SHADOWTOPO_CSR_MASKED, default for sparse graphs).  One wave = one
-// listed (vertex v, batch) of the round's frontier worklist (lane = source); v folds only the
-// (in-neighbour, source) pairs whose state changed in the previous round or this one.
-//  * The in-arcs are read 64 at a time, one per lane (coalesced tails and weights), and each
-//    lane gathers its tail's change record (32 B); a wave ballot compacts the arcs with a
-//    changed lane, and the wave walks only those, 8 at a time (uniform tail, weight and
-//    lane mask by readlane): 8 d(u) row loads in flight, each masked to the lanes whose
-//    source changed at u -- a row with one changed source costs one 64-byte line.  A hub
-//    whose in-list holds thousands of arcs but few changed tails costs a few vector loads,
-//    not a walk of every row.
-//  * v's own recorded state (D, BDU, P, H) is loaded only for lanes that receive a
-//    candidate, and the candidates fold into it with the rules of mg_fold: the unchanged
-//    pairs were folded when they last changed, so the recorded state plus the changed
-//    candidates is the full lexicographic minimum (the k_relax_delta argument).
-//  * A lane whose D, predecessor, hop count, reliability or taint changed is recorded in
-//    v's change record for this round, and v's out-neighbours go on the next worklist.
-//    A predecessor whose tree state changed at the same distance re-offers its candidate,
-//    which mg_fold sees as "the recorded predecessor refreshed" (hops / reliability are
-//    recomputed from it).
-// The fixed point is k_relax's, bit for bit (tests/test_csr_gpu.py).
-__global__ __launch_bounds__(256) void k_relax_cm(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
-                                                  const double* __restrict__ in_w, const double* __restrict__ in_r,
-                                                  const int64_t* __restrict__ out_ptr,
-                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t round,
-                                                  const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
-                                                  int32_t nb, int64_t S_, int32_t* __restrict__ cnt,
-                                                  unsigned long long* __restrict__ prof) {
-    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t Lb = flat_block();
-    const int64_t i = (Lb & 7) * S_ + (Lb >> 3) * 4 + wave;
-    const int64_t T = prefix[nb];
-    if ((Lb >> 3) * 4 + wave >= S_ || i >= T) return;
-    const int lane = threadIdx.x & 63;
-    const int32_t b = wl_batch(prefix, nb, i, lane);
-    const int4 item = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])];
-    const int32_t v = __builtin_amdgcn_readfirstlane(item.x);
-    const int32_t beg = __builtin_amdgcn_readfirstlane(item.y), end = __builtin_amdgcn_readfirstlane(item.z);
-    const int32_t parity = round & 1;
-    const BatchDev B = batch_view(pools, b);
-    if (lane == 0) B.act(parity)[v] = 0;
-    const uint32_t rc = (uint32_t)round, rp = rc - 1u;
-    const CMask* cm = B.cm;
-    const int32_t sv = B.srcv[lane];
-    const bool live = sv >= 0 && sv != v;
-    const size_t idx = (size_t)v * KL + lane;
-    const gdouble* Dl = B.D + lane;
-    MGState S;
-    S.have = S.touched = S.lt = false;
-    S.D0 = S.B0 = S.d = S.bdu = dinf();
-    S.P0 = S.pa = S.pu = -1;
-    S.H0 = 0;
-    int32_t u_first = 0;  // the first 64 tails (the out-neighbours too, undirected)
-    for (int32_t base = beg; base < end; base += 64) {
-        const int32_t e = base + lane;
-        int32_t u = 0;
-        double w = 0.0;
-        unsigned long long m = 0ull;
-        if (e < end) {
-            u = in_src[e];
-            if (base == beg) u_first = u;
-            w = in_w[e];
-            const CMask c = cm[u];
-            m = ((c.rd[0] == rp || c.rd[0] == rc) ? c.m[0] : 0ull) | ((c.rd[1] == rp || c.rd[1] == rc) ? c.m[1] : 0ull);
-        }
-        unsigned long long arcs = __ballot(m != 0ull);
-        while (arcs) {
-            int32_t uk[8], ek[8];
-            double wk[8], du[8];
-            bool on[8];
-            bool anyl = false;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                on[j] = false;
-                uk[j] = 0;
-                ek[j] = 0;
-                wk[j] = 0.0;
-                if (arcs) {
-                    const int k = __builtin_ctzll(arcs);
-                    arcs &= arcs - 1ull;
-                    uk[j] = __builtin_amdgcn_readlane(u, k);
-                    wk[j] = readlane_d(w, k);
-                    ek[j] = base + k;
-                    on[j] = live && ((readlane_u64(m, k) >> lane) & 1ull);
-                    anyl |= on[j];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) du[j] = on[j] ? Dl[(size_t)uk[j] * KL] : 0.0;
-            if (anyl && !S.have) {  // the recorded state, only for lanes that receive a candidate
-                S.D0 = B.D[idx];
-                S.B0 = B.BDU[idx];
-                S.P0 = B.P[idx];
-                S.H0 = B.H[idx];
-                S.d = S.D0;
-                S.bdu = S.B0;
-                S.pa = S.P0;
-                S.pu = -1;  // the recorded predecessor's vertex, looked up only if the finish needs it
-                S.lt = (S.H0 & LTIE) != 0;
-                S.have = true;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (on[j]) mg_fold_arc(S, du[j] + wk[j], du[j], ek[j], uk[j]);  // altdist = mindist + weight
-        }
-    }
-    bool ch = false;
-    if (S.touched) {
-        if (S.pu < 0) S.pu = in_src[S.pa];  // a tie at the recorded predecessor: its vertex
-        const size_t uidx = (size_t)S.pu * KL + lane;
-        const uint32_t hu = B.H[uidx];
-        const double ru = B.R[uidx];
-        const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (S.lt ? (TAINT | LTIE) : 0u);
-        const double r = ru * in_r[S.pa];
-        if (S.d != S.D0) {
-            ch = true;
-        } else {
-            const double R0 = B.R[idx];
-            ch = h != S.H0 || r != R0 || S.pa != S.P0;
-        }
-        if (ch) {
-            B.D[idx] = S.d;
-            B.H[idx] = h;
-            B.R[idx] = r;
-            B.P[idx] = S.pa;
-        }
-        if (S.bdu != S.B0) B.BDU[idx] = S.bdu;
-    }
-    const unsigned long long mask = __ballot(ch);
-    if (mask) {
-        if (lane == 0) {
-            CMask* c = B.cm + v;
-            c->m[parity] = mask;
-            c->rd[parity] = rc;
-        }
-        gbyte* act_nxt = B.act(parity ^ 1);
-        if (out_ptr == in_ptr && end - beg <= 64) {  // undirected: the out-neighbours are the tails in hand
-            if (beg + lane < end) act_nxt[u_first] = 1;
-        } else {
-            for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
-        }
-        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
-        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
-    }
-    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
 }
 
 // Lexicographic (candidate, d(u)) minimum with heap-order tie detection, branch-free so the
@@ -2770,7 +2274,6 @@ struct shadowtopo_engine {
     int32_t opt_force_replay = 0;
     int32_t opt_profile = 0;
     int32_t opt_dense_variant = 0;  // SHADOWTOPO_DENSE_F32 (default) or SHADOWTOPO_DENSE_F64
-    int32_t opt_csr_variant = 1;    // SHADOWTOPO_CSR_FULL (default), _FILTERED, _DELTA (see shadowtopo.h)
     int32_t opt_dense_tb = 1;       // batches per wave in the f32-filtered full sweep (1, 2 or 4)
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
@@ -2850,12 +2353,8 @@ void free_batches(shadowtopo_engine* eng) {
     eng->nb_cap = 0;
 }
 
-bool state_bdu(const shadowtopo_engine* eng) {
-    return eng->dense || eng->opt_csr_variant != SHADOWTOPO_CSR_FULL;
-}
-bool state_d32(const shadowtopo_engine* eng) {
-    return eng->dense || eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED;
-}
+bool state_bdu(const shadowtopo_engine* eng) { return eng->dense != 0; }
+bool state_d32(const shadowtopo_engine* eng) { return eng->dense != 0; }
 // bytes per (vertex, source) of the batch pools
 double state_bytes(const shadowtopo_engine* eng) {
     return 24.0 + (state_bdu(eng) ? 8.0 : 0.0) + (state_d32(eng) ? 4.0 : 0.0);
@@ -2892,7 +2391,6 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
             (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlcnt, sizeof(uint32_t) * nb)) ||
             (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlpre, sizeof(int64_t) * (nb + 1))))
             return rc;
-        if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.cm, sizeof(CMask) * (size_t)eng->Vp * nb))) return rc;
         HIP_TRY(hipHostMalloc((void**)&eng->h_wlcnt, sizeof(uint32_t) * nb, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&eng->h_wlpre, sizeof(int64_t) * (nb + 1), hipHostMallocDefault));
     }
@@ -3059,11 +2557,9 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     } else {
         const size_t total = (size_t)eng->Vp * KL;
         int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
-        const int32_t tree = eng->dense || eng->opt_csr_variant == SHADOWTOPO_CSR_DELTA ||
-                             eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED;
+        const int32_t tree = eng->dense;
         hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp, tree);
-        if (eng->pools.cm) HIP_TRY(hipMemsetAsync(eng->pools.cm, 0, sizeof(CMask) * (size_t)eng->Vp * nbg, s));
-        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools, eng->dense ? 0 : 1);
+        hipLaunchKernelGGL(k_seed, dim3(KL, nbg), dim3(256), 0, s, g, eng->pools);
         HIP_TRY(hipGetLastError());
     }
     const int32_t nvb = (V + 3) / 4;
@@ -3091,14 +2587,13 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         0x7f7f7f7e, (int64_t)V * KL * eng->opt_delta_permille / 1000);
     std::vector<uint8_t> full_b;  // dense: batches the full sweep covers this round
     // sparse FULL rounds over compacted frontier worklists (k_compact / k_relax_wl)
-    const bool masked = !eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_MASKED && eng->pools.cm && eng->d_wl;
-    const bool use_wl = masked || (!eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL && eng->opt_worklist && eng->d_wl);
+    const bool use_wl = !eng->dense && eng->opt_worklist && eng->d_wl;
     const int32_t ncb = (V + WL_SPAN - 1) / WL_SPAN;
     // small graphs (C3: 110 batches x 7000 vertices): rounds driven from the device, the
     // host reading the per-round item counts once per block of DEV_K rounds instead of
     // synchronising on every round (a round of C3 is 0.1 ms of kernel and ~0.05 ms of
     // launch + read-back otherwise)
-    const bool dev_rounds = !masked && use_wl && eng->opt_worklist == 1 && nbg <= 1024 &&
+    const bool dev_rounds = use_wl && eng->opt_worklist == 1 && nbg <= 1024 &&
                             (eng->opt_device_rounds == 2 ||
                              (eng->opt_device_rounds == 1 && (int64_t)nbg * V <= eng->dev_rounds_max));
     if (dev_rounds) {
@@ -3186,7 +2681,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             if (wl_total == 0) break;  // nothing active: converged
         }
         // worklist only where it pays: a mostly-active round runs the plain grid
-        const bool round_wl = use_wl && (masked || eng->opt_worklist == 2 || wl_total * 2 < (int64_t)nbg * V);
+        const bool round_wl = use_wl && (eng->opt_worklist == 2 || wl_total * 2 < (int64_t)nbg * V);
         if (round_wl)
             HIP_TRY(hipMemcpyAsync(eng->d_wlpre, eng->h_wlpre, sizeof(int64_t) * (nbg + 1), hipMemcpyHostToDevice, s));
         int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
@@ -3273,18 +2768,6 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 }
                 eng->st.delta_sweeps++;
             }
-        } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FILTERED) {
-            eng->st.relax_batches += nbg;
-            hipLaunchKernelGGL(k_relax_st, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
-                               g.in_w32, g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1),
-                               (int32_t)(round & 0x7fffffff), cnt_cur, eng->d_prof);
-        } else if (masked) {
-            eng->st.relax_batches += nbg;
-            eng->st.wl_launches++;
-            const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
-            hipLaunchKernelGGL(k_relax_cm, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
-                               g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 0x7fffffff), eng->d_wl,
-                               eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else if (round_wl) {
             eng->st.relax_batches += nbg;
             eng->st.wl_launches++;
@@ -3292,15 +2775,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             hipLaunchKernelGGL(k_relax_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
                                g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
                                eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
-        } else if (eng->opt_csr_variant == SHADOWTOPO_CSR_FULL) {
+        } else {
             eng->st.relax_batches += nbg;
             hipLaunchKernelGGL(k_relax, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
                                g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
-                               eng->d_prof);
-        } else {
-            eng->st.relax_batches += nbg;
-            hipLaunchKernelGGL(k_relax_delta, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
-                               g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
                                eng->d_prof);
         }
         HIP_TRY(hipGetLastError());
@@ -4178,16 +3656,11 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_dense_tb = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_CSR_VARIANT:
-            if (value != SHADOWTOPO_CSR_DELTA && value != SHADOWTOPO_CSR_FULL && value != SHADOWTOPO_CSR_FILTERED &&
-                value != SHADOWTOPO_CSR_MASKED)
-                return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
-            if (eng->nb_cap > 0 && eng->opt_csr_variant != (int32_t)value) {
-                // the pools' layout depends on the variant (state_bdu / state_d32)
-                (void)hipSetDevice(eng->device);
-                if (eng->own_stream) (void)hipStreamSynchronize(eng->own_stream);
-                free_batches(eng);
-            }
-            eng->opt_csr_variant = (int32_t)value;
+            // one sparse kernel family (k_relax / k_relax_wl / k_relax_wlp); the r01-r02
+            // cross-check variants (changed-tail delta, stamped f32 keys, change records) were
+            // slower on every config and are gone
+            if (value != SHADOWTOPO_CSR_FULL)
+                return fail(SHADOWTOPO_EINVAL, "CSR variant %lld: only SHADOWTOPO_CSR_FULL exists", (long long)value);
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SOURCE_ORDER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "source order must be 0 or 1");

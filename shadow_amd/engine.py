@@ -46,10 +46,7 @@ OPT_WORKLIST = 14
 OPT_GRID_X = 15
 OPT_PRUNE_PENDANT = 16
 OPT_DEVICE_ROUNDS = 17
-CSR_DELTA = 0  # fold changed in-neighbours into the recorded state, f64 (cross-check)
-CSR_FULL = 1  # recompute every active vertex over all in-arcs (cross-check)
-CSR_FILTERED = 2  # changed tails only: round-stamped f32 keys, f64 settle (k_relax_st)
-CSR_MASKED = 3  # changed (tail, source) pairs only, change records + ballot compaction (k_relax_cm)
+CSR_FULL = 1  # recompute every active vertex over all in-arcs (k_relax / k_relax_wl: the only sparse family)
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (

@@ -1,8 +1,7 @@
-"""CSR relaxation variants (k_relax_cm: changed (tail, source) pairs over frontier
-worklists; k_relax: full recomputation, over frontier worklists in sparse rounds;
-k_relax_st: changed tails only, round-stamped f32 keys; k_relax_delta: changed tails, f64,
-whole grid) against the oracle and against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops, kind and
-reliability; every variant must reach the same fixed point."""
+"""CSR relaxation rounds (k_relax over the whole grid, k_relax_wl / k_relax_wlp over frontier
+worklists, host- or device-driven, 1-D or 2-D grids, one or several batch groups) against
+the oracle and against each other.  Same bar as test_engine_gpu.py: bit-exact latency, hops,
+kind and reliability; every schedule must reach the same fixed point."""
 import numpy as np
 import pytest
 
@@ -42,12 +41,23 @@ def _case(case):
 CASES = ["sparse", "directed", "ties", "int_random", "vloss_prefer", "no_loops", "multigraph"]
 
 
-@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL, E.CSR_FILTERED, E.CSR_MASKED])
+@pytest.mark.parametrize("worklist", [1, 2])
 @pytest.mark.parametrize("case", CASES)
-def test_csr_variants(case, variant):
+def test_csr_rounds(case, worklist):
+    """default schedule (worklists when under half the pairs are active) and always-worklist"""
     g = _case(case)
-    st = compare(g, layout="csr", csr_variant=variant)
+    st = compare(g, layout="csr", worklist=worklist)
     assert st["dense"] == 0
+
+
+def test_csr_removed_variants_rejected():
+    g = _case("sparse")
+    eng = E.Engine.from_synth(g, layout="csr")
+    eng.set_option(E.OPT_CSR_VARIANT, E.CSR_FULL)
+    for v in (0, 2, 3):
+        with pytest.raises(E.ShadowTopoError):
+            eng.set_option(E.OPT_CSR_VARIANT, v)
+    eng.close()
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -55,37 +65,38 @@ def test_csr_full_grid_without_worklists(case):
     """the default FULL rounds run over compacted frontier worklists; the one-wave-per-pair
     grid must give the same matrices"""
     g = _case(case)
-    compare(g, layout="csr", csr_variant=E.CSR_FULL, worklist=0)
-    compare(g, layout="csr", csr_variant=E.CSR_FULL, worklist=1, batches_in_flight=2)
+    compare(g, layout="csr", worklist=0)
+    compare(g, layout="csr", worklist=1, batches_in_flight=2)
 
 
-@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FULL, E.CSR_FILTERED, E.CSR_MASKED])
 @pytest.mark.parametrize("worklist", [0, 1, 2])
-def test_csr_two_dimensional_grids(variant, worklist):
+def test_csr_two_dimensional_grids(worklist):
     """grids past 2^24 blocks (C5: 102 batches x 868k vertices = 22M blocks of 256) go 2-D
     (grid_of / flat_block: a 1-D launch's 32-bit work-item count would wrap and drop
     blocks, and a round that dropped a batch could end the iteration early); forcing the
     2-D form on every launch of a small graph must give the same matrices"""
     g = synth.random_sparse(V=400, avg_deg=5, seed=38)
-    compare(g, layout="csr", csr_variant=variant, worklist=worklist, grid_x=64)
+    compare(g, layout="csr", worklist=worklist, grid_x=64)
 
 
-@pytest.mark.parametrize("variant", [E.CSR_DELTA, E.CSR_FILTERED, E.CSR_MASKED])
-def test_csr_delta_several_groups(variant):
+@pytest.mark.parametrize("worklist", [0, 1])
+def test_csr_several_groups(worklist):
     g = synth.random_sparse(V=500, avg_deg=4, seed=37)
-    compare(g, layout="csr", batches_in_flight=3, csr_variant=variant)  # 500 sources -> 8 batches -> 3 groups
+    compare(g, layout="csr", batches_in_flight=3, worklist=worklist)  # 500 sources -> 8 batches -> 3 groups
 
 
 @pytest.mark.parametrize("case", ["ties", "sparse", "int_random", "directed"])
-def test_csr_delta_same_fixed_point(case):
-    """Distances bit-exact, tie flags identical, predecessor and hops identical wherever no
-    heap-order tie is involved."""
+def test_csr_schedules_same_fixed_point(case):
+    """Full rows (sssp) from the grid, worklist and device-driven schedules: distances
+    bit-exact, tie flags identical, predecessor and hops identical wherever no heap-order
+    tie is involved."""
     g = _case(case)
     srcs = np.arange(0, g.n, 2, dtype=np.int32)
     outs = []
-    for variant in (E.CSR_FULL, E.CSR_DELTA, E.CSR_FILTERED, E.CSR_MASKED):
+    for wl, devr in ((0, 0), (1, 0), (2, 0), (1, 2)):
         eng = E.Engine.from_synth(g, layout="csr")
-        eng.set_option(E.OPT_CSR_VARIANT, variant)
+        eng.set_option(E.OPT_WORKLIST, wl)
+        eng.set_option(E.OPT_DEVICE_ROUNDS, devr)
         outs.append(eng.sssp(srcs))
         eng.close()
     d0, p0, h0, t0 = outs[0]
@@ -176,6 +187,6 @@ def test_device_driven_rounds_same_results(case):
     per block of rounds, k_scan_wl / k_relax_wlp) against host-driven rounds (one read-back
     per round) and the oracle, with several batch groups"""
     g = _case(case)
-    st1 = compare(g, layout="csr", csr_variant=E.CSR_FULL, device_rounds=2, batches_in_flight=2)
-    st0 = compare(g, layout="csr", csr_variant=E.CSR_FULL, device_rounds=0, batches_in_flight=2)
+    st1 = compare(g, layout="csr", device_rounds=2, batches_in_flight=2)
+    st0 = compare(g, layout="csr", device_rounds=0, batches_in_flight=2)
     assert st1["rounds"] == st0["rounds"] and st1["wl_launches"] == st1["relax_launches"]
