@@ -312,7 +312,12 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
     const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? (TAINT | LTIE) : 0u);
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
     const double r = ru * in_r[arc];
+#ifdef EXP_DP_ONLY
+    (void)h; (void)r; (void)curH; (void)curR;
+    if (bc != curD || arc != curP) {
+#else
     if (bc != curD || h != curH || r != curR || arc != curP) {
+#endif
         B.D[idx] = bc;
         if (B.D32) B.D32[idx] = f32_key(bc);
         B.H[idx] = h;
@@ -356,8 +361,13 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
     const int32_t sv = B.srcv[lane];
     const size_t idx = (size_t)v * KL + lane;
     const double curD = B.D[idx];
+#ifdef EXP_DP_ONLY
+    const uint32_t curH = 0u;
+    const double curR = 0.0;
+#else
     const uint32_t curH = B.H[idx];
     const double curR = B.R[idx];
+#endif
     const int32_t curP = B.P[idx];
     const gdouble* Dl = B.D + lane;
     // (unlike the dense kernel, the running best is not seeded with curD here: rows are
@@ -1196,11 +1206,7 @@ __global__ __launch_bounds__(256) void k_dense_wr(const int32_t* __restrict__ WI
 // The arcs' reliability factors come from the dense WR table (in_r[WI], built once with the
 // tables): gathered from in_r by arc id they cost one scattered line per (v, source) and
 // C2's seed 0.17 ms per launch against 0.07 ms without them.
-#ifndef SEED_T_EXP
 constexpr int SEED_T = 16;             // destinations per block: 22 KB of LDS, 7 blocks per CU
-#else
-constexpr int SEED_T = SEED_T_EXP;
-#endif
 constexpr int SEED_ST = SEED_T + 1;    // LDS row stride: the transposed reads spread over the banks
 __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__ W, const int32_t* __restrict__ WI,
                                                       int32_t Vp, const double* __restrict__ WR,
