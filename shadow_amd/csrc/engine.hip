@@ -734,6 +734,17 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 //  * rows where any lane passes are collected and, at the end of the chunk, re-evaluated
 //    exactly in f64 (D and W from global memory) in row order -- the same lexicographic
 //    minimum and tie flag as a sequential scan.
+#ifdef EXP_PHASE_TIME
+// diagnostic build only: per-block wall-clock stamps (s_memrealtime, 100 MHz) of the dense
+// sweep's phases and its counts, read by shadowtopo_exp_phase (never in the product)
+constexpr int PHASE_BLOCKS = 16384;
+__device__ unsigned long long g_phase[PHASE_BLOCKS][8];
+#define PHASE_STAMP(slot_) do { if (threadIdx.x == 0 && blockIdx.x < PHASE_BLOCKS) g_phase[blockIdx.x][slot_] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define PHASE_SET(slot_, val_) do { if (threadIdx.x == 0 && blockIdx.x < PHASE_BLOCKS) g_phase[blockIdx.x][slot_] = (val_); } while (0)
+#else
+#define PHASE_STAMP(slot_) do { } while (0)
+#define PHASE_SET(slot_, val_) do { } while (0)
+#endif
 constexpr int SRS = 32;  // rows per LDS chunk
 constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FTDT; 4 was slower: 4.63 vs 3.8 ms on C2)
 
@@ -781,6 +792,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     if (first < 0) return;
     const int32_t vb = vt * BW;
     if (vb >= V) return;
+    PHASE_STAMP(0);
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int32_t v0 = vb + wave * TDT;
@@ -967,6 +979,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         }
         return -1;
     };
+    PHASE_STAMP(1);
     int32_t itc = next_live(0);
     if (itc >= 0) {
         fetch(itc);
@@ -975,7 +988,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     }
     __syncthreads();
     int bufc = 0;
+#ifdef EXP_PHASE_TIME
+    int32_t nvisit = 0;
+    uint32_t nhit = 0;
+#endif
     while (itc >= 0) {
+#ifdef EXP_PHASE_TIME
+        ++nvisit;
+#endif
         const int32_t c = chunk_of(itc);
         const int32_t u0 = c * SRS;
         const int cur = bufc;
@@ -1052,6 +1072,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
 #pragma unroll
             for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + (u0 / SRS)] = hits[k];
         }
+#ifdef EXP_PHASE_TIME
+        nhit += __popc(hits[0]);
+#endif
         if (more) {
             stash(cur ^ 1);
             advance();
@@ -1060,6 +1083,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         bufc ^= 1;
         itc = itn;
     }
+    PHASE_STAMP(2);
+    PHASE_SET(5, nvisit);
+    PHASE_SET(6, nhit);
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
     // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
     // j % TDT, broadcast by readlane).  A source's own row never passes (its D32 is NaN: the
@@ -1115,6 +1141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
             }
         }
     }
+    PHASE_STAMP(3);
     if (v0 < V) {
 #pragma unroll
         for (int k = 0; k < TB; ++k)
@@ -1122,6 +1149,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
                 dense_epilogue<TDT>(B[k], lane, sv[k], v0, V, bc[k], bdu[k], bu[k], tie[k], WI, Vp, in_r, parity,
                                     cnt, b0 + k, vid);
     }
+    PHASE_STAMP(4);
+#ifdef EXP_PHASE_TIME
+    {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        PHASE_SET(7, ((unsigned long long)(xcc & 0xf) << 32) | (uint32_t)grp);
+    }
+#endif
 }
 
 // Pruned full sweep (k_relax_dense_f<.., PR = true>) inputs.
@@ -3365,6 +3400,13 @@ int ensure_mirrors(shadowtopo_engine* eng) {
 }  // namespace
 
 extern "C" {
+#ifdef EXP_PHASE_TIME
+int shadowtopo_exp_phase(unsigned long long* out, int nblocks) {
+    if (nblocks > PHASE_BLOCKS) nblocks = PHASE_BLOCKS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * (size_t)nblocks) ==
+                   hipSuccess ? nblocks : -1;
+}
+#endif
 
 int shadowtopo_device_count(void) {
     int n = 0;
