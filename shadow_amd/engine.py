@@ -46,6 +46,7 @@ OPT_WORKLIST = 14
 OPT_GRID_X = 15
 OPT_PRUNE_PENDANT = 16
 OPT_DEVICE_ROUNDS = 17
+OPT_DENSE_SWEEP = 18
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (k_relax / k_relax_wl: the only sparse family)
 
 # every symbol include/shadowtopo.h declares
@@ -75,7 +76,7 @@ class Stats(ctypes.Structure):
         ("full_batches", ctypes.c_int64), ("full_changes", ctypes.c_int64), ("relax_batches", ctypes.c_int64),
         ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double), ("sparse_deltas", ctypes.c_int64),
         ("self_ms", ctypes.c_double), ("self_paths", ctypes.c_int64), ("pruned_deltas", ctypes.c_int64),
-        ("pruned_vertices", ctypes.c_int64),
+        ("pruned_vertices", ctypes.c_int64), ("pool_allocs", ctypes.c_int64), ("pool_alloc_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
