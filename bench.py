@@ -396,8 +396,6 @@ def main():
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
                     "chunk c's all-gather overlaps chunk c+1's computation")
-    ap.add_argument("--dense-sweep", type=int, default=-1,
-                    help="pruned f32 sweep: 0 = block-coupled, 1 = wave-independent (-1 = engine default)")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists when under half the pairs are active (1, default), "
@@ -450,8 +448,6 @@ def main():
     eng.set_option(E.OPT_DENSE_VARIANT, args.dense_variant)
     if args.dense_tb:
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
-    if args.dense_sweep >= 0:
-        eng.set_option(E.OPT_DENSE_SWEEP, args.dense_sweep)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "

@@ -110,9 +110,6 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               counts read back once per 8 rounds) when batches x vertices <= 4 Mi,
                                               2 = always, 0 = never (one host read-back per round). Results are
                                               identical. */
-#define SHADOWTOPO_OPT_DENSE_SWEEP 18        /* pruned f32 dense full sweep: 0 = block-coupled kernel (LDS-staged
-                                              chunks, two barriers per chunk), 1 = wave-independent kernel
-                                              (register-staged chunks, no block barrier). Results are identical. */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (55 % of free HBM, at least 24 GB) this
                                               engine may take (default 1000); engines sharing one device split it */
 

@@ -300,24 +300,13 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
                                               uint32_t curH, double curR, int32_t curP) {
     const size_t idx = (size_t)v * KL + lane;
     const size_t uidx = (size_t)u * KL + lane;
-#ifdef EXP_NO_PRED_GATHER
-    const uint32_t hu = 0u;
-    const double ru = 1.0;
-    (void)uidx;
-#else
     const uint32_t hu = B.H[uidx];
     const double ru = B.R[uidx];
-#endif
     // local tie: two candidates share (fl(d(u)+w), d(u)), or the degenerate d(u) == d(v)
     const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? (TAINT | LTIE) : 0u);
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
     const double r = ru * in_r[arc];
-#ifdef EXP_DP_ONLY
-    (void)h; (void)r; (void)curH; (void)curR;
-    if (bc != curD || arc != curP) {
-#else
     if (bc != curD || h != curH || r != curR || arc != curP) {
-#endif
         B.D[idx] = bc;
         if (B.D32) B.D32[idx] = f32_key(bc);
         B.H[idx] = h;
@@ -361,13 +350,8 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
     const int32_t sv = B.srcv[lane];
     const size_t idx = (size_t)v * KL + lane;
     const double curD = B.D[idx];
-#ifdef EXP_DP_ONLY
-    const uint32_t curH = 0u;
-    const double curR = 0.0;
-#else
     const uint32_t curH = B.H[idx];
     const double curR = B.R[idx];
-#endif
     const int32_t curP = B.P[idx];
     const gdouble* Dl = B.D + lane;
     // (unlike the dense kernel, the running best is not seeded with curD here: rows are
@@ -734,9 +718,10 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 //  * rows where any lane passes are collected and, at the end of the chunk, re-evaluated
 //    exactly in f64 (D and W from global memory) in row order -- the same lexicographic
 //    minimum and tie flag as a sequential scan.
-#ifdef EXP_PHASE_TIME
-// diagnostic build only: per-block wall-clock stamps (s_memrealtime, 100 MHz) of the dense
-// sweep's phases and its counts, read by shadowtopo_exp_phase (never in the product)
+#ifdef SHADOWTOPO_PHASE_STAMPS
+// diagnostic build only (-DSHADOWTOPO_PHASE_STAMPS, _exp/build_variant.sh; never in the
+// product library): per-block wall-clock stamps (s_memrealtime, 100 MHz) of the dense
+// sweep's phases and its counts, read by shadowtopo_exp_phase (_exp/r03_phase.py)
 constexpr int PHASE_BLOCKS = 16384;
 __device__ unsigned long long g_phase[PHASE_BLOCKS][8];
 #define PHASE_STAMP(slot_) do { if (threadIdx.x == 0 && blockIdx.x < PHASE_BLOCKS) g_phase[blockIdx.x][slot_] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -776,22 +761,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
     __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
     int32_t grp, vt;
-#ifdef EXP_DENSE_TILE_MAJOR
-    if (!xcd_tile(blockIdx.x, ntb, (nb + TB - 1) / TB, vt, grp)) return;
-#elif defined(EXP_DENSE_XCD_PAIR)
-    {
-        // batches sliced over the XCDs as xcd_tile does, but tile-major inside an XCD: the
-        // XCD's batches of one destination tile run side by side and share its W32 strip
-        const int32_t ng = (nb + TB - 1) / TB;
-        const int32_t gpx = (ng + 7) / 8;
-        const int32_t j = (int32_t)(blockIdx.x >> 3);
-        grp = (int32_t)(blockIdx.x & 7) * gpx + j % gpx;
-        vt = j / gpx;
-        if (grp >= ng || vt >= ntb) return;
-    }
-#else
     if (!xcd_tile(blockIdx.x, (nb + TB - 1) / TB, ntb, grp, vt)) return;  // block-uniform exits only (barriers below)
-#endif
     const int32_t b0 = grp * TB;  // this block's TB batches
     bool live[TB];
     int32_t first = -1;
@@ -999,12 +969,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     }
     __syncthreads();
     int bufc = 0;
-#ifdef EXP_PHASE_TIME
+#ifdef SHADOWTOPO_PHASE_STAMPS
     int32_t nvisit = 0;
     uint32_t nhit = 0;
 #endif
     while (itc >= 0) {
-#ifdef EXP_PHASE_TIME
+#ifdef SHADOWTOPO_PHASE_STAMPS
         ++nvisit;
 #endif
         const int32_t c = chunk_of(itc);
@@ -1083,7 +1053,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
 #pragma unroll
             for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + (u0 / SRS)] = hits[k];
         }
-#ifdef EXP_PHASE_TIME
+#ifdef SHADOWTOPO_PHASE_STAMPS
         nhit += __popc(hits[0]);
 #endif
         if (more) {
@@ -1161,235 +1131,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
                                     cnt, b0 + k, vid);
     }
     PHASE_STAMP(4);
-#ifdef EXP_PHASE_TIME
+#ifdef SHADOWTOPO_PHASE_STAMPS
     {
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         PHASE_SET(7, ((unsigned long long)(xcc & 0xf) << 32) | (uint32_t)grp);
     }
 #endif
-}
-
-// Wave-independent pruned sweep (SHADOWTOPO_OPT_DENSE_SWEEP = 1): the same filter,
-// thresholds, chunk bounds, hit log, exact pass and epilogue as k_relax_dense_f<TDT, XR, 1,
-// true>, but every wave runs on its own -- no block barrier anywhere.  The block-coupled
-// sweep stages each 32-row chunk through LDS for its four waves and waits at two barriers
-// per chunk; it is latency-bound (r03 phase stamps, C2: 5.3 us per chunk iteration, 83 % of
-// a block's time in the chunk loop) with at most 72 KB of loads in flight per CU, which is
-// what its 24 KB of LDS per block allows.  Here a wave keeps the D32 rows of its next live
-// chunk in registers (32 VGPRs per chunk, two chunks: the one being filtered and the one in
-// flight) and only its own 1 KB W32 slice in LDS, so a CU holds ~2x the loads in flight and
-// no wave waits for its block's slowest wave.  The D32 rows of a batch are read by all
-// four waves of a block (L2 / L1 hits: the batch-major block order keeps a batch's 2.5 MB
-// of D32 in its XCD's L2).  Liveness windows are evaluated per wave (window 0 = the tile's
-// own chunk, then 64 chunks), before the thresholds of the chunk in hand tighten them --
-// conservative, hence exact (k_relax_dense_f's argument).
-template <int TDT, int XR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_relax_dense_w(
-    const float* __restrict__ W32p, const double* __restrict__ W, const int32_t* __restrict__ WI, int32_t Vp,
-    const double* __restrict__ in_r, Pools pools, int32_t V, int32_t nb, int32_t ntb, int32_t parity,
-    int32_t thresh, const int32_t* __restrict__ cnt_prev, int32_t* __restrict__ cnt, uint32_t* __restrict__ hitlog,
-    const int32_t* __restrict__ perm, const float* __restrict__ minW, const float* __restrict__ minD) {
-    constexpr int BW = 4 * TDT;
-    constexpr int EWG = 4;  // chunk bounds in flight per step of a window evaluation
-    static_assert(TDT == 8, "one float4 per lane carries a chunk's 32 x 8 W32 slice");
-    __shared__ __attribute__((aligned(16))) float sW[4][2][SRS * TDT];
-    int32_t b, vt;
-    if (!xcd_tile(blockIdx.x, nb, ntb, b, vt)) return;
-    if (cnt_prev[b] <= thresh) return;  // converged (0) or left to the delta round
-    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int32_t v0 = vt * BW + wave * TDT;
-    if (v0 >= V) return;  // wave-level exits are fine: nothing below synchronises the block
-    const BatchDev B = batch_view(pools, b);
-    const int32_t sv = B.srcv[lane];
-    int32_t vid[TDT];
-    float thr[TDT];
-#pragma unroll
-    for (int t = 0; t < TDT; ++t) {
-        vid[t] = __builtin_amdgcn_readfirstlane(perm[v0 + t]);
-        const int32_t v = vid[t];
-        const double cd = B.D[(size_t)v * KL + lane];
-        const double ws = (sv >= 0 && sv != v) ? W[(size_t)sv * Vp + v] : dinf();
-        const double bc0 = ws < dinf() ? 0.0 + ws : dmax();
-        // padding destinations and source-less lanes never pass (NaN)
-        thr[t] = (sv >= 0 && v < V) ? f32_thr(cd < bc0 ? cd : bc0) : __int_as_float(0x7fc00000);
-    }
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef __attribute__((address_space(1))) const f4 gf4;
-    const int32_t nchunks = (V + SRS - 1) / SRS;
-    const int32_t ncol = (V + BW - 1) / BW * BW;  // columns per chunk row of minW
-    uint32_t* hl = hitlog + ((size_t)blockIdx.x * 4 + wave) * nchunks;
-    const int32_t c0 = (int32_t)((int64_t)vt * BW / SRS % nchunks);  // the chunk holding the tile
-    auto chunk_of = [&](int32_t j) { const int32_t c = c0 + j; return c >= nchunks ? c - nchunks : c; };
-    float* myW = &sW[wave][0][0];
-    // live mask of order indices [base, base + nw): a chunk is live when some lane passes its
-    // bound min D32 <= max_t fl32(thr_t - min W32_t); dead chunks' hit log entries are zeroed
-    auto eval_window = [&](int32_t base, int32_t nw) -> unsigned long long {
-        unsigned long long m = 0ull;
-        for (int32_t j0 = 0; j0 < nw; j0 += EWG) {
-            // EWG chunks at a time: min D32 per lane, and the EWG x 8 column minima spread
-            // over the lanes (lane = 8 * chunk + column), broadcast by readlane
-            float md[EWG];
-#pragma unroll
-            for (int jj = 0; jj < EWG; ++jj) {
-                const int32_t c = chunk_of(base + (j0 + jj < nw ? j0 + jj : 0));
-                md[jj] = minD[((size_t)b * nchunks + c) * KL + lane];
-            }
-            const int32_t jl = (lane >> 3) < EWG ? (lane >> 3) : 0;
-            const int32_t cl = chunk_of(base + (j0 + jl < nw ? j0 + jl : 0));
-            const float mwl = minW[(size_t)cl * ncol + v0 + (lane & 7)];
-#pragma unroll
-            for (int jj = 0; jj < EWG; ++jj) {
-                float tm = thr[0] - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mwl), jj * 8));
-#pragma unroll
-                for (int t = 1; t < TDT; ++t)
-                    tm = fmaxf(tm, thr[t] - __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mwl), jj * 8 + t)));
-                if (__ballot(md[jj] <= tm) && j0 + jj < nw) m |= 1ull << (j0 + jj);
-            }
-        }
-        if (lane < nw && !((m >> lane) & 1ull)) hl[chunk_of(base + lane)] = 0u;
-        return m;
-    };
-    int32_t win_base = -1, win_n = 0;
-    unsigned long long win_m = 0ull;
-    auto next_live = [&](int32_t j) -> int32_t {
-        while (j < nchunks) {
-            const int32_t wb = j == 0 ? 0 : 1 + ((j - 1) / 64) * 64;
-            if (wb != win_base) {
-                win_base = wb;
-                win_n = wb == 0 ? 1 : (nchunks - wb < 64 ? nchunks - wb : 64);
-                win_m = eval_window(wb, win_n);
-            }
-            const unsigned long long m = win_m & (~0ull << (j - wb));
-            if (m) return wb + __builtin_ctzll(m);
-            j = wb + win_n;
-        }
-        return -1;
-    };
-    // a chunk's D32 rows (lane = source) into registers, its 32 x 8 W32 slice as one float4 per
-    // lane (row lane & 31, columns 4 (lane >> 5) ..)
-    auto load = [&](int32_t j, float (&d)[SRS], f4& w) {
-        const int32_t u0 = chunk_of(j) * SRS;
-#pragma unroll
-        for (int r = 0; r < SRS; ++r) {
-            const int32_t u = __builtin_amdgcn_readfirstlane(perm[u0 + r]);
-            d[r] = B.D32[(size_t)u * KL + lane];
-        }
-        w = *(gf4*)((const gfloat*)W32p + (size_t)(u0 + (lane & 31)) * Vp + v0 + 4 * (lane >> 5));
-    };
-    auto process = [&](int32_t j, const float (&d)[SRS], const f4& w, int buf) {
-        float* sw = myW + buf * SRS * TDT;
-        *(f4*)&sw[(lane & 31) * TDT + 4 * (lane >> 5)] = w;  // this wave's slice only: in-order LDS, no barrier
-        __builtin_amdgcn_wave_barrier();
-        uint32_t hits = 0u;
-#pragma unroll  // full: d[r] must index registers
-        for (int r = 0; r < SRS; ++r) {
-            const f4* wr = (const f4*)&sw[r * TDT];
-            const f4 wa = wr[0], wb = wr[1];
-            const float du = d[r];
-            const f2 x0 = f2{thr[0], thr[1]} - f2{wa.x, wa.y};
-            const f2 x1 = f2{thr[2], thr[3]} - f2{wa.z, wa.w};
-            const f2 x2 = f2{thr[4], thr[5]} - f2{wb.x, wb.y};
-            const f2 x3 = f2{thr[6], thr[7]} - f2{wb.z, wb.w};
-            float g = fmaxf(fmaxf(x0.x, x0.y), x1.x);
-            g = fmaxf(fmaxf(g, x1.y), x2.x);
-            g = fmaxf(fmaxf(g, x2.y), x3.x);
-            g = fmaxf(g, x3.y);
-            if (__ballot(du <= g)) {
-                hits |= 1u << r;
-                const float wj[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-                for (int t = 0; t < TDT; ++t) {
-                    const float c32 = du + wj[t];
-                    if (c32 < __int_as_float(0x7f800000))
-                        thr[t] = fminf(thr[t], __int_as_float(__float_as_int(c32) + 9));
-                }
-            }
-        }
-        if (lane == 0) hl[chunk_of(j)] = hits;
-        __builtin_amdgcn_wave_barrier();
-    };
-    {
-        float dA[SRS], dB[SRS];
-        f4 wA, wB;
-        int32_t ja = next_live(0);
-        if (ja >= 0) load(ja, dA, wA);
-        while (ja >= 0) {
-            const int32_t jb = next_live(ja + 1);
-            if (jb >= 0) load(jb, dB, wB);
-            process(ja, dA, wA, 0);
-            if (jb < 0) break;
-            ja = next_live(jb + 1);
-            if (ja >= 0) load(ja, dA, wA);
-            process(jb, dB, wB, 1);
-        }
-    }
-    // exact f64 pass over the logged rows in row order (k_relax_dense_f's), from the seed state
-    double bc[TDT], bdu[TDT];
-    int32_t bu[TDT];
-    uint32_t tie = 0;
-#pragma unroll
-    for (int t = 0; t < TDT; ++t) {
-        const int32_t v = vid[t];
-        const double ws = (sv >= 0 && sv != v) ? W[(size_t)sv * Vp + v] : dinf();
-        if (ws < dinf()) {
-            bc[t] = 0.0 + ws;
-            bdu[t] = 0.0;
-            bu[t] = sv;
-        } else {
-            bc[t] = dmax();
-            bdu[t] = dinf();
-            bu[t] = -1;
-        }
-    }
-    const gdouble* Dl = B.D + lane;
-    const int32_t vl = perm[v0 + (lane & (TDT - 1))];
-    for (int32_t cb = 0; cb < nchunks; cb += 64) {
-        const uint32_t e = (cb + lane < nchunks) ? hl[cb + lane] : 0u;
-        unsigned long long cm = __ballot(e != 0u);
-        while (cm) {
-            const int ci = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            unsigned long long hrows = (uint32_t)__builtin_amdgcn_readlane((int)e, ci);
-            const int32_t u0 = (cb + ci) * SRS;
-            while (hrows) {
-                int32_t ur[XR];
-                int nr = 0;
-#pragma unroll
-                for (int x = 0; x < XR; ++x) {
-                    ur[x] = u0;
-                    if (hrows) {
-                        ur[x] = u0 + __builtin_ctzll(hrows);
-                        hrows &= hrows - 1;
-                        nr = x + 1;
-                    }
-                    ur[x] = perm[ur[x]];  // row index -> vertex
-                }
-                double d64[XR], wl[XR];
-#pragma unroll
-                for (int x = 0; x < XR; ++x) {
-                    d64[x] = Dl[(size_t)ur[x] * KL];
-                    wl[x] = W[(size_t)ur[x] * Vp + vl];
-                }
-#pragma unroll
-                for (int x = 0; x < XR; ++x) {
-                    if (x >= nr) break;
-                    const int32_t u = ur[x];
-                    const bool own = (u == sv);
-#pragma unroll
-                    for (int t = 0; t < TDT; ++t) {
-                        const double c = d64[x] + readlane_d(wl[x], t);
-                        if (__ballot((c <= bc[t]) & !own)) {
-                            if (!own) lex_update(c, d64[x], u, bc[t], bdu[t], bu[t], tie, 1u << t);
-                        }
-                    }
-                }
-            }
-        }
-    }
-    dense_epilogue<TDT>(B, lane, sv, v0, V, bc, bdu, bu, tie, WI, Vp, in_r, parity, cnt, b, vid);
 }
 
 // Pruned full sweep (k_relax_dense_f<.., PR = true>) inputs.
@@ -1576,14 +1324,8 @@ __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, in
     if (du == c) lt = LTIE;  // degenerate d(u) == d(v): the reference order is heap-dependent
     const int32_t arc = WI[(size_t)u * Vp + v];
     const size_t uidx = (size_t)u * KL + s;
-#ifdef EXP_NO_PRED_GATHER
-    const uint32_t hu = 0u;
-    const double ru = 1.0;
-    (void)uidx;
-#else
     const uint32_t hu = B.H[uidx];
     const double ru = B.R[uidx];
-#endif
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
     const double r = ru * in_r[arc];
     B.BDU[idx] = du;
@@ -2549,10 +2291,10 @@ struct shadowtopo_engine {
     int32_t opt_profile = 0;
     int32_t opt_dense_variant = 0;  // SHADOWTOPO_DENSE_F32 (default) or SHADOWTOPO_DENSE_F64
     int32_t opt_dense_tb = 1;       // batches per wave in the f32-filtered full sweep (1, 2 or 4)
-    int32_t opt_dense_sweep = 0;    // pruned f32 sweep: 0 = block-coupled (k_relax_dense_f), 1 = wave-independent (k_relax_dense_w)
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
     bool floor_ok = false;             // default_nb: the 24 GB budget floor was found free once
+    size_t pool_bytes = 0;             // device bytes the batch pools hold (ensure_batches)
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
@@ -2610,6 +2352,7 @@ void counting_sort(const std::vector<int32_t>& key, int32_t nkeys, std::vector<i
 void free_batches(shadowtopo_engine* eng) {
     for (void* p : eng->batch_allocs) (void)hipFree(p);
     eng->batch_allocs.clear();
+    eng->pool_bytes = 0;
     eng->pools = Pools{};
     eng->d_cnt = nullptr;
     if (eng->h_cnt) (void)hipHostFree(eng->h_cnt);
@@ -2646,6 +2389,10 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
 }
 int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     free_batches(eng);
+    const auto dev_alloc = [eng](std::vector<void*>& owner, void** p, size_t bytes) {
+        eng->pool_bytes += bytes;  // default_nb counts what the pools hold, not an estimate
+        return ::dev_alloc(owner, p, bytes);
+    };
     const size_t VK = (size_t)eng->Vp * KL;
     Pools& P = eng->pools;
     P.vk = (int64_t)VK;
@@ -2718,7 +2465,10 @@ hipError_t round_sync(shadowtopo_engine* eng, hipStream_t s) {
 int32_t default_nb(shadowtopo_engine* eng, int32_t rows) {
     const int32_t need = std::max(1, (rows + KL - 1) / KL);
     if (eng->opt_nb > 0) return std::min(eng->opt_nb, need);
-    const double per_batch = (double)eng->Vp * KL * state_bytes(eng) + 18.0 * eng->Vp + (eng->dense ? 0.0 : 36.0 * eng->Vp);
+    // ensure_batches' allocations per slot: the state, act flags (2 B) and change masks
+    // (16 B) per vertex, the worklist (16 B per vertex, sparse), and the per-lane tables
+    const double per_batch = (double)eng->Vp * KL * state_bytes(eng) + 18.0 * eng->Vp +
+                             (eng->dense ? 0.0 : 16.0 * eng->Vp) + 8.0 * KL + 160.0;
     const double cap = eng->dense ? 16.0 : 256.0;
     // the budget is never under a 24 GB floor (times the share) once one free-memory query of
     // this engine found the floor free: when it already holds every batch, later calls (one
@@ -2727,7 +2477,10 @@ int32_t default_nb(shadowtopo_engine* eng, int32_t rows) {
     if (eng->floor_ok && std::min(cap, std::floor(floor_b / per_batch)) >= (double)need) return need;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    const double held = (double)eng->nb_cap * per_batch;  // slots this engine already owns
+    // the slots this engine already owns, as allocated: an estimate above the real size would
+    // grow the budget from one call to the next and reallocate the pools every step (r03: C5
+    // paid 1.3 s per step for that after the change-record pool was dropped)
+    const double held = (double)eng->pool_bytes;
     if ((double)free_b + held >= floor_b) eng->floor_ok = true;
     // engines sharing one device (SHADOWTOPO_DEVICES listing it twice) split the budget
     const double budget = std::max(eng->floor_ok ? floor_b : 0.0,
@@ -2761,11 +2514,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
     constexpr int TDT = FTDT, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
-    #ifdef EXP_DENSE_XCD_PAIR
-    const int64_t nblocks = 8 * (int64_t)((ngroups + 7) / 8) * ntb;
-#else
-    const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
-#endif
+        const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
     const size_t nchunks = (size_t)((eng->V + SRS - 1) / SRS);
     const size_t need = (size_t)nblocks * 4 * TB * nchunks;
     if (eng->hitlog_n < need) {
@@ -2788,12 +2537,6 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
         }
         hipLaunchKernelGGL(k_min_d32, dim3((uint32_t)((nchunks + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
                            eng->d_perm, (int32_t)nchunks, eng->d_minD);
-        if (TB == 1 && eng->opt_dense_sweep == 1) {
-            hipLaunchKernelGGL((k_relax_dense_w<TDT, XR>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32p,
-                               eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh,
-                               cnt_prev, cnt_cur, eng->d_hitlog, eng->d_perm, eng->d_minW, eng->d_minD);
-            return hipGetLastError();
-        }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                            eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
@@ -3652,7 +3395,7 @@ int ensure_mirrors(shadowtopo_engine* eng) {
 }  // namespace
 
 extern "C" {
-#ifdef EXP_PHASE_TIME
+#ifdef SHADOWTOPO_PHASE_STAMPS
 int shadowtopo_exp_phase(unsigned long long* out, int nblocks) {
     if (nblocks > PHASE_BLOCKS) nblocks = PHASE_BLOCKS;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * (size_t)nblocks) ==
@@ -3961,10 +3704,6 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             // slower on every config and are gone
             if (value != SHADOWTOPO_CSR_FULL)
                 return fail(SHADOWTOPO_EINVAL, "CSR variant %lld: only SHADOWTOPO_CSR_FULL exists", (long long)value);
-            return SHADOWTOPO_OK;
-        case SHADOWTOPO_OPT_DENSE_SWEEP:
-            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense sweep must be 0 or 1");
-            eng->opt_dense_sweep = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SOURCE_ORDER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "source order must be 0 or 1");

@@ -12,6 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# SHADOWTOPO_EXP_LIB: an experiment build of the same sources (_exp/build_variant.sh, e.g. the
+# phase-stamp diagnostic) for A/B runs; the product, the tests and the bench load _build/
 LIB_PATH = os.environ.get("SHADOWTOPO_EXP_LIB") or os.path.join(HERE, "_build", "libshadowtopo_hip.so")
 
 F_DIRECTED = 0x1
@@ -46,7 +48,6 @@ OPT_WORKLIST = 14
 OPT_GRID_X = 15
 OPT_PRUNE_PENDANT = 16
 OPT_DEVICE_ROUNDS = 17
-OPT_DENSE_SWEEP = 18
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (k_relax / k_relax_wl: the only sparse family)
 
 # every symbol include/shadowtopo.h declares

@@ -319,50 +319,6 @@ def test_dense_prune_same_results(case):
         assert compare(g, layout="dense")["dense"] == 1
 
 
-@pytest.mark.parametrize("case", ["sparse", "directed", "ties", "vloss_prefer", "geometric_odd", "geometric_big"])
-def test_dense_wave_sweep_same_results(case):
-    """OPT_DENSE_SWEEP = 1 (k_relax_dense_w: wave-independent, register-staged chunks, per-wave
-    liveness windows) gives rows and matrices bit-identical to the block-coupled sweep
-    (k_relax_dense_f) and to the oracle, including several batch groups and full sweeps
-    beyond round 1 (delta threshold 0: every round is a full sweep)."""
-    if case == "sparse":
-        g = synth.random_sparse(V=301, avg_deg=5, seed=2)
-    elif case == "directed":
-        g = synth.random_sparse(V=203, avg_deg=4, seed=5, directed=True)
-    elif case == "ties":
-        g = synth.integer_grid(rows=9, cols=11, seed=2)
-    elif case == "vloss_prefer":
-        rng = np.random.default_rng(4)
-        g = synth.random_sparse(V=150, avg_deg=8, seed=6, vloss=rng.uniform(0, 0.1, 150))
-        g.prefer_direct = True
-    elif case == "geometric_odd":
-        g = synth.geometric_complete_ish(V=611, A=150)  # V not a multiple of 64, 3 batches
-    else:
-        g = synth.geometric_complete_ish(V=2500, A=400, drop=0.2)  # 7 batches, many skipped chunks
-    srcs = np.arange(0, g.n, 3, dtype=np.int32)
-    rows, mats = [], []
-    for sweep, permille, nb in ((0, 125, 0), (1, 125, 0), (1, 0, 0), (1, 125, 2)):
-        eng = E.Engine.from_synth(g, layout="dense")
-        eng.set_option(E.OPT_DENSE_SWEEP, sweep)
-        eng.set_option(E.OPT_DELTA_PERMILLE, permille)
-        if nb:
-            eng.set_option(E.OPT_BATCHES_IN_FLIGHT, nb)
-        eng.set_attached(g.attached)
-        mats.append(eng.compute_rows(want_kind=True))
-        rows.append(eng.sssp(srcs))
-        eng.close()
-    for k in range(1, len(rows)):
-        assert np.array_equal(rows[0][0].view(np.uint64), rows[k][0].view(np.uint64))
-        assert np.array_equal(rows[0][3], rows[k][3])
-        ok = rows[0][3] == 0
-        assert np.array_equal(rows[0][1][ok], rows[k][1][ok]) and np.array_equal(rows[0][2][ok], rows[k][2][ok])
-        for x, y in zip(mats[0], mats[k]):
-            assert np.array_equal(x.view(np.uint8) if x.dtype == np.float64 else x,
-                                  y.view(np.uint8) if y.dtype == np.float64 else y)
-    if case != "geometric_big":
-        assert compare(g, layout="dense", dense_sweep=1)["dense"] == 1
-
-
 @pytest.mark.parametrize("layout", ["csr", "dense"])
 def test_pinned_host_rows_pipelined(layout):
     """Rows into page-locked host memory (the shim's path): with several batch groups the
