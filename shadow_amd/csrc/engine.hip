@@ -1003,48 +1003,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         uint32_t hits[TB];
 #pragma unroll
         for (int k = 0; k < TB; ++k) hits[k] = 0;
-#pragma unroll 8  // rows per unrolled step (2: +3 %, 1: +6 %)
-        for (int r = 0; r < (run ? SRS : 0); ++r) {
-            const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
-            f4 w4[TDT / 4];
+        // Rows in branch-free groups of RG: the group's filter results are collected first
+        // (one wave vote per row into a scalar mask), so the LDS reads of the whole group can
+        // be in flight together; a per-row branch on the vote made every row wait out its own
+        // LDS latency (s_waitcnt lgkmcnt(0) per row, r03).  Passing rows then tighten the
+        // thresholds in row order; rows of the group after a passing row were filtered
+        // against the slightly older thresholds, so a few more rows may be logged -- a
+        // superset, which the exact pass resolves to the same lexicographic minimum.
+        constexpr int RG = 8;
+        for (int r0 = 0; r0 < (run ? SRS : 0); r0 += RG) {
+            uint32_t pm[TB];
 #pragma unroll
-            for (int j = 0; j < TDT / 4; ++j) {
-                w4[j] = wr[j];
+            for (int k = 0; k < TB; ++k) pm[k] = 0u;
+#pragma unroll
+            for (int rr = 0; rr < RG; ++rr) {
+                const int r = r0 + rr;
+                const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
+                f4 w4[TDT / 4];
+#pragma unroll
+                for (int j = 0; j < TDT / 4; ++j) w4[j] = wr[j];
+#pragma unroll
+                for (int k = 0; k < TB; ++k) {
+                    const float du = sD[cur][k][r * KL + lane];
+                    // slacks thr_t - w_t two at a time (v_pk_add_f32), their max as a chain of
+                    // 3-input maxima (v_max3)
+                    typedef float f2 __attribute__((ext_vector_type(2)));
+                    float x[TDT];
+#pragma unroll
+                    for (int j = 0; j < TDT / 4; ++j) {
+                        const f2 a = f2{thr[k][4 * j], thr[k][4 * j + 1]} - f2{w4[j].x, w4[j].y};
+                        const f2 c = f2{thr[k][4 * j + 2], thr[k][4 * j + 3]} - f2{w4[j].z, w4[j].w};
+                        x[4 * j] = a.x;
+                        x[4 * j + 1] = a.y;
+                        x[4 * j + 2] = c.x;
+                        x[4 * j + 3] = c.y;
+                    }
+                    float g = fmaxf(fmaxf(x[0], x[1]), x[2]);
+#pragma unroll
+                    for (int t = 3; t + 1 < TDT; t += 2) g = fmaxf(fmaxf(g, x[t]), x[t + 1]);
+                    if (TDT % 2 == 0) g = fmaxf(g, x[TDT - 1]);
+                    pm[k] |= (__ballot(du <= g) != 0ull) ? (1u << rr) : 0u;
+                }
             }
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
-                const float du = sD[cur][k][r * KL + lane];
-                // slacks thr_t - w_t two at a time (v_pk_add_f32), their max as a chain of
-                // 3-input maxima (v_max3)
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                float x[TDT];
-#pragma unroll
-                for (int j = 0; j < TDT / 4; ++j) {
-                    const f2 a = f2{thr[k][4 * j], thr[k][4 * j + 1]} - f2{w4[j].x, w4[j].y};
-                    const f2 c = f2{thr[k][4 * j + 2], thr[k][4 * j + 3]} - f2{w4[j].z, w4[j].w};
-                    x[4 * j] = a.x;
-                    x[4 * j + 1] = a.y;
-                    x[4 * j + 2] = c.x;
-                    x[4 * j + 3] = c.y;
-                }
-                float g = fmaxf(fmaxf(x[0], x[1]), x[2]);
-#pragma unroll
-                for (int t = 3; t + 1 < TDT; t += 2) g = fmaxf(fmaxf(g, x[t]), x[t + 1]);
-                if (TDT % 2 == 0) g = fmaxf(g, x[TDT - 1]);
-                if (__ballot(du <= g)) {
-                    hits[k] |= 1u << r;
+                hits[k] |= pm[k] << r0;
+                for (uint32_t m = pm[k]; m; m &= m - 1) {
                     // c_exact <= fl32(D32 + W32) * (1 + 2^-22) <= that + 5 ulps, and f32_thr
                     // adds 4 ulps: every lane may lower thr_t to bits(c32) + 9 (a no-op where
                     // the row did not pass)
+                    const int r = r0 + __builtin_ctz(m);
+                    const float du = sD[cur][k][r * KL + lane];
+                    const float* wr = &sW[cur][r * BW + wave * TDT];
 #pragma unroll
-                    for (int j = 0; j < TDT / 4; ++j) {
-                        const float wj[4] = {w4[j].x, w4[j].y, w4[j].z, w4[j].w};
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const float c32 = du + wj[i];
-                            if (c32 < __int_as_float(0x7f800000))
-                                thr[k][4 * j + i] = fminf(thr[k][4 * j + i], __int_as_float(__float_as_int(c32) + 9));
-                        }
+                    for (int t = 0; t < TDT; ++t) {
+                        const float c32 = du + wr[t];
+                        if (c32 < __int_as_float(0x7f800000))
+                            thr[k][t] = fminf(thr[k][t], __int_as_float(__float_as_int(c32) + 9));
                     }
                 }
             }
