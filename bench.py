@@ -439,6 +439,7 @@ def main():
     log(f"[rank {rank}] workload {desc}: E={g.m} built in {time.perf_counter() - t:.1f}s; rows [{r0},{r1})")
     t_cold = t = time.perf_counter()
     eng = E.Engine.from_synth(g, device=local)
+    create_ms = (time.perf_counter() - t_cold) * 1e3
     eng.set_attached(g.attached)
     eng.set_option(E.OPT_TIMING, 1)
     if args.profile_counts:
@@ -567,6 +568,12 @@ def main():
                        "delta_sweeps_per_step": st["delta_sweeps"] / args.steps,
                        "host_buffers_ms": host_ms, "host_buffers_pageable_ms": host_pageable_ms,
                        "cold_start_ms": cold_start_ms,
+                       # where the cold start goes: shadowtopo_create (edge validation, upload,
+                       # device build), the dense locality order, the rest of the first step
+                       "cold_start_parts_ms": {"create": create_ms, "validate": st["create_validate_ms"],
+                                               "upload": st["create_upload_ms"], "build": st["create_build_ms"],
+                                               "order": st["order_ms"],
+                                               "first_step": cold_start_ms - create_ms},
                        "host_buffers_source_paths_per_s": (rows / host_ms * 1e3) if host_ms else None},
         }
         print(json.dumps(out), flush=True)

@@ -160,6 +160,13 @@ typedef struct shadowtopo_stats {
     int64_t pruned_vertices; /* CSR: vertices the relaxation view leaves out (OPT_PRUNE_PENDANT) */
     int64_t pool_allocs;     /* batch-pool (re)allocations (a computation needing more slots than held) */
     double pool_alloc_ms;    /* host wall time of those allocations */
+    /* cold start (kept across shadowtopo_reset_stats): host wall time of shadowtopo_create's
+       edge validation, edge-list upload and device table build (dense tables included), and
+       of the dense locality order built on the first computation */
+    double create_validate_ms;
+    double create_upload_ms;
+    double create_build_ms;
+    double order_ms;
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

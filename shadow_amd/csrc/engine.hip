@@ -830,16 +830,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     // before the far chunks are tested
     const int32_t c0 = PR ? (int32_t)((int64_t)vt * BW / SRS % nchunks) : 0;  // the chunk holding the tile
     auto chunk_of = [&](int32_t j) { return PR ? (c0 + j) % nchunks : j; };
-    // fetch the chunk of order index j into registers (rows in the locality order: PR reads
-    // each row's vertex from perm, an L2-resident 40 KB table)
-    auto fetch = [&](int32_t j) {
-        const int32_t c = chunk_of(j);
-        const int32_t u0 = c * SRS;
-        int32_t prow[DQ];
+    // PR: the vertices of this thread's rows of the chunk of order index j (perm, an
+    // L2-resident 40 KB table).  Loaded one chunk ahead of the fetch that uses them, so the
+    // D32 row loads never wait on a dependent perm load.
+    auto perm_of = [&](int32_t j, int32_t* prow) {
         if (PR) {
+            const int32_t u0 = chunk_of(j) * SRS;
 #pragma unroll
             for (int i = 0; i < DQ; ++i) prow[i] = perm[u0 + (threadIdx.x + i * 256) / (KL / 4)];
         }
+    };
+    // fetch the chunk of order index j into registers (rows in the locality order: prow
+    // holds each row's vertex, from perm_of)
+    auto fetch = [&](int32_t j, const int32_t* prow) {
+        const int32_t c = chunk_of(j);
+        const int32_t u0 = c * SRS;
 #pragma unroll
         for (int k = 0; k < TB; ++k)
 #pragma unroll
@@ -961,12 +966,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         return -1;
     };
     PHASE_STAMP(1);
+    // chunks in flight: itc (in LDS, filtered this iteration), itn (its loads issued this
+    // iteration, staged at its end) and itn2 (its rows' perm entries loaded this iteration)
+    int32_t prow_n[DQ];
     int32_t itc = next_live(0);
     if (itc >= 0) {
-        fetch(itc);
+        perm_of(itc, prow_n);
+        fetch(itc, prow_n);
         stash(0);
         advance();
     }
+    int32_t itn = itc >= 0 ? next_live(itc + 1) : -1;
+    if (itn >= 0) perm_of(itn, prow_n);
     __syncthreads();
     int bufc = 0;
 #ifdef SHADOWTOPO_PHASE_STAMPS
@@ -980,9 +991,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         const int32_t c = chunk_of(itc);
         const int32_t u0 = c * SRS;
         const int cur = bufc;
-        const int32_t itn = next_live(itc + 1);  // block-uniform (a window evaluation holds a barrier)
         const bool more = itn >= 0;
-        if (more) fetch(itn);
+        if (more) fetch(itn, prow_n);
+        // block-uniform (a window evaluation holds a barrier); a window evaluated one chunk
+        // earlier uses slightly older thresholds, which only skips less
+        const int32_t itn2 = more ? next_live(itn + 1) : -1;
+        if (itn2 >= 0) perm_of(itn2, prow_n);
         bool run = true;
         if (PR) {
             bool p = false;
@@ -1003,63 +1017,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         uint32_t hits[TB];
 #pragma unroll
         for (int k = 0; k < TB; ++k) hits[k] = 0;
-        // Rows in branch-free groups of RG: the group's filter results are collected first
-        // (one wave vote per row into a scalar mask), so the LDS reads of the whole group can
-        // be in flight together; a per-row branch on the vote made every row wait out its own
-        // LDS latency (s_waitcnt lgkmcnt(0) per row, r03).  Passing rows then tighten the
-        // thresholds in row order; rows of the group after a passing row were filtered
-        // against the slightly older thresholds, so a few more rows may be logged -- a
-        // superset, which the exact pass resolves to the same lexicographic minimum.
-        constexpr int RG = 8;
-        for (int r0 = 0; r0 < (run ? SRS : 0); r0 += RG) {
-            uint32_t pm[TB];
+#pragma unroll 8  // rows per unrolled step (2: +3 %, 1: +6 %)
+        for (int r = 0; r < (run ? SRS : 0); ++r) {
+            const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
+            f4 w4[TDT / 4];
 #pragma unroll
-            for (int k = 0; k < TB; ++k) pm[k] = 0u;
-#pragma unroll
-            for (int rr = 0; rr < RG; ++rr) {
-                const int r = r0 + rr;
-                const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
-                f4 w4[TDT / 4];
-#pragma unroll
-                for (int j = 0; j < TDT / 4; ++j) w4[j] = wr[j];
-#pragma unroll
-                for (int k = 0; k < TB; ++k) {
-                    const float du = sD[cur][k][r * KL + lane];
-                    // slacks thr_t - w_t two at a time (v_pk_add_f32), their max as a chain of
-                    // 3-input maxima (v_max3)
-                    typedef float f2 __attribute__((ext_vector_type(2)));
-                    float x[TDT];
-#pragma unroll
-                    for (int j = 0; j < TDT / 4; ++j) {
-                        const f2 a = f2{thr[k][4 * j], thr[k][4 * j + 1]} - f2{w4[j].x, w4[j].y};
-                        const f2 c = f2{thr[k][4 * j + 2], thr[k][4 * j + 3]} - f2{w4[j].z, w4[j].w};
-                        x[4 * j] = a.x;
-                        x[4 * j + 1] = a.y;
-                        x[4 * j + 2] = c.x;
-                        x[4 * j + 3] = c.y;
-                    }
-                    float g = fmaxf(fmaxf(x[0], x[1]), x[2]);
-#pragma unroll
-                    for (int t = 3; t + 1 < TDT; t += 2) g = fmaxf(fmaxf(g, x[t]), x[t + 1]);
-                    if (TDT % 2 == 0) g = fmaxf(g, x[TDT - 1]);
-                    pm[k] |= (__ballot(du <= g) != 0ull) ? (1u << rr) : 0u;
-                }
+            for (int j = 0; j < TDT / 4; ++j) {
+                w4[j] = wr[j];
             }
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
-                hits[k] |= pm[k] << r0;
-                for (uint32_t m = pm[k]; m; m &= m - 1) {
+                const float du = sD[cur][k][r * KL + lane];
+                // slacks thr_t - w_t two at a time (v_pk_add_f32), their max as a chain of
+                // 3-input maxima (v_max3)
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                float x[TDT];
+#pragma unroll
+                for (int j = 0; j < TDT / 4; ++j) {
+                    const f2 a = f2{thr[k][4 * j], thr[k][4 * j + 1]} - f2{w4[j].x, w4[j].y};
+                    const f2 c = f2{thr[k][4 * j + 2], thr[k][4 * j + 3]} - f2{w4[j].z, w4[j].w};
+                    x[4 * j] = a.x;
+                    x[4 * j + 1] = a.y;
+                    x[4 * j + 2] = c.x;
+                    x[4 * j + 3] = c.y;
+                }
+                float g = fmaxf(fmaxf(x[0], x[1]), x[2]);
+#pragma unroll
+                for (int t = 3; t + 1 < TDT; t += 2) g = fmaxf(fmaxf(g, x[t]), x[t + 1]);
+                if (TDT % 2 == 0) g = fmaxf(g, x[TDT - 1]);
+                if (__ballot(du <= g)) {
+                    hits[k] |= 1u << r;
                     // c_exact <= fl32(D32 + W32) * (1 + 2^-22) <= that + 5 ulps, and f32_thr
                     // adds 4 ulps: every lane may lower thr_t to bits(c32) + 9 (a no-op where
                     // the row did not pass)
-                    const int r = r0 + __builtin_ctz(m);
-                    const float du = sD[cur][k][r * KL + lane];
-                    const float* wr = &sW[cur][r * BW + wave * TDT];
 #pragma unroll
-                    for (int t = 0; t < TDT; ++t) {
-                        const float c32 = du + wr[t];
-                        if (c32 < __int_as_float(0x7f800000))
-                            thr[k][t] = fminf(thr[k][t], __int_as_float(__float_as_int(c32) + 9));
+                    for (int j = 0; j < TDT / 4; ++j) {
+                        const float wj[4] = {w4[j].x, w4[j].y, w4[j].z, w4[j].w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            // branch-free (v_cndmask): an infinite or NaN candidate, or a bound
+                            // that would wrap past +inf into a NaN pattern, leaves thr as it is
+                            const float c32 = du + wj[i];
+                            const float nb = __int_as_float(__float_as_int(c32) + 9);
+                            float& th = thr[k][4 * j + i];
+                            th = ((c32 < __int_as_float(0x7f800000)) & (nb < th)) ? nb : th;
+                        }
                     }
                 }
             }
@@ -1078,6 +1080,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         __syncthreads();
         bufc ^= 1;
         itc = itn;
+        itn = itn2;
     }
     PHASE_STAMP(2);
     PHASE_SET(5, nvisit);
@@ -3066,6 +3069,7 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->vperm_ready || !eng->dense || !eng->opt_dense_prune || !eng->d_W32) return SHADOWTOPO_OK;
     const int32_t V = eng->V, Vp = eng->Vp;
     if (V <= SRS) return SHADOWTOPO_OK;
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<int32_t> all((size_t)V);
     for (int32_t v = 0; v < V; ++v) all[v] = v;
     std::vector<uint64_t>& key = eng->h_vkey;
@@ -3091,6 +3095,7 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     eng->vperm_ready = true;
+    eng->st.order_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return SHADOWTOPO_OK;
 }
 
@@ -3437,6 +3442,9 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         return fail(SHADOWTOPO_EINVAL, "NULL edge array");
     const int32_t V = n_vertices;
     const bool directed = flags & SHADOWTOPO_F_DIRECTED;
+    using clk = std::chrono::steady_clock;
+    const auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+    auto t_phase = clk::now();
     int64_t n_loops = 0;
     for (int64_t e = 0; e < n_edges; ++e) {
         n_loops += edge_source[e] == edge_target[e];
@@ -3454,6 +3462,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
 
     auto* eng = new (std::nothrow) shadowtopo_engine();
     if (!eng) return fail(SHADOWTOPO_ENOMEM, "engine alloc");
+    eng->st.create_validate_ms = ms_since(t_phase);
+    t_phase = clk::now();
     eng->V = V;
     eng->E = n_edges;
     eng->device = device;
@@ -3481,6 +3491,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
             if (e == hipSuccess) e = hipMemcpy(d_lat, edge_latency, (size_t)n_edges * 8, hipMemcpyHostToDevice);
             if (e == hipSuccess) e = hipMemcpy(d_loss, edge_packetloss, (size_t)n_edges * 8, hipMemcpyHostToDevice);
         }
+        eng->st.create_upload_ms = ms_since(t_phase);
+        t_phase = clk::now();
         hipStream_t bs = nullptr;
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
         if (e == hipSuccess)
@@ -3598,6 +3610,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
     }
+    eng->st.create_build_ms = ms_since(t_phase);
     eng->st.n_vertices = V;
     eng->st.n_edges = n_edges;
     eng->st.n_arcs = eng->n_arcs;
@@ -3866,6 +3879,10 @@ void shadowtopo_reset_stats(shadowtopo_engine* eng) {
     eng->st.device = keep.device;
     eng->st.multigraph = keep.multigraph;
     eng->st.dense = keep.dense;
+    eng->st.create_validate_ms = keep.create_validate_ms;
+    eng->st.create_upload_ms = keep.create_upload_ms;
+    eng->st.create_build_ms = keep.create_build_ms;
+    eng->st.order_ms = keep.order_ms;
 }
 
 int shadowtopo_is_complete(const shadowtopo_engine* eng) {

@@ -78,6 +78,8 @@ class Stats(ctypes.Structure):
         ("wl_launches", ctypes.c_int64), ("wl_ms", ctypes.c_double), ("sparse_deltas", ctypes.c_int64),
         ("self_ms", ctypes.c_double), ("self_paths", ctypes.c_int64), ("pruned_deltas", ctypes.c_int64),
         ("pruned_vertices", ctypes.c_int64), ("pool_allocs", ctypes.c_int64), ("pool_alloc_ms", ctypes.c_double),
+        ("create_validate_ms", ctypes.c_double), ("create_upload_ms", ctypes.c_double),
+        ("create_build_ms", ctypes.c_double), ("order_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
