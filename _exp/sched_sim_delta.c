@@ -10,6 +10,9 @@
 #include <stdlib.h>
 #include <string.h>
 #define KL 64
+#ifndef WIN
+#define WIN 0  /* 0: Jacobi rounds; W > 0: a window of W vertices reads the values at its start */
+#endif
 static int32_t V; static int64_t M; static int64_t* ptr; static int32_t* src; static double* w;
 static int32_t nsrc; static int32_t* srcs;
 static void dijkstra1(int s, double* d) { // simple O(V^2)-free binary heap dijkstra
@@ -62,10 +65,12 @@ int main(int argc, char** argv) {
       if (!anyp && !anya) break;
       if (!anya) { for (int l = 0; l < KL; l++) T[l] += delta; phases++; continue; }
       phases++;
-      while (anya) {  // rounds within the phase (Jacobi)
+      while (anya) {  // rounds within the phase (Jacobi, or Gauss-Seidel with window W)
         rounds++; anya = 0; memset(actn, 0, V);
         memcpy(Dn, D, 8 * (size_t)V * KL);
-        for (int v = 0; v < V; v++) if (act[v]) {
+        for (int v = 0; v < V; v++) {
+          if (WIN > 0 && v % WIN == 0 && v) memcpy(D + (size_t)(v - WIN) * KL, Dn + (size_t)(v - WIN) * KL, 8 * (size_t)WIN * KL);
+          if (!act[v]) continue;
           act[v] = 0; visits++; rows += ptr[v+1]-ptr[v];
           uint64_t prop = 0;
           for (int l = 0; l < KL; l++) { if (s[l] == v) continue; double bst = D[(size_t)v*KL+l];
