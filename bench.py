@@ -571,7 +571,8 @@ def main():
                        # where the cold start goes: shadowtopo_create (edge validation, upload,
                        # device build), the dense locality order, the rest of the first step
                        "cold_start_parts_ms": {"create": create_ms, "validate": st["create_validate_ms"],
-                                               "upload": st["create_upload_ms"], "build": st["create_build_ms"],
+                                               "upload": st["create_upload_ms"],
+                                               "upload_alloc": st["create_alloc_ms"], "build": st["create_build_ms"],
                                                "order": st["order_ms"],
                                                "first_step": cold_start_ms - create_ms},
                        "host_buffers_source_paths_per_s": (rows / host_ms * 1e3) if host_ms else None},

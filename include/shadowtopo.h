@@ -167,6 +167,7 @@ typedef struct shadowtopo_stats {
     double create_upload_ms;
     double create_build_ms;
     double order_ms;
+    double create_alloc_ms;  /* of create_upload_ms: the device allocation of the edge buffers */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -5,7 +5,9 @@ sequence of queries -- so the tests can say what the drop-in getters must return
 It follows /root/reference/src/main/routing/topology.c:
   _topology_getPathEntry            :1969-2051  (cache lookup (s, t), then (t, s) when
                                                  undirected; on a miss: direct lookup,
-                                                 self path or one Dijkstra from s)
+                                                 self path or one Dijkstra from s; after a
+                                                 successful one (s, t), then (t, s) in ANY
+                                                 graph, :2033-2038)
   _topology_getPathFromCache        :1284-1303
   _topology_shouldStorePath         :1305-1334
   _topology_storePathInCache        :1336-1386  (running minimum -> worker_updateMinTimeJump)
@@ -23,19 +25,18 @@ import numpy as np
 
 
 class RefPathCache:
-    def __init__(self, lat, kind, *, directed, complete, prefer_direct, adjacent, reverse_blocks_directed=True):
+    def __init__(self, lat, kind, *, directed, complete, prefer_direct, adjacent):
         """lat / kind: [A, A] oracle matrices over attached indices (kind 0 = unroutable);
         adjacent(i, j): the graph has an edge i -> j (either way when undirected; i == j:
-        a self-loop).  reverse_blocks_directed: _topology_shouldStorePath refuses (s, t)
-        when (t, s) is cached even in a directed graph (topology.c:1311-1317), so there the
-        later query (s, t) finds no Path and fails; False models the drop-in, which stores
-        (s, t) in a directed graph (documented deviation)."""
+        a self-loop).  In a directed graph too, _topology_shouldStorePath refuses (s, t) once
+        (t, s) is cached (topology.c:1311-1317); the query (s, t) then misses every time
+        (a directed lookup tries (s, t) only), reruns s's Dijkstra, and returns the (t, s)
+        Path through the post-computation fallback (:2033-2038)."""
         self.lat = np.asarray(lat)
         self.kind = np.asarray(kind)
         self.A = self.lat.shape[0]
         self.directed, self.complete, self.prefer_direct = directed, complete, prefer_direct
         self.adjacent = adjacent
-        self.reverse_blocks = reverse_blocks_directed or not directed
         self.cache = {}          # (s, t) -> latency of the stored Path
         self.min_latency = 0.0   # topology.c minimumPathLatency
         self.upcalls = []        # every value handed to worker_updateMinTimeJump
@@ -47,7 +48,7 @@ class RefPathCache:
         return (s, t) if (s, t) in self.cache else None
 
     def _should_store(self, is_direct, s, t):
-        if (s, t) in self.cache or (self.reverse_blocks and (t, s) in self.cache):
+        if (s, t) in self.cache or (t, s) in self.cache:
             return False
         if self.complete and not is_direct:
             return False
@@ -65,14 +66,19 @@ class RefPathCache:
             self.upcalls.append(latency)
 
     # ---------------------------------------------------------------- miss branches
+    # each returns the reference's `success`
     def _lookup_direct(self, s, t):  # :1877-1927 (get_eid fails without an edge)
-        if self.adjacent(s, t):
-            self._store(True, s, t)
+        if not self.adjacent(s, t):
+            return False
+        self._store(True, s, t)
+        return True
 
     def _self_path(self, s):  # :1545-1653 (no incident edge: no path)
         self.self_paths += 1
-        if self.kind[s, s] != 0:
-            self._store(False, s, s)
+        if self.kind[s, s] == 0:
+            return False
+        self._store(False, s, s)
+        return True
 
     def _compute_source_paths(self, s, t):  # :1655-1875
         if s == t:
@@ -82,6 +88,7 @@ class RefPathCache:
             if self.kind[s, position] == 0:  # igraph returns an empty path: nothing stored
                 continue
             self._store(False, s, position)
+        return True
 
     # ---------------------------------------------------------------- :1969-2051
     def get_path_entry(self, s, t):
@@ -91,10 +98,11 @@ class RefPathCache:
             path = self._from_cache(t, s)
         if path is None:
             if self.complete or (self.prefer_direct and self.adjacent(s, t)):
-                self._lookup_direct(s, t)
+                success = self._lookup_direct(s, t)
             else:
-                self._compute_source_paths(s, t)
-            path = self._from_cache(s, t) or (None if self.directed else self._from_cache(t, s))
+                success = self._compute_source_paths(s, t)
+            if success:  # :2033-2038, directed or not
+                path = self._from_cache(s, t) or self._from_cache(t, s)
         return path
 
 

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -37,6 +38,7 @@
 #include <limits>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "graph_build.h"
@@ -3432,6 +3434,149 @@ int shadowtopo_device_count(void) {
 const char* shadowtopo_last_error(void) { return g_err.c_str(); }
 
 
+namespace {  // (internal linkage inside the extern "C" block)
+// ---------------------------------------------------------------- engine creation helpers
+// Host threads for the edge-list passes of shadowtopo_create: the box's CPU share, at most 16.
+int host_workers(int64_t n_edges) {
+    if (n_edges < (1 << 20)) return 1;
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+}
+
+// The edge checks of topology.c:1070 and :1090 (plus endpoint range) over [a, z): the first
+// failing edge, or z; loops counted into *loops.
+int64_t first_bad_edge(int32_t V, int64_t a, int64_t z, const int32_t* src, const int32_t* dst, const double* lat,
+                       const double* loss, int64_t* loops) {
+    int64_t nl = 0;
+    for (int64_t e = a; e < z; ++e) {
+        nl += src[e] == dst[e];
+        if (src[e] < 0 || src[e] >= V || dst[e] < 0 || dst[e] >= V || !(lat[e] > 0.0) || std::isinf(lat[e]) ||
+            !(loss[e] >= 0.0 && loss[e] <= 1.0)) {
+            *loops = nl;
+            return e;
+        }
+    }
+    *loops = nl;
+    return z;
+}
+
+// Validate the edge list with W threads, each over its own slice; the error names the first
+// failing edge in edge order, as one sequential scan would.
+int validate_edges(int32_t V, int64_t n_edges, const int32_t* src, const int32_t* dst, const double* lat,
+                   const double* loss, int64_t* n_loops) {
+    const int W = host_workers(n_edges);
+    std::vector<int64_t> bad((size_t)W, n_edges), loops((size_t)W, 0);
+    auto work = [&](int w) {
+        const int64_t a = n_edges * w / W, z = n_edges * (w + 1) / W;
+        const int64_t e = first_bad_edge(V, a, z, src, dst, lat, loss, &loops[w]);
+        bad[w] = e < z ? e : n_edges;
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < W; ++w) th.emplace_back(work, w);
+    work(0);
+    for (auto& t : th) t.join();
+    int64_t e = n_edges, nl = 0;
+    for (int w = 0; w < W; ++w) {
+        e = std::min(e, bad[w]);
+        nl += loops[w];
+    }
+    *n_loops = nl;
+    if (e == n_edges) return SHADOWTOPO_OK;
+    if (src[e] < 0 || src[e] >= V || dst[e] < 0 || dst[e] >= V)
+        return fail(SHADOWTOPO_EINVAL, "edge %lld endpoint out of range", (long long)e);
+    if (!(lat[e] > 0.0) || std::isinf(lat[e]))
+        return fail(SHADOWTOPO_EINVAL, "edge %lld latency must be > 0 (topology.c:1070)", (long long)e);
+    return fail(SHADOWTOPO_EINVAL, "edge %lld packetloss out of [0,1] (topology.c:1090)", (long long)e);
+}
+
+// Host -> device copies of the caller's (pageable) edge arrays through page-locked staging
+// (tools/upload/upload_bench.hip, profiles/r03n_upload.jsonl, C2's 1.2 GB on the GPU box):
+// hipMemcpy from pageable memory pins the source pages on first touch -- 80 ms, 15 GB/s for
+// a fresh array (21 ms once pinned) -- while two threads filling a ring of four 8 MB
+// page-locked buffers, each chunk's DMA issued in chunk order on one stream, move it at
+// ~50 GB/s.  The ring is allocated once per process (hipHostMalloc costs ~3 ms per buffer)
+// and kept; engine creations take it in turn.
+struct UploadPart {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+#define GB_TRY_HIP(expr)                  \
+    do {                                  \
+        hipError_t e_ = (expr);           \
+        if (e_ != hipSuccess) return e_;  \
+    } while (0)
+struct StagingRing {
+    static constexpr size_t CH = (size_t)8 << 20;
+    static constexpr int NB = 4;
+    std::mutex mu;
+    int device = -1;
+    hipStream_t st = nullptr;
+    void* buf[NB] = {};
+    hipEvent_t ev[NB] = {};
+};
+StagingRing g_ring;
+
+hipError_t upload_staged(int device, const std::vector<UploadPart>& parts) {
+    std::lock_guard<std::mutex> lk(g_ring.mu);
+    StagingRing& R = g_ring;
+    constexpr size_t CH = StagingRing::CH;
+    constexpr int NB = StagingRing::NB, W = 2;
+    if (R.device != device) {  // first use, or another device: (re)create on this one
+        if (R.st) (void)hipStreamDestroy(R.st);
+        for (int k = 0; k < NB; ++k) {
+            if (R.buf[k]) (void)hipHostFree(R.buf[k]);
+            if (R.ev[k]) (void)hipEventDestroy(R.ev[k]);
+            R.buf[k] = nullptr;
+            R.ev[k] = nullptr;
+        }
+        R.st = nullptr;
+        R.device = -1;
+        GB_TRY_HIP(hipStreamCreateWithFlags(&R.st, hipStreamNonBlocking));
+        for (int k = 0; k < NB; ++k) {
+            GB_TRY_HIP(hipHostMalloc(&R.buf[k], CH, hipHostMallocDefault));
+            GB_TRY_HIP(hipEventCreateWithFlags(&R.ev[k], hipEventDisableTiming));
+        }
+        R.device = device;
+    }
+    std::vector<std::pair<size_t, size_t>> chunks;  // (part, offset)
+    for (size_t p = 0; p < parts.size(); ++p)
+        for (size_t o = 0; o < parts[p].bytes; o += CH) chunks.emplace_back(p, o);
+    // chunk c fills buffer c % NB (after the DMA of chunk c - NB left it) on thread c % W, and
+    // its DMA is issued in chunk order (a ticket), so the ring is reused in order
+    std::atomic<size_t> ticket{0};
+    std::atomic<int> failed{0};
+    std::vector<hipError_t> err(W, hipSuccess);
+    auto work = [&](int w) {
+        hipError_t e = hipSetDevice(device);
+        for (size_t c = (size_t)w; c < chunks.size(); c += W) {
+            const int k = (int)(c % NB);
+            if (e == hipSuccess && c >= (size_t)NB) e = hipEventSynchronize(R.ev[k]);
+            if (e == hipSuccess) {
+                const UploadPart& pt = parts[chunks[c].first];
+                const size_t o = chunks[c].second, n = std::min(CH, pt.bytes - o);
+                std::memcpy(R.buf[k], static_cast<const char*>(pt.src) + o, n);
+                while (ticket.load(std::memory_order_acquire) != c && !failed.load(std::memory_order_relaxed))
+                    std::this_thread::yield();
+                e = hipMemcpyAsync(static_cast<char*>(pt.dst) + o, R.buf[k], n, hipMemcpyHostToDevice, R.st);
+                if (e == hipSuccess) e = hipEventRecord(R.ev[k], R.st);
+            }
+            if (e != hipSuccess) failed.store(1, std::memory_order_relaxed);
+            ticket.store(c + 1, std::memory_order_release);  // a failed chunk still passes the ticket on
+        }
+        err[w] = e;
+    };
+    std::thread helper(work, 1);
+    work(0);
+    helper.join();
+    const hipError_t e = hipStreamSynchronize(R.st);
+    for (hipError_t x : err)
+        if (x != hipSuccess) return x;
+    return e;
+}
+
+}  // namespace
+
 int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_source, const int32_t* edge_target,
                       const double* edge_latency, const double* edge_packetloss, const double* vertex_packetloss,
                       uint32_t flags, int32_t device, shadowtopo_engine** out) {
@@ -3446,14 +3591,9 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     const auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
     auto t_phase = clk::now();
     int64_t n_loops = 0;
-    for (int64_t e = 0; e < n_edges; ++e) {
-        n_loops += edge_source[e] == edge_target[e];
-        if (edge_source[e] < 0 || edge_source[e] >= V || edge_target[e] < 0 || edge_target[e] >= V)
-            return fail(SHADOWTOPO_EINVAL, "edge %lld endpoint out of range", (long long)e);
-        if (!(edge_latency[e] > 0.0) || std::isinf(edge_latency[e]))
-            return fail(SHADOWTOPO_EINVAL, "edge %lld latency must be > 0 (topology.c:1070)", (long long)e);
-        if (!(edge_packetloss[e] >= 0.0 && edge_packetloss[e] <= 1.0))
-            return fail(SHADOWTOPO_EINVAL, "edge %lld packetloss out of [0,1] (topology.c:1090)", (long long)e);
+    if (n_edges > 0) {
+        const int rcv = validate_edges(V, n_edges, edge_source, edge_target, edge_latency, edge_packetloss, &n_loops);
+        if (rcv) return rcv;
     }
     int ndev = shadowtopo_device_count();
     if (ndev <= 0) return fail(SHADOWTOPO_EDEVICE, "no HIP device visible");
@@ -3481,15 +3621,26 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         int32_t *d_src = nullptr, *d_dst = nullptr;
         double *d_lat = nullptr, *d_loss = nullptr;
         const size_t ne = (size_t)std::max<int64_t>(n_edges, 1);
-        hipError_t e = hipMalloc((void**)&d_src, ne * 4);
-        if (e == hipSuccess) e = hipMalloc((void**)&d_dst, ne * 4);
-        if (e == hipSuccess) e = hipMalloc((void**)&d_lat, ne * 8);
-        if (e == hipSuccess) e = hipMalloc((void**)&d_loss, ne * 8);
+        // the edge buffers become the graph's igraph storage (graph_build::build works in
+        // place): owned by the engine from here on
+        hipError_t e = hipSuccess;
+        for (auto& [p, bytes] : {std::pair<void**, size_t>{(void**)&d_src, ne * 4}, {(void**)&d_dst, ne * 4},
+                                 {(void**)&d_lat, ne * 8}, {(void**)&d_loss, ne * 8}}) {
+            if (e == hipSuccess) e = hipMalloc(p, bytes);
+            if (e == hipSuccess) eng->graph_allocs.push_back(*p);
+        }
+        eng->st.create_alloc_ms = ms_since(t_phase);
         if (e == hipSuccess && n_edges > 0) {
-            e = hipMemcpy(d_src, edge_source, (size_t)n_edges * 4, hipMemcpyHostToDevice);
-            if (e == hipSuccess) e = hipMemcpy(d_dst, edge_target, (size_t)n_edges * 4, hipMemcpyHostToDevice);
-            if (e == hipSuccess) e = hipMemcpy(d_lat, edge_latency, (size_t)n_edges * 8, hipMemcpyHostToDevice);
-            if (e == hipSuccess) e = hipMemcpy(d_loss, edge_packetloss, (size_t)n_edges * 8, hipMemcpyHostToDevice);
+            const size_t n = (size_t)n_edges;
+            if (n * 24 >= ((size_t)64 << 20)) {  // small lists: the pageable copy's pinning is cheap
+                e = upload_staged(device, {{d_src, edge_source, n * 4}, {d_dst, edge_target, n * 4},
+                                           {d_lat, edge_latency, n * 8}, {d_loss, edge_packetloss, n * 8}});
+            } else {
+                e = hipMemcpy(d_src, edge_source, n * 4, hipMemcpyHostToDevice);
+                if (e == hipSuccess) e = hipMemcpy(d_dst, edge_target, n * 4, hipMemcpyHostToDevice);
+                if (e == hipSuccess) e = hipMemcpy(d_lat, edge_latency, n * 8, hipMemcpyHostToDevice);
+                if (e == hipSuccess) e = hipMemcpy(d_loss, edge_packetloss, n * 8, hipMemcpyHostToDevice);
+            }
         }
         eng->st.create_upload_ms = ms_since(t_phase);
         t_phase = clk::now();
@@ -3499,10 +3650,6 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
             e = graph_build::build(V, n_edges, n_loops, directed, CSR_PAD, d_src, d_dst, d_lat, d_loss, bs, gb,
                                    eng->graph_allocs);
         if (bs) (void)hipStreamDestroy(bs);
-        (void)hipFree(d_src);
-        (void)hipFree(d_dst);
-        (void)hipFree(d_lat);
-        (void)hipFree(d_loss);
         if (e != hipSuccess) {
             shadowtopo_destroy(eng);
             return fail(e == hipErrorOutOfMemory ? SHADOWTOPO_ENOMEM : SHADOWTOPO_EDEVICE, "graph build: %s",
@@ -3883,6 +4030,7 @@ void shadowtopo_reset_stats(shadowtopo_engine* eng) {
     eng->st.create_upload_ms = keep.create_upload_ms;
     eng->st.create_build_ms = keep.create_build_ms;
     eng->st.order_ms = keep.order_ms;
+    eng->st.create_alloc_ms = keep.create_alloc_ms;
 }
 
 int shadowtopo_is_complete(const shadowtopo_engine* eng) {

@@ -37,12 +37,13 @@ struct Built {
     int32_t complete = 0;        // _topology_isComplete's count rule (topology.c:450-552)
 };
 
-// d_src/d_dst/d_lat/d_loss: the GraphML edge list already on the device (E entries);
-// n_loops: self-loop edges among them (counted by the caller's validation pass);
-// pad: padding arcs appended to the in-CSR (u = 0, w = +inf)
-hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, const int32_t* d_src,
-                 const int32_t* d_dst, const double* d_lat, const double* d_loss, hipStream_t s, Built& out,
-                 std::vector<void*>& allocs);
+// d_src/d_dst/d_lat/d_loss: the GraphML edge list already on the device (E entries), in
+// buffers the caller has recorded in `allocs`: they become the igraph storage in place
+// (efrom/eto overwrite src/dst, erel overwrites packetloss, elat IS d_lat), so the build
+// allocates and copies nothing for them; n_loops: self-loop edges among them (counted by
+// the caller's validation pass); pad: padding arcs appended to the in-CSR (u = 0, w = +inf)
+hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, int32_t* d_src, int32_t* d_dst,
+                 double* d_lat, double* d_loss, hipStream_t s, Built& out, std::vector<void*>& allocs);
 
 // dense tables [Vp][Vp] of the merged in-CSR: W (latency, +inf where no arc), WI (in-arc
 // index, -1) and W32 (latency rounded toward -inf, NaN where no arc)

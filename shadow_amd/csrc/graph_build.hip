@@ -64,9 +64,11 @@ int bitlen(uint64_t x) {
 
 // igraph storage, 1 - loss, the lowest self-loop, and the relaxation arcs (key v << 32 | u,
 // value eid); a loop's arcs get the sentinel head V, which sorts them past every real arc
-__global__ void k_edges(int64_t E, int32_t V, int directed, const int32_t* __restrict__ src,
-                        const int32_t* __restrict__ dst, const double* __restrict__ loss, int32_t* efrom,
-                        int32_t* eto, double* erel, int32_t* loop_min, uint64_t* akey, int32_t* aval) {
+// in place: efrom / eto / erel may be src / dst / loss themselves (each element is read, then
+// written, by the same thread)
+__global__ void k_edges(int64_t E, int32_t V, int directed, const int32_t* src, const int32_t* dst,
+                        const double* loss, int32_t* efrom, int32_t* eto, double* erel, int32_t* loop_min,
+                        uint64_t* akey, int32_t* aval) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
         const int32_t a = src[e], b = dst[e];
         int32_t f = a, t = b;
@@ -257,21 +259,19 @@ hipError_t exclusive_sum(Scratch& sc, const T* in, T* out, int64_t n, hipStream_
 
 }  // namespace
 
-hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, const int32_t* d_src,
-                 const int32_t* d_dst, const double* d_lat, const double* d_loss, hipStream_t s, Built& g,
-                 std::vector<void*>& allocs) {
+hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, int32_t* d_src, int32_t* d_dst,
+                 double* d_lat, double* d_loss, hipStream_t s, Built& g, std::vector<void*>& allocs) {
     Scratch sc;
     const int dir = directed ? 1 : 0;
     const int64_t NA = directed ? E : 2 * E;           // arcs before dropping loops
     const int64_t NL = NA - (directed ? 1 : 2) * n_loops;  // non-loop arcs
     if (NA >= INT_MAX) return hipErrorInvalidValue;      // hipCUB item counts are int
-    // igraph storage
-    GB_TRY(dalloc(allocs, &g.efrom, E));
-    GB_TRY(dalloc(allocs, &g.eto, E));
-    GB_TRY(dalloc(allocs, &g.elat, E));
-    GB_TRY(dalloc(allocs, &g.erel, E));
+    // igraph storage, in the uploaded buffers themselves
+    g.efrom = d_src;
+    g.eto = d_dst;
+    g.elat = d_lat;
+    g.erel = d_loss;
     GB_TRY(dalloc(allocs, &g.loop_eid, V));
-    if (E) GB_TRY(hipMemcpyAsync(g.elat, d_lat, sizeof(double) * E, hipMemcpyDeviceToDevice, s));
     {
         // loop_eid starts at INT_MAX (atomicMin), then -1 where no loop
         std::vector<int32_t> init((size_t)V, INT_MAX);

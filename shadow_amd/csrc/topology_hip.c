@@ -798,34 +798,25 @@ static uint64_t counter_peek(const Topology* top, int32_t i, int32_t j) {
                 : 0;
 }
 
-/* The emulated path cache's stored set (cache_resolve).  Directed graphs: one bit per
- * ordered pair, bit j % 64 of word i % 64 of tile (i / 64, j / 64).  Undirected graphs: one
- * 2-bit cell per unordered pair {a <= b} -- bit 0: (a, b) is cached, bit 1: (b, a) -- in
- * tile (a / 64, b / 64), word 2 (a % 64) + (b % 64) / 32, so the direction that holds a
- * pair is decided by ONE compare-and-swap: _topology_shouldStorePath's "neither direction
- * cached yet" (topology.c:1309-1318) as an atomic claim, with no lock on the store path. */
-#define STILE_WORDS(top) ((top)->directed ? CTILE : 2 * CTILE)
+/* The emulated path cache's stored set (cache_resolve): one 2-bit cell per unordered pair
+ * {a <= b} -- bit 0: (a, b) is cached, bit 1: (b, a) -- in tile (a / 64, b / 64), word
+ * 2 (a % 64) + (b % 64) / 32, so the direction that holds a pair is decided by ONE
+ * compare-and-swap: _topology_shouldStorePath's "neither direction cached yet"
+ * (topology.c:1309-1318) as an atomic claim, with no lock on the store path.  Directed graphs
+ * too: the reference refuses (s, t) there as well once (t, s) is cached. */
+#define STILE_WORDS(top) (2 * CTILE)
 
 static _Atomic uint64_t* cell_word(const Topology* top, int32_t a, int32_t b, int alloc, int* shift) {
     uint64_t* tile = alloc ? tile_get(top->srow, top->ctd, a / CTILE, b / CTILE, STILE_WORDS(top))
                            : tile_peek(top->srow, top->ctd, a / CTILE, b / CTILE);
     if (!tile) return NULL;
-    if (top->directed) {
-        *shift = b % CTILE;
-        return (_Atomic uint64_t*)&tile[a % CTILE];
-    }
     *shift = 2 * (b % 32);
     return (_Atomic uint64_t*)&tile[2 * (a % CTILE) + (b % CTILE) / 32];
 }
 
-/* which direction of attached pair (i, j) is cached: 1 = (i, j), 2 = (j, i) (undirected
- * graphs only), 0 = neither */
+/* which direction of attached pair (i, j) is cached: 1 = (i, j), 2 = (j, i), 0 = neither */
 static int cached_dir(const Topology* top, int32_t i, int32_t j) {
     int sh;
-    if (top->directed) {
-        _Atomic uint64_t* w = cell_word(top, i, j, 0, &sh);
-        return w && ((atomic_load_explicit(w, memory_order_acquire) >> sh) & 1u) ? 1 : 0;
-    }
     const int32_t a = i < j ? i : j, b = i < j ? j : i;
     _Atomic uint64_t* w = cell_word(top, a, b, 0, &sh);
     const unsigned c = w ? (unsigned)((atomic_load_explicit(w, memory_order_acquire) >> sh) & 3u) : 0u;
@@ -835,16 +826,10 @@ static int cached_dir(const Topology* top, int32_t i, int32_t j) {
     return ((c & 1u) != 0) == (i < j) ? 1 : 2;
 }
 
-/* cache (i, j) unless the pair is cached already in either direction (undirected) or in
- * this direction (directed: the drop-in keeps both directions); 1 when this
- * call stored it */
+/* cache (i, j) unless the pair is cached already in either direction (directed graphs too,
+ * topology.c:1311-1317); 1 when this call stored it */
 static int cache_claim(Topology* top, int32_t i, int32_t j) {
     int sh;
-    if (top->directed) {
-        _Atomic uint64_t* w = cell_word(top, i, j, 1, &sh);
-        if (!w) return 0;
-        return !((atomic_fetch_or_explicit(w, 1ull << sh, memory_order_acq_rel) >> sh) & 1u);
-    }
     const int32_t a = i < j ? i : j, b = i < j ? j : i;
     _Atomic uint64_t* w = cell_word(top, a, b, 1, &sh);
     if (!w) return 0;
@@ -897,15 +882,9 @@ void topology_free(Topology* top) {
                 for (int32_t x = 0; x < STILE_WORDS(top); x++) {
                     for (uint64_t w = tile[x]; w; w &= w - 1) {
                         const int bit = __builtin_ctzll(w);
-                        int32_t i, j;
-                        if (top->directed) {
-                            i = ti * CTILE + x;
-                            j = tj * CTILE + bit;
-                        } else {  /* cell (a, b): bit 0 -> (a, b) cached, bit 1 -> (b, a) */
-                            const int32_t a = ti * CTILE + x / 2, b = tj * CTILE + (x % 2) * 32 + bit / 2;
-                            i = (bit & 1) ? b : a;
-                            j = (bit & 1) ? a : b;
-                        }
+                        /* cell (a, b): bit 0 -> (a, b) cached, bit 1 -> (b, a) */
+                        const int32_t a = ti * CTILE + x / 2, b = tj * CTILE + (x % 2) * 32 + bit / 2;
+                        const int32_t i = (bit & 1) ? b : a, j = (bit & 1) ? a : b;
                         if (i >= m->A || j >= m->A) continue;
                         uint64_t c = counter_peek(top, i, j);
                         int32_t s = top->attached[i], t = top->attached[j];
@@ -1639,7 +1618,9 @@ static void note_min_latency(Topology* top, double mn) {
 /* The reference's path cache over the eager matrix.  Every value is computed up front; what
  * follows the reference's query order is WHICH pairs are cached and in which direction, so
  * a getter returns exactly the entry the reference would (_topology_getPathEntry tries
- * (s, t), then (t, s) in undirected graphs, topology.c:1983-1990), the minimum handed to
+ * (s, t), then (t, s) in undirected graphs, topology.c:1983-1990; after a successful miss
+ * (s, t), then (t, s) in any graph, :2033-2038 -- so in a directed graph whose (t, s) was
+ * cached first, (s, t) misses every time, reruns s's Dijkstra and returns (t, s)), the minimum handed to
  * worker_updateMinTimeJump changes when the reference's would (:1374-1385), the teardown
  * log lists the reference's cached Paths (:1929-1967), and the Dijkstra / self-path counts
  * are the reference's.  A miss (:1992-2045) replays the reference's branch, which the pair's
@@ -1659,6 +1640,7 @@ static void note_min_latency(Topology* top, double mn) {
 static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32_t* si, int32_t* sj) {
     matrix* m = *mp;
     int d = cached_dir(top, i, j);
+    if (top->directed && d == 2) d = 0; /* a directed lookup tries (s, t) only (:1983-1986) */
     if (!d) {
         /* a late attach may have published a larger matrix meanwhile: its target list is the
          * one the reference's Dijkstra would use now */
@@ -1670,15 +1652,20 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
         const uint8_t k = cell_k(&m->kind[(size_t)i * A + j]);
         double mn = 0.0;
         int64_t stored = 0;
+        int success = 1; /* the reference's `success` (:2009-2031) */
         if (k == SHADOWTOPO_KIND_DIRECT || top->complete) {
             /* a complete graph without the edge: get_eid fails, nothing is stored */
-            if (k == SHADOWTOPO_KIND_DIRECT && cache_claim(top, i, j)) {
+            if (k != SHADOWTOPO_KIND_DIRECT)
+                success = 0;
+            else if (cache_claim(top, i, j)) {
                 mn = cell_d(&m->lat[(size_t)i * A + j]);
                 stored = 1;
             }
         } else if (i == j) {
             atomic_fetch_add_explicit(&top->self_count, 1, memory_order_relaxed);
-            if (k != SHADOWTOPO_KIND_NONE && cache_claim(top, i, i)) {
+            if (k == SHADOWTOPO_KIND_NONE)
+                success = 0; /* no incident edge: no self path */
+            else if (cache_claim(top, i, i)) {
                 mn = cell_d(&m->lat[(size_t)i * A + i]);
                 stored = 1;
             }
@@ -1707,7 +1694,8 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
             atomic_fetch_add_explicit(&top->cached_paths, stored, memory_order_relaxed);
             note_min_latency(top, mn);
         }
-        d = cached_dir(top, i, j);
+        if (!success) return -1;
+        d = cached_dir(top, i, j); /* (s, t), else (t, s), directed or not (:2033-2038) */
         if (!d) return -1;
     }
     *si = d == 1 ? i : j;

@@ -80,6 +80,7 @@ class Stats(ctypes.Structure):
         ("pruned_vertices", ctypes.c_int64), ("pool_allocs", ctypes.c_int64), ("pool_alloc_ms", ctypes.c_double),
         ("create_validate_ms", ctypes.c_double), ("create_upload_ms", ctypes.c_double),
         ("create_build_ms", ctypes.c_double), ("order_ms", ctypes.c_double),
+        ("create_alloc_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -211,8 +211,9 @@ def test_tie_break_second_restatement(case):
 def test_path_cache_model_reference_quirks():
     """oracle/path_cache_ref.py restates topology.c's cache literally: in an undirected graph
     the second direction of a pair is served by the first one's Path; in a directed graph
-    _topology_shouldStorePath refuses (s, t) once (t, s) is cached, so the reference's query
-    (s, t) then finds no Path (the drop-in stores it: reverse_blocks_directed=False)"""
+    _topology_shouldStorePath refuses (s, t) once (t, s) is cached (topology.c:1311-1317), so
+    the query (s, t) misses, reruns s's Dijkstra on every call and is answered with the (t, s)
+    Path by the post-computation fallback (topology.c:2033-2038)"""
     import numpy as np
     from oracle.path_cache_ref import RefPathCache
     lat = np.array([[2.0, 5.0, 7.0], [6.0, 2.0, 4.0], [7.5, 4.5, 3.0]])
@@ -227,9 +228,8 @@ def test_path_cache_model_reference_quirks():
     assert und.get_path_entry(0, 0) == (0, 0) and und.self_paths == 0  # cached by source 0's run
     assert und.get_path_entry(2, 2) == (2, 2) and und.self_paths == 1  # a self-path run
     d = RefPathCache(lat, kind, directed=True, complete=False, prefer_direct=False, adjacent=adj)
-    assert d.get_path_entry(1, 0) == (1, 0)
-    assert d.get_path_entry(0, 1) is None  # the reference's quirk
-    d2 = RefPathCache(lat, kind, directed=True, complete=False, prefer_direct=False, adjacent=adj,
-                      reverse_blocks_directed=False)
-    d2.get_path_entry(1, 0)
-    assert d2.get_path_entry(0, 1) == (0, 1)
+    assert d.get_path_entry(1, 0) == (1, 0) and d.dijkstra_runs == 1
+    assert d.get_path_entry(0, 1) == (1, 0) and d.dijkstra_runs == 2  # the reverse Path
+    assert d.get_path_entry(0, 1) == (1, 0) and d.dijkstra_runs == 3  # a miss every time
+    assert d.get_path_entry(0, 2) == (0, 2) and (0, 1) not in d.cache  # stored by run 2
+    assert d.get_path_entry(0, 2) == (0, 2) and d.dijkstra_runs == 3  # a hit

@@ -46,10 +46,10 @@ def attach_all(top, ips, vertices, base=0):
 
 
 def ref_cache(g, lat_o, kind_o, complete=False):
-    # directed graphs: the drop-in stores (s, t) even when (t, s) is cached (the reference
-    # refuses it and then fails the query: DESIGN.md 2)
+    # directed graphs as the reference: (s, t) is refused once (t, s) is cached, and the query
+    # (s, t) is then answered with the (t, s) Path (topology.c:1311-1317, :2033-2038)
     return RefPathCache(lat_o, kind_o, directed=g.directed, complete=complete, prefer_direct=bool(g.prefer_direct),
-                        adjacent=adjacency_of(g), reverse_blocks_directed=False)
+                        adjacent=adjacency_of(g))
 
 
 def check_cache_state(top, model):
@@ -78,30 +78,55 @@ def check_against_oracle(tmp_path, g, n_hosts=None):
     reversed_seen = 0
     for i, a in enumerate(hosts):
         for j, b in enumerate(hosts):
-            si, sj = model.get_path_entry(i, j)
+            # one model lookup per getter call: a directed pair whose reverse holds the cache
+            # misses (and reruns a Dijkstra) on every call, as in the reference
+            path = model.get_path_entry(i, j)
+            if path is None:  # unroutable (a directed graph's unreachable pair)
+                assert g.directed and top.getLatency(a, b) == -1.0, (i, j)
+                assert model.get_path_entry(i, j) is None and not top.isRoutable(a, b), (i, j)
+                continue
+            si, sj = path
             reversed_seen += (si, sj) != (i, j)
             lat = top.getLatency(a, b)
             assert lat == lat_o[si, sj], (i, j, lat, lat_o[si, sj])
-            assert top.getReliability(a, b) == rel_o[si, sj]
-            assert top.isRoutable(a, b)
+            assert model.get_path_entry(i, j) == path and top.getReliability(a, b) == rel_o[si, sj]
+            assert model.get_path_entry(i, j) == path and top.isRoutable(a, b)
     inf = top.info()
     assert inf["computed_for"] == len(hosts)
     check_cache_state(top, model)
-    if not g.directed:
-        assert reversed_seen > 0  # the lower triangle came from the upper one's Paths
-    return top, hosts
+    # the lower triangle came from the upper one's Paths -- in a directed graph too, through
+    # the post-computation fallback (topology.c:2033-2038)
+    assert reversed_seen > 0
+    return top, hosts, model
 
 
 def test_sparse_graph_all_pairs(tmp_path):
     g = synth.random_sparse(V=180, avg_deg=4, seed=41, A=60)
-    top, _ = check_against_oracle(tmp_path, g)
+    top, _, _ = check_against_oracle(tmp_path, g)
+    top.free()
+
+
+def test_directed_graph_all_pairs(tmp_path):
+    """directed: once (t, s) is cached the reference refuses (s, t) (topology.c:1311-1317), so
+    the query (s, t) misses every time, reruns s's Dijkstra and gets the (t, s) Path; the
+    drop-in's getters, cached set and Dijkstra count follow it"""
+    g = synth.random_sparse(V=150, avg_deg=4, seed=47, A=40, directed=True)
+    top, hosts, model = check_against_oracle(tmp_path, g)
+    i, j = next((i, j) for (j, i) in sorted(model.cache) if i != j and (i, j) not in model.cache)
+    a, b = hosts[i], hosts[j]
+    runs = top.info()["dijkstra_runs"]
+    assert top.getLatency(a, b) == top.getLatency(b, a)  # (j, i) holds the pair
+    assert top.info()["dijkstra_runs"] == runs + 1  # (i, j) missed and reran i's Dijkstra
+    top.incrementPathPacketCounter(a, b)  # counted on the (j, i) Path
+    va, vb = top.vertex_of_ip(a.ip), top.vertex_of_ip(b.ip)
+    assert top.packet_count(vb, va) == 1 and top.packet_count(va, vb) == 0
     top.free()
 
 
 def test_prefer_direct_graph(tmp_path):
     g = synth.random_sparse(V=120, avg_deg=6, seed=42, A=50)
     g.prefer_direct = True
-    top, _ = check_against_oracle(tmp_path, g)
+    top, _, _ = check_against_oracle(tmp_path, g)
     assert top.info()["prefers_direct_paths"] == 1
     top.free()
 
@@ -109,13 +134,13 @@ def test_prefer_direct_graph(tmp_path):
 def test_vertex_loss_graph(tmp_path):
     rng = np.random.default_rng(1)
     g = synth.random_sparse(V=120, avg_deg=4, seed=43, A=40, vloss=rng.uniform(0, 0.05, 120))
-    top, _ = check_against_oracle(tmp_path, g)
+    top, _, _ = check_against_oracle(tmp_path, g)
     top.free()
 
 
 def test_packet_counters_one_per_unordered_pair(tmp_path):
     g = synth.random_sparse(V=60, avg_deg=4, seed=44, A=10)
-    top, hosts = check_against_oracle(tmp_path, g)
+    top, hosts, _ = check_against_oracle(tmp_path, g)
     a, b, c = hosts[0], hosts[1], hosts[2]
     for _ in range(3):
         top.incrementPathPacketCounter(a, b)
@@ -185,22 +210,28 @@ def test_late_attach_keeps_counters_and_values(tmp_path, directed):
     hosts = attach_all(top, ips, g.attached[:10])
     vx = [top.vertex_of_ip(h.ip) for h in hosts]
 
+    # every drop-in query is mirrored by one model lookup: in a directed graph a pair whose
+    # reverse holds the cache misses (and reruns a Dijkstra) on every call
     def q(i, j, a, b):
         path = model.get_path_entry(i, j)
         got = top.getLatency(a, b)
         if path is None:  # unroutable (directed graphs)
-            assert got == -1.0 and top.getReliability(a, b) == -1.0, (i, j)
+            assert got == -1.0 and model.get_path_entry(i, j) is None and top.getReliability(a, b) == -1.0, (i, j)
             return got
         si, sj = path
         assert got == lat_o[si, sj], (i, j, si, sj)
-        assert top.getReliability(a, b) == rel_o[si, sj], (i, j)
+        assert model.get_path_entry(i, j) == path and top.getReliability(a, b) == rel_o[si, sj], (i, j)
         return got
+
+    def inc(i, j, a, b):
+        model.get_path_entry(i, j)
+        top.incrementPathPacketCounter(a, b)
 
     model.A = 10
     l01 = q(0, 1, hosts[0], hosts[1])
     for _ in range(3):
-        top.incrementPathPacketCounter(hosts[0], hosts[1])
-    top.incrementPathPacketCounter(hosts[2], hosts[5])
+        inc(0, 1, hosts[0], hosts[1])
+    inc(2, 5, hosts[2], hosts[5])
     q(2, 5, hosts[2], hosts[5])
     assert top.info()["computed_for"] == 10
     more = attach_all(top, ips, g.attached[10:20], base=100)
@@ -210,15 +241,13 @@ def test_late_attach_keeps_counters_and_values(tmp_path, directed):
     assert q(0, 1, hosts[0], hosts[1]) == l01
     q(13, 4, more[3], hosts[4])  # new source, old target
     q(4, 13, hosts[4], more[3])
-    top.incrementPathPacketCounter(hosts[0], hosts[1])
-    top.incrementPathPacketCounter(more[0], hosts[3])
-    model.get_path_entry(10, 3)
+    inc(0, 1, hosts[0], hosts[1])
+    inc(10, 3, more[0], hosts[3])
     assert top.packet_count(vx[0], vx[1]) == 4
     assert top.packet_count(vx[2], vx[5]) == 1
     even_more = attach_all(top, ips, g.attached[20:26], base=200)
     model.A = 26
-    top.incrementPathPacketCounter(even_more[0], hosts[0])
-    model.get_path_entry(20, 0)
+    inc(20, 0, even_more[0], hosts[0])
     assert top.info()["computed_for"] == 26
     assert top.packet_count(vx[0], vx[1]) == 4
     assert top.packet_count(top.vertex_of_ip(more[0].ip), vx[3]) == 1

@@ -413,3 +413,32 @@ def test_ip_table_lookups_through_attach_detach_churn(tmp_path):
     # cap / 4 detaches each: bounded by the live table plus 32 bytes per detach
     assert inf["ip_retired_bytes"] <= 8 * inf["ip_table_slots"] + 32 * detaches + 4096 * inf["ip_tables_retired"]
     top.free()
+
+
+@pytest.mark.parametrize("n_edges", [1000, 3_000_000])  # the sequential and the threaded scan
+def test_engine_edge_validation_reports_the_first_bad_edge(n_edges):
+    """shadowtopo_create checks every edge (topology.c:1070, :1090 and the endpoint range)
+    before it touches a device; past 2^20 edges the scan is split over host threads and
+    must still name the FIRST failing edge in edge order, with that edge's own message."""
+    rng = np.random.default_rng(5)
+    V = 5000
+    src = rng.integers(0, V, n_edges).astype(np.int32)
+    dst = rng.integers(0, V, n_edges).astype(np.int32)
+    lat = rng.uniform(1.0, 50.0, n_edges)
+    loss = rng.uniform(0.0, 0.02, n_edges)
+    cases = [  # (index, field, value, message) -- the later, different fault must not win
+        (int(n_edges * 0.61), "lat", 0.0, "latency must be > 0"),
+        (int(n_edges * 0.37), "loss", 1.5, "packetloss out of [0,1]"),
+        (int(n_edges * 0.12), "dst", V, "endpoint out of range"),
+        (n_edges - 1, "lat", np.inf, "latency must be > 0"),
+    ]
+    arrays = {"src": src, "dst": dst, "lat": lat, "loss": loss}
+    for k in range(len(cases)):
+        first = min(cases[: k + 1])  # faults 0..k present: the lowest index is reported
+        a = {key: v.copy() for key, v in arrays.items()}
+        for idx, field, val, _ in cases[: k + 1]:
+            a[field][idx] = val
+        with pytest.raises(E.ShadowTopoError) as ei:
+            E.Engine(V, a["src"], a["dst"], a["lat"], a["loss"])
+        msg = str(ei.value)
+        assert f"edge {first[0]} " in msg and first[3] in msg, msg
