@@ -738,7 +738,7 @@ constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FT
 // Occupancy: LDS (24 KB per block) allows 6 blocks = 6 waves per SIMD, and 80 VGPRs fit 6
 // (the kernel wants 82, i.e. 5 waves); waves_per_eu(6) spills 3 dwords outside the chunk
 // loop and buys a sixth wave: 3.89 -> 3.68 ms on C2 together with the unrolls below.
-template <int TDT, int XR, int TB, bool PR>
+template <int TDT, int XR, int TB, bool PR, int PH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6 : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
@@ -782,6 +782,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     int32_t vid[TDT];  // this wave's destinations (vertex ids)
 #pragma unroll
     for (int t = 0; t < TDT; ++t) vid[t] = PR ? perm[v0 + t] : v0 + t;
+    // PH: 0 = the whole sweep in one kernel; 1 = the f32 chunk loop alone (the hit log out);
+    // 2 = the exact f64 pass and epilogue alone (the hit log in).  Split, the chunk loop holds
+    // no f64 lexicographic state (40 VGPRs) and the exact pass no staging registers.
     BatchDev B[TB];
     int32_t sv[TB];
     double bc[TB][TDT], bdu[TB][TDT];
@@ -798,7 +801,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
 #pragma unroll
         for (int t = 0; t < TDT; ++t) {
             const int32_t v = vid[t];
-            const double cd = B[k].D[(size_t)v * KL + lane];  // padding rows are +inf
             const double ws = (sv[k] >= 0 && sv[k] != v) ? W[(size_t)sv[k] * Vp + v] : dinf();
             if (ws < dinf()) {
                 bc[k][t] = 0.0 + ws;
@@ -809,16 +811,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
                 bdu[k][t] = dinf();
                 bu[k][t] = -1;
             }
-            // a lane without a source (a partial batch) never passes: NaN, so it cannot hold a
-            // pruned wave's chunk skip back either
-            thr[k][t] = live[k] && sv[k] >= 0 ? f32_thr(cd < bc[k][t] ? cd : bc[k][t]) : __int_as_float(0x7fc00000);
+            if constexpr (PH != 2) {
+                const double cd = B[k].D[(size_t)v * KL + lane];  // padding rows are +inf
+                // a lane without a source (a partial batch) never passes: NaN, so it cannot hold a
+                // pruned wave's chunk skip back either
+                thr[k][t] = live[k] && sv[k] >= 0 ? f32_thr(cd < bc[k][t] ? cd : bc[k][t]) : __int_as_float(0x7fc00000);
+            }
         }
     }
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(1))) const f4 gf4;
     const int32_t nrows = (V + SRS - 1) / SRS * SRS;  // <= Vp: rows past V are NaN padding
     const int32_t nchunks = nrows / SRS;
     const int64_t gw = (int64_t)blockIdx.x * 4 + wave;  // this wave's hit log: [TB][nchunks] row masks
+    if constexpr (PH != 2) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const f4 gf4;
     // chunk fill: TB x D32 rows = SRS*64 floats each (2 float4 per thread), W32 = SRS*BW floats
     constexpr int DQ = SRS * KL / 4 / 256;       // float4 of one batch's D32 chunk per thread
     constexpr int WQT = (SRS * WQ + 255) / 256;  // float4 of W32 per thread
@@ -1019,17 +1025,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         uint32_t hits[TB];
 #pragma unroll
         for (int k = 0; k < TB; ++k) hits[k] = 0;
+        // PH 1 (the chunk loop alone has VGPRs to spare): each row's LDS reads are issued one
+        // row ahead, so they are in flight while the previous row is filtered and votes
+#ifdef SHADOWTOPO_EXP_NO_ROW_AHEAD
+        constexpr bool RP = false;  // A/B build
+#else
+        constexpr bool RP = PH == 1;
+#endif
+        f4 wn[TDT / 4];
+        float dn[TB];
+        auto lds_row = [&](int r) {
+            const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
+#pragma unroll
+            for (int j = 0; j < TDT / 4; ++j) wn[j] = wr[j];
+#pragma unroll
+            for (int k = 0; k < TB; ++k) dn[k] = sD[cur][k][r * KL + lane];
+        };
+        if (RP && run) lds_row(0);
 #pragma unroll 8  // rows per unrolled step (2: +3 %, 1: +6 %)
         for (int r = 0; r < (run ? SRS : 0); ++r) {
-            const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
             f4 w4[TDT / 4];
+            float dk[TB];
+            if constexpr (RP) {
 #pragma unroll
-            for (int j = 0; j < TDT / 4; ++j) {
-                w4[j] = wr[j];
+                for (int j = 0; j < TDT / 4; ++j) w4[j] = wn[j];
+#pragma unroll
+                for (int k = 0; k < TB; ++k) dk[k] = dn[k];
+                if (r + 1 < SRS) lds_row(r + 1);
+            } else {
+                const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
+#pragma unroll
+                for (int j = 0; j < TDT / 4; ++j) w4[j] = wr[j];
+#pragma unroll
+                for (int k = 0; k < TB; ++k) dk[k] = sD[cur][k][r * KL + lane];
             }
 #pragma unroll
             for (int k = 0; k < TB; ++k) {
-                const float du = sD[cur][k][r * KL + lane];
+                const float du = dk[k];
                 // slacks thr_t - w_t two at a time (v_pk_add_f32), their max as a chain of
                 // 3-input maxima (v_max3)
                 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -1087,6 +1119,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     PHASE_STAMP(2);
     PHASE_SET(5, nvisit);
     PHASE_SET(6, nhit);
+    }  // PH != 2
+    if constexpr (PH == 1) return;
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
     // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
     // j % TDT, broadcast by readlane).  A source's own row never passes (its D32 is NaN: the
@@ -2319,6 +2353,7 @@ struct shadowtopo_engine {
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
+    int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
@@ -2557,6 +2592,17 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
         }
         hipLaunchKernelGGL(k_min_d32, dim3((uint32_t)((nchunks + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
                            eng->d_perm, (int32_t)nchunks, eng->d_minD);
+        if (TB == 1 && eng->opt_sweep_split) {  // the chunk loop, then the exact pass + epilogue
+            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
+                               eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
+                               par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
+                               eng->d_minD);
+            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 2>), dim3((uint32_t)nblocks), dim3(256), 0, s,
+                               eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
+                               par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
+                               eng->d_minD);
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                            eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
@@ -3754,6 +3800,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (dl && dl[0] >= '0' && dl[0] <= '2') eng->opt_delta_live = dl[0] - '0';
         const char* dd = getenv("SHADOWTOPO_DELTA_LIVE_DIV");
         if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
+        const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
+        if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
     }
