@@ -15,7 +15,11 @@ Which dispatches: those of the kernels matching KERNEL_RE, in dispatch order, th
 earlier) -- summed and divided by their count: bytes per launch averaged over the step's
 launches, the unit of bench.py's roofline.
 
-usage: roofline_counters.py KEY KERNEL_RE BENCH_JSON FETCH_DIR WRITE_DIR SQ_DIR
+A launch may be several dispatches (PER_LAUNCH: the pruned dense sweep runs as two kernels,
+its chunk loop and its exact pass, both matched by KERNEL_RE): then the last n x PER_LAUNCH
+dispatches are summed and divided by n.
+
+usage: roofline_counters.py KEY KERNEL_RE BENCH_JSON FETCH_DIR WRITE_DIR SQ_DIR [PER_LAUNCH]
 """
 import csv
 import glob
@@ -46,28 +50,30 @@ def dispatches(d, kre):
 
 def main():
     key, kre, bench_json, fdir, wdir, sdir = sys.argv[1:7]
+    per = int(sys.argv[7]) if len(sys.argv) > 7 else 1
     bench = json.loads(open(bench_json).read().strip().splitlines()[-1])
     rf = bench["roofline"]
     n = int(round((bench["warmup"] + bench["steps"]) * rf["launches_per_step"]))
     # label-correcting rounds read values that other waves of the same round may already have
     # updated, so a step can converge a round earlier or later from one run to the next: each
     # pass averages over its own last dispatches (at most n; up to a tenth fewer is accepted)
-    f, w, s = (dispatches(d, kre)[-n:] for d in (fdir, wdir, sdir))
-    if min(len(f), len(w), len(s)) < max(1, n - max(2, n // 10)):
-        raise SystemExit(f"expected {n} dispatches matching {kre}, found {len(f)}/{len(w)}/{len(s)}")
-    fetch = sum(v["FETCH_SIZE"] for v in f) * 1024 * 2 / len(f)
-    write = sum(v["WRITE_SIZE"] for v in w) * 1024 / len(w)
-    valu = sum(v["SQ_INSTS_VALU"] * (v["_grid"] / 64.0) / v["SQ_WAVES"] for v in s if v.get("SQ_WAVES")) / len(s)
+    f, w, s = (dispatches(d, kre)[-n * per:] for d in (fdir, wdir, sdir))
+    if min(len(f), len(w), len(s)) < per * max(1, n - max(2, n // 10)):
+        raise SystemExit(f"expected {n * per} dispatches matching {kre}, found {len(f)}/{len(w)}/{len(s)}")
+    lf, lw, ls = (len(x) / per for x in (f, w, s))  # launches covered by each pass
+    fetch = sum(v["FETCH_SIZE"] for v in f) * 1024 * 2 / lf
+    write = sum(v["WRITE_SIZE"] for v in w) * 1024 / lw
+    valu = sum(v["SQ_INSTS_VALU"] * (v["_grid"] / 64.0) / v["SQ_WAVES"] for v in s if v.get("SQ_WAVES")) / ls
     ns = sum(v["_ns"] for v in s)
     clk = sum(v["GRBM_GUI_ACTIVE"] for v in s) / 8.0 / ns if ns else None  # GHz
     rec = {"kernel": rf["kernel"], "batches_per_launch": rf["batches_per_launch"],
            "hbm_bytes_per_launch": fetch + write, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "valu_insts_per_launch": valu, "effective_clock_ghz_profiled": clk,
-           "dispatches": n, "dispatches_per_pass": [len(f), len(w), len(s)],
-           "profiled_avg_launch_ms": sum(v["_ns"] for v in f) / len(f) / 1e6,
+           "dispatches": n * per, "dispatches_per_launch": per, "dispatches_per_pass": [len(f), len(w), len(s)],
+           "profiled_avg_launch_ms": sum(v["_ns"] for v in f) / lf / 1e6,
            "source": f"rocprofv3 --pmc passes over the bench command of {os.path.basename(bench_json)}: "
                      f"FETCH_SIZE x1024 x2, WRITE_SIZE x1024, SQ_INSTS_VALU x (Grid_Size/64)/SQ_WAVES; the last "
-                     f"{n} dispatches of kernels matching '{kre}'"}
+                     f"{n * per} dispatches of kernels matching '{kre}' ({per} per launch)"}
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "roofline_counters.json")
     db = json.load(open(p)) if os.path.exists(p) else {}
     db[key] = rec

@@ -738,8 +738,8 @@ constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FT
 // Occupancy: LDS (24 KB per block) allows 6 blocks = 6 waves per SIMD, and 80 VGPRs fit 6
 // (the kernel wants 82, i.e. 5 waves); waves_per_eu(6) spills 3 dwords outside the chunk
 // loop and buys a sixth wave: 3.89 -> 3.68 ms on C2 together with the unrolls below.
-template <int TDT, int XR, int TB, bool PR, int PH = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6 : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
+template <int TDT, int XR, int TB, bool PR, int PH = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1 ? (NW == 8 ? 8 : 6) : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
                                                        int32_t nb, int32_t ntb, int32_t parity, int32_t thresh,
@@ -758,7 +758,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     // D32(u) >= min D32, so the skip is exact; minD is taken before the sweep, which is the
     // same as having read those rows' pre-sweep values (later changes reach the delta round
     // through the change masks).
-    constexpr int BW = 4 * TDT;  // block columns
+    // NW waves per block: 4.  (8 for the split chunk loop -- one staged D32 chunk for 8 waves,
+    // 8 waves per SIMD -- measured 3.57 vs 3.42-3.43 ms on C2, r03s: a block-wide chunk skip
+    // then needs all 8 waves dead, so more chunks are staged.)
+    static_assert(NW == 4 || (NW == 8 && PH == 1), "8-wave blocks only for the chunk loop");
+    constexpr int NT = 64 * NW;  // threads per block
+    constexpr int BW = NW * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
     __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
@@ -821,18 +826,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
     }
     const int32_t nrows = (V + SRS - 1) / SRS * SRS;  // <= Vp: rows past V are NaN padding
     const int32_t nchunks = nrows / SRS;
-    const int64_t gw = (int64_t)blockIdx.x * 4 + wave;  // this wave's hit log: [TB][nchunks] row masks
+    // this wave's hit log [TB][nchunks] of row masks, indexed by (batch group, wave tile) so the
+    // exact-pass kernel finds it whatever block shape wrote it
+    const int64_t gw = (int64_t)grp * (Vp / TDT) + v0 / TDT;
     if constexpr (PH != 2) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const f4 gf4;
     // chunk fill: TB x D32 rows = SRS*64 floats each (2 float4 per thread), W32 = SRS*BW floats
-    constexpr int DQ = SRS * KL / 4 / 256;       // float4 of one batch's D32 chunk per thread
-    constexpr int WQT = (SRS * WQ + 255) / 256;  // float4 of W32 per thread
+    constexpr int DQ = SRS * KL / 4 / NT;       // float4 of one batch's D32 chunk per thread
+    constexpr int WQT = (SRS * WQ + NT - 1) / NT;  // float4 of W32 per thread
+    static_assert(DQ * NT * 4 == SRS * KL, "the D32 chunk is whole float4s per thread");
     f4 pd[TB][DQ], pw[WQT];
     // PR: the chunk's skip bounds (md: min D32 per lane and batch, mw: min W32 of the
     // wave's tile columns)
     float mdn[TB], mdc[TB], mwn[TDT], mwc[TDT];
-    const int32_t ncol = (V + BW - 1) / BW * BW;  // columns per chunk row of minW
+    const int32_t ncol = Vp;  // columns per chunk row of minW
     // PR: chunks in the order vt, vt+1, .., wrapping: the block's own tile (its destinations'
     // nearest rows) first, which gives unreached and arc-less (t, s) pairs a tight threshold
     // before the far chunks are tested
@@ -845,7 +853,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         if (PR) {
             const int32_t u0 = chunk_of(j) * SRS;
 #pragma unroll
-            for (int i = 0; i < DQ; ++i) prow[i] = perm[u0 + (threadIdx.x + i * 256) / (KL / 4)];
+            for (int i = 0; i < DQ; ++i) prow[i] = perm[u0 + (threadIdx.x + i * NT) / (KL / 4)];
         }
     };
     // fetch the chunk of order index j into registers (rows in the locality order: prow
@@ -857,7 +865,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         for (int k = 0; k < TB; ++k)
 #pragma unroll
             for (int i = 0; i < DQ; ++i) {
-                const int e = threadIdx.x + i * 256;  // float4 index within the chunk
+                const int e = threadIdx.x + i * NT;  // float4 index within the chunk
                 if (PR)
                     pd[k][i] = *(gf4*)(B[k].D32 + (size_t)prow[i] * KL + (size_t)(e % (KL / 4)) * 4);
                 else
@@ -872,7 +880,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
         }
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
-            const int e = threadIdx.x + i * 256;
+            const int e = threadIdx.x + i * NT;
             if (e < SRS * WQ) {
                 const int r = e / WQ, c = e % WQ;
                 pw[i] = *(gf4*)((const gfloat*)W32 + (size_t)(u0 + r) * Vp + vb + c * 4);
@@ -883,10 +891,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
 #pragma unroll
         for (int k = 0; k < TB; ++k)
 #pragma unroll
-            for (int i = 0; i < DQ; ++i) *(f4*)&sD[buf][k][(threadIdx.x + i * 256) * 4] = pd[k][i];
+            for (int i = 0; i < DQ; ++i) *(f4*)&sD[buf][k][(threadIdx.x + i * NT) * 4] = pd[k][i];
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
-            const int e = threadIdx.x + i * 256;
+            const int e = threadIdx.x + i * NT;
             if (e < SRS * WQ) *(f4*)&sW[buf][e * 4] = pw[i];
         }
     };
@@ -1030,7 +1038,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB == 1 ? 6
 #ifdef SHADOWTOPO_EXP_NO_ROW_AHEAD
         constexpr bool RP = false;  // A/B build
 #else
-        constexpr bool RP = PH == 1;
+        constexpr bool RP = PH == 1 && NW == 4;
 #endif
         f4 wn[TDT / 4];
         float dn[TB];
@@ -2569,9 +2577,10 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
     constexpr int TDT = FTDT, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
-        const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
+    const int64_t nblocks = 8 * (((int64_t)ngroups * ntb + 7) / 8);
     const size_t nchunks = (size_t)((eng->V + SRS - 1) / SRS);
-    const size_t need = (size_t)nblocks * 4 * TB * nchunks;
+    // hit log: per (batch group, wave tile of TDT destinations), TB x nchunks row masks
+    const size_t need = (size_t)ngroups * (size_t)(eng->Vp / TDT) * TB * nchunks;
     if (eng->hitlog_n < need) {
         if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
         eng->d_hitlog = nullptr;
@@ -3128,7 +3137,7 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     for (int32_t i = V; i < Vp; ++i) perm.push_back(i);
     constexpr int TDT = FTDT;  // launch_dense_ft's wave tile
     const int32_t nchunks = (V + SRS - 1) / SRS;
-    const int32_t nwt = (V + 4 * TDT - 1) / (4 * TDT) * 4 * TDT;  // columns
+    const int32_t nwt = Vp;  // columns (every block shape's tiles stay inside Vp)
     HIP_TRY(hipMalloc((void**)&eng->d_perm, sizeof(int32_t) * (size_t)Vp));
     HIP_TRY(hipMalloc((void**)&eng->d_W32p, sizeof(float) * (size_t)Vp * Vp));
     HIP_TRY(hipMalloc((void**)&eng->d_minW, sizeof(float) * (size_t)nchunks * nwt));
