@@ -39,6 +39,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "graph_build.h"
@@ -749,9 +750,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        uint32_t* __restrict__ hitlog,
                                                        const int32_t* __restrict__ perm,
                                                        const float* __restrict__ minW,
-                                                       const float* __restrict__ minD) {
-    // PR (pruned): rows, columns and W32 are in the locality order `perm` (W32 here is the
-    // permuted copy W32p[i][j] = W32[perm i][perm j]); a wave skips a chunk outright when no
+                                                       const float* __restrict__ minD,
+                                                       const int32_t* __restrict__ ipos) {
+    // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
+    // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
+    // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
+    // segment, not 8 scattered lines, and so is a logged row's W(u, v_0..v_7).  A wave skips a chunk outright when no
     // lane can pass any of its rows: min D32 over the chunk's rows (minD, per lane) exceeds
     // max_t fl32(thr_t - minW_t), minW_t = min W32 over the chunk's rows in column v_t.  Every
     // row's filter bound max_t fl32(thr_t - W32(u, v_t)) is <= that (rounding is monotone), and
@@ -803,10 +807,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         B[k] = batch_view(pools, live[k] ? b0 + k : first);
         sv[k] = B[k].srcv[lane];
         tie[k] = 0;
+        const size_t wrow = (size_t)(PR ? (sv[k] >= 0 ? ipos[sv[k]] : 0) : sv[k]) * Vp;  // the source's W row
 #pragma unroll
         for (int t = 0; t < TDT; ++t) {
             const int32_t v = vid[t];
-            const double ws = (sv[k] >= 0 && sv[k] != v) ? W[(size_t)sv[k] * Vp + v] : dinf();
+            const double ws = (sv[k] >= 0 && sv[k] != v) ? W[wrow + (PR ? v0 + t : v)] : dinf();
             if (ws < dinf()) {
                 bc[k][t] = 0.0 + ws;
                 bdu[k][t] = 0.0;
@@ -1138,7 +1143,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         if (!live[k]) continue;
         const uint32_t* hl = hitlog + ((size_t)gw * TB + k) * nchunks;
         const gdouble* Dl = B[k].D + lane;
-        const int32_t vl = PR ? perm[v0 + (lane & (TDT - 1))] : v0 + (lane & (TDT - 1));
+        const int32_t vl = v0 + (lane & (TDT - 1));  // PR: a position (W is permuted), else the vertex
         for (int32_t c0 = 0; c0 < nchunks; c0 += 64) {
             const uint32_t e = (c0 + lane < nchunks) ? hl[c0 + lane] : 0u;
             unsigned long long cm = __ballot(e != 0u);
@@ -1149,23 +1154,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                 const int32_t u0 = (c0 + ci) * SRS;
                 if (prof && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hrows));
                 while (hrows) {
-                    int32_t ur[XR];
+                    int32_t ur[XR], rp[XR];
                     int nr = 0;
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
-                        ur[x] = u0;
+                        rp[x] = u0;
                         if (hrows) {
-                            ur[x] = u0 + __builtin_ctzll(hrows);
+                            rp[x] = u0 + __builtin_ctzll(hrows);
                             hrows &= hrows - 1;
                             nr = x + 1;
                         }
-                        if (PR) ur[x] = perm[ur[x]];  // row index -> vertex
+                        ur[x] = PR ? perm[rp[x]] : rp[x];  // row position -> vertex
                     }
                     double d64[XR], wl[XR];
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
                         d64[x] = Dl[(size_t)ur[x] * KL];
-                        wl[x] = W[(size_t)ur[x] * Vp + vl];
+                        wl[x] = W[(size_t)rp[x] * Vp + vl];
                     }
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
@@ -1204,11 +1209,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
 
 // Pruned full sweep (k_relax_dense_f<.., PR = true>) inputs.
 // W32p[i][j] = W32[perm i][perm j]: the f32 weights in the vertex locality order, one row per block
-__global__ __launch_bounds__(256) void k_permute_w32(const float* __restrict__ W32, const int32_t* __restrict__ perm,
-                                                     int32_t Vp, float* __restrict__ W32p) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_permute_w(const T* __restrict__ W, const int32_t* __restrict__ perm,
+                                                   int32_t Vp, T* __restrict__ Wp) {
     const size_t i = blockIdx.x;
-    const gfloat* src = (const gfloat*)W32 + (size_t)perm[i] * Vp;
-    for (int32_t j = threadIdx.x; j < Vp; j += 256) W32p[i * Vp + j] = src[perm[j]];
+    const __attribute__((address_space(1))) T* src = (const __attribute__((address_space(1))) T*)W + (size_t)perm[i] * Vp;
+    for (int32_t j = threadIdx.x; j < Vp; j += 256) Wp[i * Vp + j] = src[perm[j]];
 }
 
 // minW[c][w] = min of W32p over rows [c*SRS, c*SRS+SRS) x columns [w*tdt, w*tdt+tdt), NaN (no
@@ -2272,6 +2278,8 @@ struct shadowtopo_engine {
     // pruned full sweep (OPT_DENSE_PRUNE): vertex locality order and its chunk bounds
     int32_t* d_perm = nullptr;  // [Vp] row/column order (padding maps to itself)
     float* d_W32p = nullptr;    // [Vp][Vp] W32 in that order
+    double* d_Wp = nullptr;     // [Vp][Vp] W in that order
+    int32_t* d_pos = nullptr;   // [Vp] position of each vertex in that order (perm's inverse)
     float* d_minW = nullptr;    // [nchunks][columns] min W32p over each chunk's rows
     float* d_minD = nullptr;    // [nb_cap][nchunks][64] min D32 per chunk and lane
     float* d_minW64 = nullptr;  // [nvc][nvc] min W32p over each 64 x 64 block (pruned delta rounds)
@@ -2603,24 +2611,25 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                            eng->d_perm, (int32_t)nchunks, eng->d_minD);
         if (TB == 1 && eng->opt_sweep_split) {  // the chunk loop, then the exact pass + epilogue
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
-                               eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
+                               eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD);
+                               eng->d_minD, eng->d_pos);
+            // (4 logged rows in flight per wave instead of 2 measured the same, r03u)
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 2>), dim3((uint32_t)nblocks), dim3(256), 0, s,
-                               eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
+                               eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD);
+                               eng->d_minD, eng->d_pos);
             return hipGetLastError();
         }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
-                           eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
+                           eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                           eng->d_minD);
+                           eng->d_minD, eng->d_pos);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, false>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32,
                        eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr);
+                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -3142,7 +3151,16 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     HIP_TRY(hipMalloc((void**)&eng->d_W32p, sizeof(float) * (size_t)Vp * Vp));
     HIP_TRY(hipMalloc((void**)&eng->d_minW, sizeof(float) * (size_t)nchunks * nwt));
     HIP_TRY(hipMemcpyAsync(eng->d_perm, perm.data(), sizeof(int32_t) * (size_t)Vp, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_permute_w32, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_W32, eng->d_perm, Vp, eng->d_W32p);
+    hipLaunchKernelGGL(k_permute_w<float>, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_W32, eng->d_perm, Vp,
+                       eng->d_W32p);
+    // the f64 weights in the same order, and the order's inverse (the sweep's seed and exact
+    // row reads: one segment per lane and row instead of a line per weight)
+    std::vector<int32_t> ipos((size_t)Vp);
+    for (int32_t i = 0; i < Vp; ++i) ipos[(size_t)perm[i]] = i;
+    HIP_TRY(hipMalloc((void**)&eng->d_Wp, sizeof(double) * (size_t)Vp * Vp));
+    HIP_TRY(hipMalloc((void**)&eng->d_pos, sizeof(int32_t) * (size_t)Vp));
+    HIP_TRY(hipMemcpyAsync(eng->d_pos, ipos.data(), sizeof(int32_t) * (size_t)Vp, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_permute_w<double>, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_W, eng->d_perm, Vp, eng->d_Wp);
     hipLaunchKernelGGL(k_min_w32, dim3((uint32_t)(((int64_t)nchunks * nwt + 255) / 256)), dim3(256), 0, s,
                        eng->d_W32p, Vp, nchunks, nwt, 1, eng->d_minW);
     const int32_t nvc = Vp / KL;
@@ -3845,6 +3863,8 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
     if (eng->d_perm) (void)hipFree(eng->d_perm);
     if (eng->d_W32p) (void)hipFree(eng->d_W32p);
+    if (eng->d_Wp) (void)hipFree(eng->d_Wp);
+    if (eng->d_pos) (void)hipFree(eng->d_pos);
     if (eng->d_minW) (void)hipFree(eng->d_minW);
     if (eng->d_minD) (void)hipFree(eng->d_minD);
     if (eng->d_minW64) (void)hipFree(eng->d_minW64);
