@@ -613,13 +613,25 @@ __device__ __forceinline__ void relax_u(double du, double w, int32_t u, double& 
 // its lex key d(pred) (BDU, read by the delta rounds), and the per-vertex change mask of
 // the round (lane = source) that the next delta round walks; the batch counter gets the
 // number of changed (vertex, source) pairs.
+// Seed (pruned sweep, optional): the lane's rows of the permuted arc-index and reliability
+// tables, WIp / WRp + srow, and R(s) = 1 - loss_v(s) of its source: when the seed candidate
+// won (the predecessor is the source itself, whose record is H 0, R vfac(s): k_seed), the
+// new record comes from one segment of those rows instead of the scattered WI / H / R
+// gathers of finish_vertex.
+struct SeedRows {
+    const int32_t* WIp = nullptr;
+    const double* WRp = nullptr;
+    size_t srow = 0;
+    double rs = 0.0;
+};
+
 template <int TDT = DT>
 __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int32_t sv, int32_t v0, int32_t V,
                                                const double* bc, const double* bdu, const int32_t* bu, uint32_t tie,
                                                const int32_t* __restrict__ WI, int32_t Vp,
                                                const double* __restrict__ in_r, int32_t parity,
                                                int32_t* __restrict__ cnt, int32_t b,
-                                               const int32_t* vids = nullptr) {
+                                               const int32_t* vids = nullptr, const SeedRows& sr = SeedRows{}) {
     unsigned long long* chn = B.chm(parity);
     int32_t nch = 0;
 #pragma unroll
@@ -629,9 +641,25 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
         bool ch = false;
         if (bu[t] >= 0 && sv >= 0 && sv != v) {
             const size_t idx = (size_t)v * KL + lane;
-            const int32_t arc = WI[(size_t)bu[t] * Vp + v];
-            ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx], B.H[idx],
-                               B.R[idx], B.P[idx]);
+            if (sr.WIp && bu[t] == sv) {
+                // finish_vertex with hu = 0, ru = vfac(s): h = 1 (+ a local tie), r = vfac(s) * in_r[arc]
+                // (WRp holds in_r of the same arc, the same double)
+                const int32_t arc = sr.WIp[sr.srow + v0 + t];
+                const double r = sr.rs * sr.WRp[sr.srow + v0 + t];
+                const uint32_t h = 1u | ((((tie >> t) & 1u) || bdu[t] == bc[t]) ? (TAINT | LTIE) : 0u);
+                if (bc[t] != B.D[idx] || h != B.H[idx] || r != B.R[idx] || arc != B.P[idx]) {
+                    B.D[idx] = bc[t];
+                    if (B.D32) B.D32[idx] = f32_key(bc[t]);
+                    B.H[idx] = h;
+                    B.R[idx] = r;
+                    B.P[idx] = arc;
+                    ch = true;
+                }
+            } else {
+                const int32_t arc = WI[(size_t)bu[t] * Vp + v];
+                ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx],
+                                   B.H[idx], B.R[idx], B.P[idx]);
+            }
             B.BDU[idx] = bdu[t];
         }
         const unsigned long long m = __ballot(ch);
@@ -751,7 +779,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        const int32_t* __restrict__ perm,
                                                        const float* __restrict__ minW,
                                                        const float* __restrict__ minD,
-                                                       const int32_t* __restrict__ ipos) {
+                                                       const int32_t* __restrict__ ipos,
+                                                       const int32_t* __restrict__ WIp,
+                                                       const double* __restrict__ WRp,
+                                                       const double* __restrict__ vfac) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -1194,8 +1225,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
 #pragma unroll
         for (int k = 0; k < TB; ++k)
             if (live[k])
+            {
+                SeedRows sr;
+                if (PR && WIp && sv[k] >= 0) {
+                    sr.WIp = WIp;
+                    sr.WRp = WRp;
+                    sr.srow = (size_t)ipos[sv[k]] * Vp;
+                    sr.rs = vfac[sv[k]];
+                }
                 dense_epilogue<TDT>(B[k], lane, sv[k], v0, V, bc[k], bdu[k], bu[k], tie[k], WI, Vp, in_r, parity,
-                                    cnt, b0 + k, vid);
+                                    cnt, b0 + k, vid, sr);
+            }
     }
     PHASE_STAMP(4);
 #ifdef SHADOWTOPO_PHASE_STAMPS
@@ -2279,6 +2319,8 @@ struct shadowtopo_engine {
     int32_t* d_perm = nullptr;  // [Vp] row/column order (padding maps to itself)
     float* d_W32p = nullptr;    // [Vp][Vp] W32 in that order
     double* d_Wp = nullptr;     // [Vp][Vp] W in that order
+    int32_t* d_WIp = nullptr;   // [Vp][Vp] WI in that order
+    double* d_WRp = nullptr;    // [Vp][Vp] WR in that order
     int32_t* d_pos = nullptr;   // [Vp] position of each vertex in that order (perm's inverse)
     float* d_minW = nullptr;    // [nchunks][columns] min W32p over each chunk's rows
     float* d_minD = nullptr;    // [nb_cap][nchunks][64] min D32 per chunk and lane
@@ -2613,23 +2655,23 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD, eng->d_pos);
+                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac);
             // (4 logged rows in flight per wave instead of 2 measured the same, r03u)
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 2>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD, eng->d_pos);
+                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac);
             return hipGetLastError();
         }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                           eng->d_minD, eng->d_pos);
+                           eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, false>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32,
                        eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr);
+                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -3161,6 +3203,14 @@ int ensure_vperm(shadowtopo_engine* eng, hipStream_t s) {
     HIP_TRY(hipMalloc((void**)&eng->d_pos, sizeof(int32_t) * (size_t)Vp));
     HIP_TRY(hipMemcpyAsync(eng->d_pos, ipos.data(), sizeof(int32_t) * (size_t)Vp, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_permute_w<double>, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_W, eng->d_perm, Vp, eng->d_Wp);
+    if (eng->d_WI && eng->d_WR) {  // the seed winners' arcs and reliability factors (dense_epilogue)
+        HIP_TRY(hipMalloc((void**)&eng->d_WIp, sizeof(int32_t) * (size_t)Vp * Vp));
+        HIP_TRY(hipMalloc((void**)&eng->d_WRp, sizeof(double) * (size_t)Vp * Vp));
+        hipLaunchKernelGGL(k_permute_w<int32_t>, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_WI, eng->d_perm, Vp,
+                           eng->d_WIp);
+        hipLaunchKernelGGL(k_permute_w<double>, dim3((uint32_t)Vp), dim3(256), 0, s, eng->d_WR, eng->d_perm, Vp,
+                           eng->d_WRp);
+    }
     hipLaunchKernelGGL(k_min_w32, dim3((uint32_t)(((int64_t)nchunks * nwt + 255) / 256)), dim3(256), 0, s,
                        eng->d_W32p, Vp, nchunks, nwt, 1, eng->d_minW);
     const int32_t nvc = Vp / KL;
@@ -3864,6 +3914,8 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_perm) (void)hipFree(eng->d_perm);
     if (eng->d_W32p) (void)hipFree(eng->d_W32p);
     if (eng->d_Wp) (void)hipFree(eng->d_Wp);
+    if (eng->d_WIp) (void)hipFree(eng->d_WIp);
+    if (eng->d_WRp) (void)hipFree(eng->d_WRp);
     if (eng->d_pos) (void)hipFree(eng->d_pos);
     if (eng->d_minW) (void)hipFree(eng->d_minW);
     if (eng->d_minD) (void)hipFree(eng->d_minD);
