@@ -392,6 +392,8 @@ def main():
     ap.add_argument("--no-shim", action="store_true",
                     help="skip the drop-in's in-process multi-GPU host-matrix build (C4 through topology_new)")
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
+    ap.add_argument("--delta-step", type=int, default=0,
+                    help="sparse: delta-stepping rounds, bucket width in 1/1000 latency units (0 = off, default)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
@@ -451,6 +453,8 @@ def main():
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
+    if args.delta_step:
+        eng.set_option(E.OPT_DELTA_STEP, args.delta_step)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0

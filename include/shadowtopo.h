@@ -110,6 +110,12 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               counts read back once per 8 rounds) when batches x vertices <= 4 Mi,
                                               2 = always, 0 = never (one host read-back per round). Results are
                                               identical. */
+#define SHADOWTOPO_OPT_DELTA_STEP 18      /* CSR FULL rounds over worklists: 0 (default) = ungated label-correcting rounds;
+                                            D > 0 = batched delta-stepping: a visit's changes are propagated only
+                                            when one of them is <= its batch's threshold T (the rest wait as
+                                            pending vertices), and T rises by D / 1000 latency units (at least to
+                                            the smallest pending value) whenever a batch has nothing active --
+                                            the north star's bucketed relaxation, measured slower */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (55 % of free HBM, at least 24 GB) this
                                               engine may take (default 1000); engines sharing one device split it */
 
@@ -168,6 +174,8 @@ typedef struct shadowtopo_stats {
     double create_build_ms;
     double order_ms;
     double create_alloc_ms;  /* of create_upload_ms: the device allocation of the edge buffers */
+    int64_t gated_final_releases; /* OPT_DELTA_STEP: groups whose closing release at an infinite
+                                     threshold still found pending work */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

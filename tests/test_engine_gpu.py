@@ -32,6 +32,17 @@ def test_more_than_one_batch_group():
     compare(g, batches_in_flight=2)
 
 
+@pytest.mark.parametrize("delta", [500, 5000, 50000])
+def test_delta_stepping_rounds_same_results(delta):
+    """OPT_DELTA_STEP (the north star's bucketed relaxation: propagation gated by a per-batch
+    threshold, pending vertices released as it rises) reaches the same fixed point; several
+    batch groups, ties (integer latencies: the replay path), device-driven rounds off"""
+    g = synth.random_sparse(V=500, avg_deg=4, seed=21)
+    compare(g, delta_step=delta, device_rounds=0, batches_in_flight=3)
+    gi = synth.random_sparse(V=300, avg_deg=5, seed=22, int_lat=True)
+    compare(gi, delta_step=delta, device_rounds=0)
+
+
 def test_directed():
     g = synth.random_sparse(V=300, avg_deg=4, seed=5, directed=True)
     compare(g)
