@@ -176,10 +176,24 @@ typedef struct shadowtopo_stats {
     double create_alloc_ms;  /* of create_upload_ms: the device allocation of the edge buffers */
     int64_t gated_final_releases; /* OPT_DELTA_STEP: groups whose closing release at an infinite
                                      threshold still found pending work */
+    double prepare_ms;       /* cold start: the device preparation's own wall time (shadowtopo_prepare:
+                                HIP runtime and queue initialisation, staging buffers, code objects) */
+    double create_prepare_wait_ms; /* of create_validate_ms: the part shadowtopo_create waited for it */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */
 int shadowtopo_device_count(void);
+
+/*
+ * Start preparing HIP device `device` on a background thread and return at once: the HIP
+ * runtime's device and queue initialisation (~85 ms on MI355X, once per process), the
+ * page-locked staging buffers of the edge upload, the engine's first stream and the loading
+ * of this library's code objects.  shadowtopo_create starts it itself if nobody did and waits
+ * for it after validating the edge list; a caller that knows a graph is coming (the shim,
+ * before it parses the GraphML file) calls it first so the work overlaps the parse.
+ * Idempotent per device.  Returns SHADOWTOPO_OK, or SHADOWTOPO_EINVAL for a bad ordinal.
+ */
+int shadowtopo_prepare(int32_t device);
 
 /* Message for the last failing call on this thread. */
 const char* shadowtopo_last_error(void);

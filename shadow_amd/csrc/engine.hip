@@ -1380,13 +1380,6 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
 }
 
 // WR[i] = in_r[WI[i]]: the dense reliability factors (0 where there is no arc)
-__global__ __launch_bounds__(256) void k_dense_wr(const int32_t* __restrict__ WI, const double* __restrict__ in_r,
-                                                  double* __restrict__ WR, size_t n) {
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        const int32_t a = WI[i];
-        WR[i] = a >= 0 ? in_r[a] : 0.0;
-    }
-}
 
 // Dense round 0 in one pass: the state k_init + k_seed + k_seed_dense would leave, with
 // every (v, source) entry written once.  A block owns 32 destinations [v0, v0+32) of one
@@ -3186,40 +3179,45 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
     if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
     const shadowtopo_stats keep = eng->st;
     std::vector<std::vector<double>> dl;
+    // One batch of up to 64 sampled candidates (cand[0] first, then every (A/64)-th), and
+    // farthest-point selection of the NL landmarks among them: each next landmark is the
+    // sample farthest (finite) from those chosen so far.  One SSSP batch instead of NL
+    // single-source runs one after another (C2 order 15.5 -> ~4 ms); any landmarks give a
+    // valid order, spread ones a local one.
+    const int32_t S = std::min<int32_t>(KL, A);
+    std::vector<int32_t> samp((size_t)S);
+    for (int32_t i = 0; i < S; ++i) samp[i] = cand[(size_t)((int64_t)i * A / S)];
     double* d_dist = nullptr;
-    HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V));
-    int32_t land = cand[0];
-    for (int k = 0; k < NL && land >= 0 && rc == 0; ++k) {
-        for (int j = 0; j < KL; ++j) {
-            eng->h_srcv[j] = j == 0 ? land : -1;
-            eng->h_row[j] = -1;
-        }
-        dl.emplace_back((size_t)V);
-        bool ok = hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL, hipMemcpyHostToDevice,
-                                 s) == hipSuccess;
-        if (!ok) {
-            rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
-            break;
-        }
-        if ((rc = run_rounds(eng, 1, s))) break;
-        hipLaunchKernelGGL(k_extract, dim3((V + 255) / 256, 1), dim3(256), 0, s, eng->g, eng->pools, 1, d_dist,
+    HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V * S));
+    for (int j = 0; j < KL; ++j) {
+        eng->h_srcv[j] = j < S ? samp[j] : -1;
+        eng->h_row[j] = -1;
+    }
+    if (hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL, hipMemcpyHostToDevice, s) !=
+        hipSuccess)
+        rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
+    if (rc == 0) rc = run_rounds(eng, 1, s);
+    if (rc == 0) {
+        hipLaunchKernelGGL(k_extract, dim3((V + 255) / 256, S), dim3(256), 0, s, eng->g, eng->pools, S, d_dist,
                            nullptr, nullptr, nullptr);
-        ok = hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(dl.back().data(), d_dist, sizeof(double) * (size_t)V, hipMemcpyDeviceToHost, s) ==
-                 hipSuccess &&
-             hipStreamSynchronize(s) == hipSuccess;
-        if (!ok) {
+        if (hipGetLastError() != hipSuccess) rc = fail(SHADOWTOPO_EDEVICE, "landmark distances");
+    }
+    std::vector<double> mind((size_t)S, HINF);  // each sample's distance from the landmarks so far
+    std::vector<char> taken((size_t)S, 0);
+    for (int32_t li = 0, k = 0; k < NL && li >= 0 && rc == 0; ++k) {
+        dl.emplace_back((size_t)V);
+        if (hipMemcpyAsync(dl.back().data(), d_dist + (size_t)li * V, sizeof(double) * (size_t)V,
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
             rc = fail(SHADOWTOPO_EDEVICE, "landmark distances");
             break;
         }
-        // next landmark: the attached vertex farthest (finite) from all landmarks so far
+        taken[li] = 1;
         double best = -1.0;
-        land = -1;
-        for (int32_t i = 0; i < A; ++i) {
-            const int32_t a = cand[i];
-            double m = HINF;
-            for (const auto& d : dl) m = std::min(m, d[a]);
-            if (m < HINF && m > best) best = m, land = a;
+        li = -1;
+        for (int32_t i = 0; i < S; ++i) {
+            mind[i] = std::min(mind[i], dl.back()[samp[i]]);
+            if (!taken[i] && mind[i] < HINF && mind[i] > best) best = mind[i], li = i;
         }
     }
     (void)hipFree(d_dist);
@@ -3799,11 +3797,9 @@ struct StagingRing {
 };
 StagingRing g_ring;
 
-hipError_t upload_staged(int device, const std::vector<UploadPart>& parts) {
-    std::lock_guard<std::mutex> lk(g_ring.mu);
-    StagingRing& R = g_ring;
-    constexpr size_t CH = StagingRing::CH;
-    constexpr int NB = StagingRing::NB, W = 2;
+// the ring on `device` (caller holds R.mu)
+hipError_t ring_ensure(StagingRing& R, int device) {
+    constexpr int NB = StagingRing::NB;
     if (R.device != device) {  // first use, or another device: (re)create on this one
         if (R.st) (void)hipStreamDestroy(R.st);
         for (int k = 0; k < NB; ++k) {
@@ -3816,11 +3812,28 @@ hipError_t upload_staged(int device, const std::vector<UploadPart>& parts) {
         R.device = -1;
         GB_TRY_HIP(hipStreamCreateWithFlags(&R.st, hipStreamNonBlocking));
         for (int k = 0; k < NB; ++k) {
-            GB_TRY_HIP(hipHostMalloc(&R.buf[k], CH, hipHostMallocDefault));
+            GB_TRY_HIP(hipHostMalloc(&R.buf[k], StagingRing::CH, hipHostMallocDefault));
             GB_TRY_HIP(hipEventCreateWithFlags(&R.ev[k], hipEventDisableTiming));
         }
         R.device = device;
     }
+    return hipSuccess;
+}
+
+hipError_t upload_staged(int device, const std::vector<UploadPart>& parts) {
+    std::lock_guard<std::mutex> lk(g_ring.mu);
+    StagingRing& R = g_ring;
+    constexpr size_t CH = StagingRing::CH;
+    constexpr int NB = StagingRing::NB;
+    int W = 2;
+    if (const char* f = getenv("SHADOWTOPO_UPLOAD_FILLERS"))  // A/B knob
+        if (atoi(f) >= 1 && atoi(f) <= NB) W = atoi(f);
+    const bool tr = getenv("SHADOWTOPO_TRACE_BUILD") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    GB_TRY_HIP(ring_ensure(R, device));
+    if (tr)
+        fprintf(stderr, "[upload] ring setup %.2f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     std::vector<std::pair<size_t, size_t>> chunks;  // (part, offset)
     for (size_t p = 0; p < parts.size(); ++p)
         for (size_t o = 0; o < parts[p].bytes; o += CH) chunks.emplace_back(p, o);
@@ -3848,16 +3861,85 @@ hipError_t upload_staged(int device, const std::vector<UploadPart>& parts) {
         }
         err[w] = e;
     };
-    std::thread helper(work, 1);
+    std::vector<std::thread> helpers;
+    for (int w = 1; w < W; ++w) helpers.emplace_back(work, w);
     work(0);
-    helper.join();
+    for (auto& h : helpers) h.join();
     const hipError_t e = hipStreamSynchronize(R.st);
+    if (tr)
+        fprintf(stderr, "[upload] %d fillers, total %.2f ms\n", W,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     for (hipError_t x : err)
         if (x != hipSuccess) return x;
     return e;
 }
 
+// Device preparation (shadowtopo_prepare), one background thread per process at a time: the
+// HIP runtime initialises a device lazily, at the first call that needs its queues (~85 ms on
+// MI355X, measured at the first stream creation), and each of the first few streams of a
+// process creates a hardware queue (~6-16 ms each); a code object loads at its first launch
+// (~10 ms each).  The thread does all of it -- the staging ring (its stream is the first), a
+// spare stream the next engine adopts, both code objects -- while the caller parses or
+// validates the edge list.
+struct Prep {
+    std::mutex mu;
+    std::thread th;
+    int device = -1;              // the device the running or finished preparation is for
+    hipStream_t spare = nullptr;  // an engine stream on `device`, adopted by the next create
+    double ms = 0.0;
+    ~Prep() {
+        if (th.joinable()) th.join();
+    }
+};
+Prep g_prep;
+
+void prep_work(int device) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipSetDevice(device) == hipSuccess) {
+        {
+            std::lock_guard<std::mutex> lk(g_ring.mu);
+            (void)ring_ensure(g_ring, device);
+        }
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+        hipFuncAttributes a;
+        (void)graph_build::preload();
+        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_self));
+        g_prep.spare = st;  // read only after the thread is joined
+    }
+    g_prep.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// waits for a preparation of `device` (none running: returns at once); hands over its spare
+// stream (nullptr if none) and how long it ran
+hipStream_t prep_wait(int device, double* prep_ms) {
+    std::lock_guard<std::mutex> lk(g_prep.mu);
+    if (g_prep.th.joinable()) g_prep.th.join();
+    hipStream_t st = nullptr;
+    if (g_prep.device == device) {
+        st = g_prep.spare;
+        g_prep.spare = nullptr;
+        *prep_ms = g_prep.ms;
+    }
+    return st;
+}
+
 }  // namespace
+
+int shadowtopo_prepare(int32_t device) {
+    if (device < 0 || device >= shadowtopo_device_count()) return fail(SHADOWTOPO_EINVAL, "device %d out of range", device);
+    std::lock_guard<std::mutex> lk(g_prep.mu);
+    if (g_prep.device == device && (g_prep.th.joinable() || g_prep.spare)) return SHADOWTOPO_OK;  // running or ready
+    if (g_prep.th.joinable()) g_prep.th.join();
+    if (g_prep.spare) {  // another device's spare stream
+        (void)hipStreamDestroy(g_prep.spare);
+        g_prep.spare = nullptr;
+    }
+    g_prep.device = device;
+    g_prep.ms = 0.0;
+    g_prep.th = std::thread(prep_work, device);
+    return SHADOWTOPO_OK;
+}
 
 int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_source, const int32_t* edge_target,
                       const double* edge_latency, const double* edge_packetloss, const double* vertex_packetloss,
@@ -3872,6 +3954,11 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     using clk = std::chrono::steady_clock;
     const auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
     auto t_phase = clk::now();
+    // the device preparation runs while the edge list is validated (unless a caller started it
+    // earlier); SHADOWTOPO_PRELOAD=0 (A/B knob) leaves all of it to the calls that need it
+    const char* pl = getenv("SHADOWTOPO_PRELOAD");
+    const bool prep = !(pl && pl[0] == '0');
+    if (prep && device >= 0 && device < shadowtopo_device_count()) (void)shadowtopo_prepare(device);
     int64_t n_loops = 0;
     if (n_edges > 0) {
         const int rcv = validate_edges(V, n_edges, edge_source, edge_target, edge_latency, edge_packetloss, &n_loops);
@@ -3880,10 +3967,25 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     int ndev = shadowtopo_device_count();
     if (ndev <= 0) return fail(SHADOWTOPO_EDEVICE, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(SHADOWTOPO_EINVAL, "device %d out of range", device);
+    double prep_ms = 0.0;
+    const auto t_wait = clk::now();
+    hipStream_t spare = prep ? prep_wait(device, &prep_ms) : nullptr;
+    const double wait_ms = ms_since(t_wait);
     HIP_TRY(hipSetDevice(device));
 
     auto* eng = new (std::nothrow) shadowtopo_engine();
-    if (!eng) return fail(SHADOWTOPO_ENOMEM, "engine alloc");
+    if (!eng) {
+        if (spare) (void)hipStreamDestroy(spare);
+        return fail(SHADOWTOPO_ENOMEM, "engine alloc");
+    }
+    eng->own_stream = spare;
+    if (!eng->own_stream && hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        eng->own_stream = nullptr;
+        shadowtopo_destroy(eng);
+        return fail(SHADOWTOPO_EDEVICE, "stream create failed");
+    }
+    eng->st.prepare_ms = prep_ms;
+    eng->st.create_prepare_wait_ms = wait_ms;
     eng->st.create_validate_ms = ms_since(t_phase);
     t_phase = clk::now();
     eng->V = V;
@@ -3899,6 +4001,15 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
             if (!std::isnan(vertex_packetloss[v])) vfac[v] = 1.0 - vertex_packetloss[v];
     int rc = 0;
     graph_build::Built gb;
+    // the build's scratch, freed after the dense tables are allocated (graph_build.h)
+    struct ScratchList {
+        std::vector<void*> v;
+        void release() {
+            for (void* p : v) (void)hipFree(p);
+            v.clear();
+        }
+        ~ScratchList() { release(); }
+    } scratch;
     {
         int32_t *d_src = nullptr, *d_dst = nullptr;
         double *d_lat = nullptr, *d_loss = nullptr;
@@ -3926,12 +4037,13 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         }
         eng->st.create_upload_ms = ms_since(t_phase);
         t_phase = clk::now();
-        hipStream_t bs = nullptr;
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
+        // the engine's stream builds the tables too (each further stream of a young process
+        // costs a hardware queue's creation)
+        hipStream_t bs = eng->own_stream;
         if (e == hipSuccess)
             e = graph_build::build(V, n_edges, n_loops, directed, CSR_PAD, d_src, d_dst, d_lat, d_loss, bs, gb,
-                                   eng->graph_allocs);
-        if (bs) (void)hipStreamDestroy(bs);
+                                   eng->graph_allocs, scratch.v);
+        if (getenv("SHADOWTOPO_TRACE_BUILD")) fprintf(stderr, "[create] graph build %.2f ms\n", ms_since(t_phase));
         if (e != hipSuccess) {
             shadowtopo_destroy(eng);
             return fail(e == hipErrorOutOfMemory ? SHADOWTOPO_ENOMEM : SHADOWTOPO_EDEVICE, "graph build: %s",
@@ -3991,15 +4103,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
             shadowtopo_destroy(eng);
             return rc;
         }
-        hipStream_t bs = nullptr;
-        hipError_t e = hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
-        if (e == hipSuccess) e = graph_build::build_dense(eng->Vp, gb, W, WI, W32, bs);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_dense_wr, dim3(4096), dim3(256), 0, bs, WI, gb.in_r, WR, Vp * Vp);
-            e = hipGetLastError();
-            if (e == hipSuccess) e = hipStreamSynchronize(bs);
-        }
-        if (bs) (void)hipStreamDestroy(bs);
+        if (getenv("SHADOWTOPO_TRACE_BUILD")) fprintf(stderr, "[create] dense alloc %.2f ms\n", ms_since(t_phase));
+        const hipError_t e = graph_build::build_dense(eng->Vp, gb, W, WI, W32, WR, eng->own_stream);
         if (e != hipSuccess) {
             shadowtopo_destroy(eng);
             return fail(SHADOWTOPO_EDEVICE, "dense tables: %s", hipGetErrorString(e));
@@ -4008,7 +4113,10 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         eng->d_WI = WI;
         eng->d_WR = WR;
         eng->d_W32 = W32;
+        if (getenv("SHADOWTOPO_TRACE_BUILD")) fprintf(stderr, "[create] dense tables %.2f ms\n", ms_since(t_phase));
     }
+    scratch.release();
+    if (getenv("SHADOWTOPO_TRACE_BUILD")) fprintf(stderr, "[create] scratch freed %.2f ms\n", ms_since(t_phase));
     // the arc heads were needed only for the dense tables
     for (auto& p : eng->graph_allocs)
         if (p == (void*)gb.arc_v) {
@@ -4022,8 +4130,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         g.out_ptr = g.in_ptr;
         g.out_dst = g.in_src;
     }
-    if (hipStreamCreateWithFlags(&eng->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess ||
+    if (hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess ||
         hipEventCreate(&eng->evm) != hipSuccess || hipEventCreate(&eng->evm2) != hipSuccess ||
         hipEventCreateWithFlags(&eng->ev_spin, hipEventDisableTiming) != hipSuccess) {
         shadowtopo_destroy(eng);
@@ -4042,6 +4149,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
     }
     eng->st.create_build_ms = ms_since(t_phase);
+    if (getenv("SHADOWTOPO_TRACE_BUILD")) fprintf(stderr, "[create] build total %.2f ms\n", eng->st.create_build_ms);
     eng->st.n_vertices = V;
     eng->st.n_edges = n_edges;
     eng->st.n_arcs = eng->n_arcs;
@@ -4323,6 +4431,8 @@ void shadowtopo_reset_stats(shadowtopo_engine* eng) {
     eng->st.create_build_ms = keep.create_build_ms;
     eng->st.order_ms = keep.order_ms;
     eng->st.create_alloc_ms = keep.create_alloc_ms;
+    eng->st.prepare_ms = keep.prepare_ms;
+    eng->st.create_prepare_wait_ms = keep.create_prepare_wait_ms;
 }
 
 int shadowtopo_is_complete(const shadowtopo_engine* eng) {

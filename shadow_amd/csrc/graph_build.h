@@ -41,13 +41,22 @@ struct Built {
 // buffers the caller has recorded in `allocs`: they become the igraph storage in place
 // (efrom/eto overwrite src/dst, erel overwrites packetloss, elat IS d_lat), so the build
 // allocates and copies nothing for them; n_loops: self-loop edges among them (counted by
-// the caller's validation pass); pad: padding arcs appended to the in-CSR (u = 0, w = +inf)
+// the caller's validation pass); pad: padding arcs appended to the in-CSR (u = 0, w = +inf);
+// scratch: the build's temporary device buffers, for the caller to hipFree once it has made
+// its next large allocations (VRAM freed just before an allocation stalls it: the dense
+// tables' allocation took 15-21 ms right after the 2.3 GB scratch of C2 was freed)
 hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, int32_t* d_src, int32_t* d_dst,
-                 double* d_lat, double* d_loss, hipStream_t s, Built& out, std::vector<void*>& allocs);
+                 double* d_lat, double* d_loss, hipStream_t s, Built& out, std::vector<void*>& allocs,
+                 std::vector<void*>& scratch);
 
-// dense tables [Vp][Vp] of the merged in-CSR: W (latency, +inf where no arc), WI (in-arc
-// index, -1) and W32 (latency rounded toward -inf, NaN where no arc)
-hipError_t build_dense(int32_t Vp, const Built& g, double* W, int32_t* WI, float* W32, hipStream_t s);
+// dense tables [Vp][Vp] of the merged in-CSR, row = tail u, column = head v: W (latency,
+// +inf where no arc), WI (in-arc index, -1), W32 (latency rounded toward -inf, NaN where no
+// arc) and WR (the arc's reliability factor, 0 where no arc)
+hipError_t build_dense(int32_t Vp, const Built& g, double* W, int32_t* WI, float* W32, double* WR, hipStream_t s);
+
+// Loads this file's code object on the current device (the runtime does it at the first launch
+// otherwise), so a caller can overlap it with host work.
+hipError_t preload();
 
 }  // namespace graph_build
 

@@ -17,7 +17,10 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <chrono>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 
@@ -40,12 +43,9 @@ hipError_t dalloc(std::vector<void*>& owner, T** p, size_t n) {
     return hipSuccess;
 }
 
-// scratch freed at the end of build()
+// the build's scratch allocations, recorded in the caller's list (it frees them)
 struct Scratch {
-    std::vector<void*> v;
-    ~Scratch() {
-        for (void* p : v) (void)hipFree(p);
-    }
+    std::vector<void*>& v;
 };
 
 inline unsigned grid_of(int64_t n, int bs = 256) {
@@ -199,29 +199,58 @@ __global__ void k_inc_fill(int64_t E, const int32_t* __restrict__ row, const int
 // a self-loop) reaches V
 __global__ void k_complete(int32_t V, int directed, const int64_t* __restrict__ inc_ptr,
                            const int32_t* __restrict__ loop_eid, int32_t* ok) {
+    bool short_list = false;
     for (int32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
         int64_t c = inc_ptr[v + 1] - inc_ptr[v];
         if (!directed && loop_eid[v] >= 0) c -= 1;
-        if (c < V) atomicAnd(ok, 0);
+        short_list |= c < V;
     }
+    // one atomic per wave (one per vertex serialised 8.7e5 atomics on one word: 9.9 ms on C5)
+    if (__ballot(short_list) != 0ull && (threadIdx.x & 63) == 0) atomicAnd(ok, 0);
 }
 
-__global__ void k_dense_fill(int64_t n, double* W, int32_t* WI, float* W32) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        W[i] = __longlong_as_double(0x7ff0000000000000LL);
+__global__ void k_dense_fill(int64_t n, int32_t* WI) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         WI[i] = -1;
-        W32[i] = __int_as_float(0x7fc00000);
-    }
 }
 
-__global__ void k_dense_scatter(int64_t M, int32_t Vp, const int32_t* __restrict__ in_src,
-                                const int32_t* __restrict__ arc_v, const double* __restrict__ in_w, double* W,
-                                int32_t* WI, float* W32) {
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < M; p += (int64_t)gridDim.x * blockDim.x) {
-        const size_t o = (size_t)in_src[p] * Vp + arc_v[p];
-        W[o] = in_w[p];
-        WI[o] = (int32_t)p;
-        W32[o] = __double2float_rd(in_w[p]);
+// the arcs' ids at their TRANSPOSED cells WI[v][u]: the in-CSR lists each head v's arcs by
+// ascending tail u, so consecutive arcs write neighbouring words (the direct cell [u][v]
+// would be one line per arc, Vp * 4 bytes apart: 4.8 ms on C2 against 0.1 ms)
+__global__ void k_dense_scatter_t(int64_t M, int32_t Vp, const int32_t* __restrict__ in_src,
+                                  const int32_t* __restrict__ arc_v, int32_t* WI) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < M; p += (int64_t)gridDim.x * blockDim.x)
+        WI[(size_t)arc_v[p] * Vp + in_src[p]] = (int32_t)p;
+}
+
+// WI transposed in place, 64 x 64 tiles: block (I, J), I <= J, holds tiles (I, J) and (J, I)
+// in LDS and writes each one's transpose over the other, with the W / W32 / WR cells of both
+// from the arcs' latency and reliability (the arcs of one tile's column are consecutive, so
+// the gathers stay within a few lines per column)
+constexpr int DTT = 64;
+__global__ __launch_bounds__(256) void k_dense_tr(int32_t Vp, int32_t* WI, const double* __restrict__ in_w,
+                                                  const double* __restrict__ in_r, double* __restrict__ W,
+                                                  float* __restrict__ W32, double* __restrict__ WR) {
+    __shared__ int32_t sa[DTT][DTT + 1], sb[DTT][DTT + 1];
+    const int32_t I = blockIdx.x, J = blockIdx.y;
+    if (I > J) return;
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+    const size_t a0 = (size_t)I * DTT * Vp + (size_t)J * DTT, b0 = (size_t)J * DTT * Vp + (size_t)I * DTT;
+    for (int r = r0; r < DTT; r += 4) {
+        sa[r][c] = WI[a0 + (size_t)r * Vp + c];
+        if (I != J) sb[r][c] = WI[b0 + (size_t)r * Vp + c];
+    }
+    __syncthreads();
+    auto put = [&](size_t o, int32_t a) {
+        const double w = a >= 0 ? in_w[a] : __longlong_as_double(0x7ff0000000000000LL);
+        WI[o] = a;
+        W[o] = w;
+        W32[o] = a >= 0 ? __double2float_rd(w) : __int_as_float(0x7fc00000);
+        WR[o] = a >= 0 ? in_r[a] : 0.0;
+    };
+    for (int r = r0; r < DTT; r += 4) {
+        put(b0 + (size_t)r * Vp + c, sa[c][r]);  // cell (J*64 + r, I*64 + c) = transposed (I, J) tile
+        if (I != J) put(a0 + (size_t)r * Vp + c, sb[c][r]);
     }
 }
 
@@ -260,8 +289,18 @@ hipError_t exclusive_sum(Scratch& sc, const T* in, T* out, int64_t n, hipStream_
 }  // namespace
 
 hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, int32_t* d_src, int32_t* d_dst,
-                 double* d_lat, double* d_loss, hipStream_t s, Built& g, std::vector<void*>& allocs) {
-    Scratch sc;
+                 double* d_lat, double* d_loss, hipStream_t s, Built& g, std::vector<void*>& allocs,
+                 std::vector<void*>& scratch) {
+    const bool tr = getenv("SHADOWTOPO_TRACE_BUILD") != nullptr;
+    auto t_ph = std::chrono::steady_clock::now();
+    auto stamp = [&](const char* what) {
+        if (!tr) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[graph_build] %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_ph).count());
+        t_ph = t;
+    };
+    Scratch sc{scratch};
     const int dir = directed ? 1 : 0;
     const int64_t NA = directed ? E : 2 * E;           // arcs before dropping loops
     const int64_t NL = NA - (directed ? 1 : 2) * n_loops;  // non-loop arcs
@@ -290,7 +329,9 @@ hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, 
     hipLaunchKernelGGL(k_loop_fix, dim3(grid_of(V)), dim3(256), 0, s, V, g.loop_eid);
     GB_TRY(hipGetLastError());
     const int kbits = 32 + bitlen((uint64_t)V);
+    stamp("edges");
     GB_TRY(sort_pairs(sc, ak, ak2, av, av2, NA, kbits, s));
+    stamp("arc sort");
     // merge runs of parallel arcs
     int32_t *head = nullptr, *pos = nullptr, *d_mg = nullptr;
     GB_TRY(dalloc(sc.v, &head, NL));
@@ -321,6 +362,7 @@ hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, 
     if (pad > 0) hipLaunchKernelGGL(k_pad, dim3(1), dim3(64), 0, s, M, pad, g.in_src, g.in_w, g.in_w32, g.in_r, g.in_eid);
     hipLaunchKernelGGL(k_bounds, dim3(grid_of(M > 0 ? M : V + 1)), dim3(256), 0, s, M, V, g.arc_v, g.in_ptr);
     GB_TRY(hipGetLastError());
+    stamp("merge");
     // out-CSR (directed): merged arcs by (u, v)
     if (directed) {
         GB_TRY(dalloc(allocs, &g.out_ptr, (size_t)V + 1));
@@ -336,6 +378,7 @@ hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, 
         hipLaunchKernelGGL(k_bounds, dim3(grid_of(M > 0 ? M : V + 1)), dim3(256), 0, s, M, V, ou, g.out_ptr);
         GB_TRY(hipGetLastError());
     }
+    stamp("out-csr");
     // igraph_incident(OUT) order
     GB_TRY(dalloc(allocs, &g.inc_ptr, (size_t)V + 1));
     int64_t *os = nullptr, *is = nullptr, *cnt = nullptr;
@@ -376,6 +419,7 @@ hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, 
             hipLaunchKernelGGL(k_inc_fill, dim3(grid_of(E)), dim3(256), 0, s, E, irow, ival, is, os, g.inc_ptr, 1,
                                g.inc_eid);
     }
+    stamp("incidence");
     int32_t* d_ok = nullptr;
     GB_TRY(dalloc(sc.v, &d_ok, 1));
     const int32_t one = 1;
@@ -386,18 +430,39 @@ hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, 
     GB_TRY(hipMemcpyAsync(&flags[0], d_mg, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GB_TRY(hipMemcpyAsync(&flags[1], d_ok, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GB_TRY(hipStreamSynchronize(s));
+    stamp("tail");
     g.multigraph = flags[0];
     g.complete = flags[1];
     return hipSuccess;
 }
 
-hipError_t build_dense(int32_t Vp, const Built& g, double* W, int32_t* WI, float* W32, hipStream_t s) {
+hipError_t preload() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_edges));
+}
+
+hipError_t build_dense(int32_t Vp, const Built& g, double* W, int32_t* WI, float* W32, double* WR, hipStream_t s) {
+    if (Vp % DTT) return hipErrorInvalidValue;
     const int64_t n = (int64_t)Vp * Vp;
-    hipLaunchKernelGGL(k_dense_fill, dim3(grid_of(n)), dim3(256), 0, s, n, W, WI, W32);
+    const bool tr = getenv("SHADOWTOPO_TRACE_BUILD") != nullptr;
+    auto t_ph = std::chrono::steady_clock::now();
+    auto stamp = [&](const char* what) {
+        if (!tr) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[graph_build] %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_ph).count());
+        t_ph = t;
+    };
+    stamp("dense start");
+    hipLaunchKernelGGL(k_dense_fill, dim3(grid_of(n)), dim3(256), 0, s, n, WI);
+    stamp("dense fill");
     if (g.n_arcs > 0)
-        hipLaunchKernelGGL(k_dense_scatter, dim3(grid_of(g.n_arcs)), dim3(256), 0, s, g.n_arcs, Vp, g.in_src, g.arc_v,
-                           g.in_w, W, WI, W32);
+        hipLaunchKernelGGL(k_dense_scatter_t, dim3(grid_of(g.n_arcs)), dim3(256), 0, s, g.n_arcs, Vp, g.in_src,
+                           g.arc_v, WI);
+    stamp("dense scatter");
+    hipLaunchKernelGGL(k_dense_tr, dim3(Vp / DTT, Vp / DTT), dim3(256), 0, s, Vp, WI, g.in_w, g.in_r, W, W32, WR);
     GB_TRY(hipGetLastError());
+    stamp("dense transpose");
     return hipStreamSynchronize(s);
 }
 

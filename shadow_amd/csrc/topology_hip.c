@@ -977,6 +977,9 @@ Topology* topology_new(const char* graphPath) {
         }
     }
     atomic_store(&top->mat, NULL);
+    /* the device's runtime initialisation, staging buffers and code objects on a background
+     * thread while the file is parsed (shadowtopo_prepare); the engine is created later */
+    if (top->device >= 0 && top->device < shadowtopo_device_count()) (void)shadowtopo_prepare(top->device);
 
     char err[512] = {0};
     st_message("reading graphml topology graph at '%s'...", graphPath);

@@ -53,7 +53,7 @@ CSR_FULL = 1  # recompute every active vertex over all in-arcs (k_relax / k_rela
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (
-    "shadowtopo_device_count", "shadowtopo_last_error", "shadowtopo_create", "shadowtopo_destroy",
+    "shadowtopo_device_count", "shadowtopo_prepare", "shadowtopo_last_error", "shadowtopo_create", "shadowtopo_destroy",
     "shadowtopo_set_attached", "shadowtopo_set_option", "shadowtopo_compute_rows", "shadowtopo_sssp",
     "shadowtopo_get_stats", "shadowtopo_reset_stats", "shadowtopo_is_complete", "shadowtopo_get_eid",
     "shadowtopo_host_alloc", "shadowtopo_host_free",
@@ -82,6 +82,7 @@ class Stats(ctypes.Structure):
         ("create_validate_ms", ctypes.c_double), ("create_upload_ms", ctypes.c_double),
         ("create_build_ms", ctypes.c_double), ("order_ms", ctypes.c_double),
         ("create_alloc_ms", ctypes.c_double), ("gated_final_releases", ctypes.c_int64),
+        ("prepare_ms", ctypes.c_double), ("create_prepare_wait_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -103,6 +104,8 @@ def lib():
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         vp = ctypes.c_void_p
         L.shadowtopo_device_count.restype = ctypes.c_int
+        L.shadowtopo_prepare.restype = ctypes.c_int
+        L.shadowtopo_prepare.argtypes = [ctypes.c_int32]
         L.shadowtopo_last_error.restype = ctypes.c_char_p
         L.shadowtopo_create.restype = ctypes.c_int
         L.shadowtopo_create.argtypes = [ctypes.c_int32, ctypes.c_int64, vp, vp, vp, vp, vp, ctypes.c_uint32,
@@ -161,6 +164,13 @@ def pinned_empty(shape, dtype):
 
 def device_count():
     return int(lib().shadowtopo_device_count())
+
+
+def prepare(device=0):
+    """Start the device preparation on a background thread (shadowtopo_prepare)."""
+    rc = lib().shadowtopo_prepare(int(device))
+    if rc != 0:
+        raise ShadowTopoError(f"shadowtopo_prepare: {lib().shadowtopo_last_error().decode()}")
 
 
 class Engine:
