@@ -438,3 +438,22 @@ def test_dense_delta_live_chunks(case, live, monkeypatch):
     st = compare(g, layout="dense", delta_permille=1000, dense_prune=0)
     assert st["dense"] == 1 and st["delta_sweeps"] > 0
     assert (st["sparse_deltas"] > 0) == (live == "1")
+
+
+@pytest.mark.gpu
+def test_prepare_then_create_same_results():
+    """An engine created after shadowtopo_prepare adopts the prepared stream and gives the
+    same results as one created without it (the preparation only moves runtime work)."""
+    g = synth.random_sparse(V=400, avg_deg=5, seed=31)
+    E.prepare(0)
+    E.prepare(0)  # idempotent while running or ready
+    a = E.Engine.from_synth(g)
+    st = a.stats()
+    assert st["prepare_ms"] >= 0.0 and st["create_prepare_wait_ms"] >= 0.0
+    a.set_attached(g.attached)
+    ra = a.compute_rows(0, len(g.attached))
+    b = E.Engine.from_synth(g)  # no preparation pending: creates its own stream
+    b.set_attached(g.attached)
+    rb = b.compute_rows(0, len(g.attached))
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x, y)

@@ -442,3 +442,12 @@ def test_engine_edge_validation_reports_the_first_bad_edge(n_edges):
             E.Engine(V, a["src"], a["dst"], a["lat"], a["loss"])
         msg = str(ei.value)
         assert f"edge {first[0]} " in msg and first[3] in msg, msg
+
+
+def test_prepare_rejects_a_bad_device():
+    """shadowtopo_prepare validates the ordinal before starting its thread (no device here:
+    every ordinal is out of range; on a GPU box -1 still is)."""
+    with pytest.raises(E.ShadowTopoError):
+        E.prepare(-1)
+    with pytest.raises(E.ShadowTopoError):
+        E.prepare(E.device_count())
