@@ -1675,7 +1675,8 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
                                                                  const int32_t* __restrict__ nlive,
                                                                  const int32_t* __restrict__ perm,
                                                                  const float* __restrict__ minW64,
-                                                                 const float* __restrict__ minDc) {
+                                                                 const float* __restrict__ minDc,
+                                                                 const float* __restrict__ minWc) {
     // PR (pruned): rows, destinations and W32 (here W32p) in the vertex locality order `perm`,
     // and the block walks only the chunks that can hold a passing pair: a chunk is dead when
     // for every source s, minDc(chunk, s) > fl32(maxT_s - minW64(chunk, tile)), where minDc is
@@ -1684,6 +1685,10 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     // tighten) and minW64 the smallest W32 of the chunk x tile block.  Every pair's filter
     // bound max_v fl32(sT[s][v] - W32(u, v)) is <= the chunk's (rounding is monotone), so a dead
     // chunk holds no pair the filter would pass: the skip is exact.
+    // With minWc (the sweep's per-(32-row chunk, column) W32 minima) the bound is taken per
+    // destination instead: the chunk is dead when minDc(chunk, s) > max_v fl32(sT[s][v] -
+    // mWc(chunk, v)) for every s, mWc(chunk, v) = min W32 of the chunk's rows into v -- the
+    // same argument (W32(u, v) >= mWc(chunk, v)), and never looser than the tile bound.
     constexpr int SW = KL / DW;  // sources per wave
     constexpr int PF = KL * KL / 4 / (64 * DW);  // float4 of one W32 slab per thread
     __shared__ __attribute__((aligned(16))) float sT[KL * SWS];  // [s][v] thresholds
@@ -1720,7 +1725,49 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     int16_t* ring = sP[wave];
     unsigned long long mine = 0;
 
-    if (PR) {
+    if (PR && minWc) {
+        // per-destination bounds: wave w evaluates chunks w, w + DW, ... for all 64 sources
+        // (lane = source) with the chunk's column minima staged in its own row of sW (free
+        // until the first slab); the live flags go to sP's bytes, wave 0 lists them in order
+        __syncthreads();  // thresholds staged
+        uint8_t* flags = reinterpret_cast<uint8_t*>(&sP[0][0]);
+        float* mrow = &sW[wave * SWS];
+        const int32_t nc32 = (V + SRS - 1) / SRS;
+        const float* md = minDc + (size_t)b * nvc * KL + lane;
+        const float* trow = &sT[lane * SWS];
+        for (int32_t c = wave; c < nvc; c += DW) {
+            const float m0 = minWc[(size_t)(2 * c) * Vp + v0 + lane];
+            const float m1 = 2 * c + 1 < nc32 ? minWc[(size_t)(2 * c + 1) * Vp + v0 + lane] : __int_as_float(0x7f800000);
+            const float d = md[(size_t)c * KL];
+            mrow[lane] = fminf(m0, m1);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row is written
+            float g = __int_as_float(0x7fc00000);
+#pragma unroll
+            for (int j = 0; j < KL / 4; ++j) {
+                const f4 t4 = *(const f4*)&trow[4 * j];
+                const f4 w4 = *(const f4*)&mrow[4 * j];
+                g = fmaxf(fmaxf(g, t4.x - w4.x), t4.y - w4.y);
+                g = fmaxf(fmaxf(g, t4.z - w4.z), t4.w - w4.w);
+            }
+            const unsigned long long bal = __ballot(d <= g);
+            if (lane == 0) flags[c] = bal != 0ull;
+            __builtin_amdgcn_wave_barrier();  // every lane's reads of mrow before the next chunk's write
+        }
+        __syncthreads();  // flags
+        if (wave == 0) {
+            int32_t n = 0;
+            for (int32_t c0 = 0; c0 < nvc; c0 += 64) {
+                const bool f = c0 + lane < nvc && flags[c0 + lane];
+                const unsigned long long bal = __ballot(f);
+                if (f)
+                    sL[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] =
+                        (int16_t)(c0 + lane);
+                n += __popcll(bal);
+            }
+            if (lane == 0) sNL = n;
+        }
+    } else if (PR) {
         // the block's live chunks: every wave evaluates every chunk for all 64 sources (lane =
         // source) and gets the same answer; wave 0 writes the list
         __syncthreads();  // thresholds staged
@@ -2472,6 +2519,7 @@ struct shadowtopo_engine {
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
+    int32_t opt_delta_colbound = 1;    // pruned delta: per-destination chunk bounds (k_relax_dense_delta_s)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
@@ -3041,7 +3089,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur, nullptr, nullptr, eng->d_perm,
-                                       eng->d_minW64, eng->d_minDc);
+                                       eng->d_minW64, eng->d_minDc, eng->opt_delta_colbound ? eng->d_minW : nullptr);
                     eng->st.pruned_deltas++;
                 } else {
                     // a round after one that changed few pairs walks only the chunks holding
@@ -3066,7 +3114,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     hipLaunchKernelGGL(k_relax_dense_delta_s<false>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur, live, nlive, nullptr, nullptr,
-                                       nullptr);
+                                       nullptr, nullptr);
                 }
                 eng->st.delta_sweeps++;
             }
@@ -4143,6 +4191,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (dl && dl[0] >= '0' && dl[0] <= '2') eng->opt_delta_live = dl[0] - '0';
         const char* dd = getenv("SHADOWTOPO_DELTA_LIVE_DIV");
         if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
+        const char* cb = getenv("SHADOWTOPO_DELTA_COLBOUND");  // A/B knob: 0 or 1 (default)
+        if (cb && (cb[0] == '0' || cb[0] == '1')) eng->opt_delta_colbound = cb[0] - '0';
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
