@@ -1676,7 +1676,8 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
                                                                  const int32_t* __restrict__ perm,
                                                                  const float* __restrict__ minW64,
                                                                  const float* __restrict__ minDc,
-                                                                 const float* __restrict__ minWc) {
+                                                                 const float* __restrict__ minWc,
+                                                                 unsigned long long* __restrict__ cmask) {
     // PR (pruned): rows, destinations and W32 (here W32p) in the vertex locality order `perm`,
     // and the block walks only the chunks that can hold a passing pair: a chunk is dead when
     // for every source s, minDc(chunk, s) > fl32(maxT_s - minW64(chunk, tile)), where minDc is
@@ -1751,7 +1752,11 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
                 g = fmaxf(fmaxf(g, t4.z - w4.z), t4.w - w4.w);
             }
             const unsigned long long bal = __ballot(d <= g);
-            if (lane == 0) flags[c] = bal != 0ull;
+            if (lane == 0) {
+                flags[c] = bal != 0ull;
+                // the sources that can pass in this chunk: the walk lists only their pairs
+                if (cmask) cmask[(size_t)L * PR_CHUNKS + c] = bal;
+            }
             __builtin_amdgcn_wave_barrier();  // every lane's reads of mrow before the next chunk's write
         }
         __syncthreads();  // flags
@@ -1878,10 +1883,15 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         if (PR) return (all_chunks ? i : (int32_t)sL[i]) * KL;
         return (live ? live[(size_t)b * nvc + i] : i) * KL;
     };
+    // PR with per-destination bounds: the chunk's passing sources (cmask, written above by the
+    // evaluating wave; visible after the barrier), one chunk ahead like the change masks
+    const unsigned long long* cm = (PR && minWc && cmask && !all_chunks) ? cmask + (size_t)L * PR_CHUNKS : nullptr;
+    unsigned long long smk = ~0ull, smk_n = ~0ull;
     // PR: row vertices one chunk ahead of the masks that are gathered through them
     int32_t urow = 0, urow_n = 0;
     unsigned long long mnext = 0;
     if (nwalk > 0) {
+        if (cm) smk = cm[chunk_u0(0) / KL];
         const int32_t f0 = chunk_u0(0);
         fetch(f0);
         stash();
@@ -1894,7 +1904,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         const int32_t u0 = chunk_u0(ci);
         const bool more = ci + 1 < nwalk;
         const int32_t un = more ? chunk_u0(ci + 1) : 0;
-        const unsigned long long m = (u0 + lane < V) ? (mnext & srange) : 0ull;
+        const unsigned long long m = (u0 + lane < V) ? (mnext & srange & smk) : 0ull;
         // exclusive prefix sum of the per-row pair counts (<= 16, five bits) from ballots
         // and mbcnt: no cross-lane LDS round trips
         const int p = __popcll(m);
@@ -1911,6 +1921,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         const int32_t urow_nn = (PR && ci + 2 < nwalk) ? perm[chunk_u0(ci + 2) + lane] : 0;
         pma = chp + (PR ? (more ? urow_n : 0) : un + lane);
         mnext = *pma;
+        if (cm && more) smk_n = cm[un / KL];
         if (more) fetch(un);
         for (int base = 0; base < tot; base += RING_S) {  // usually one segment (C2: ~40 pairs)
             unsigned long long mm = m;
@@ -1931,6 +1942,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         __syncthreads();
         urow = PR ? urow_n : un + lane;
         urow_n = urow_nn;
+        smk = smk_n;
     }
     // the waves' change masks, in the thresholds' LDS (every wave is past the walk's last
     // barrier: nobody reads sT any more)
@@ -2432,6 +2444,8 @@ struct shadowtopo_engine {
     float* d_minD = nullptr;    // [nb_cap][nchunks][64] min D32 per chunk and lane
     float* d_minW64 = nullptr;  // [nvc][nvc] min W32p over each 64 x 64 block (pruned delta rounds)
     float* d_minDc = nullptr;   // [nb_cap][nvc][64] min D32 over each 64-row chunk's changed pairs
+    unsigned long long* d_cmask = nullptr;  // pruned delta: per block and live chunk, the sources that can pass
+    size_t cmask_n = 0;
     size_t minDc_n = 0;
     size_t minD_n = 0;
     bool vperm_ready = false;
@@ -2519,7 +2533,7 @@ struct shadowtopo_engine {
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
-    int32_t opt_delta_colbound = 1;    // pruned delta: per-destination chunk bounds (k_relax_dense_delta_s)
+    int32_t opt_delta_colbound = 2;    // pruned delta: per-destination chunk bounds (1), + per-chunk source masks (2)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
@@ -3084,12 +3098,21 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                         HIP_TRY(hipMalloc((void**)&eng->d_minDc, need * sizeof(float)));
                         eng->minDc_n = need;
                     }
+                    const size_t need_cm = (size_t)nblocks_delta * PR_CHUNKS;
+                    if (eng->opt_delta_colbound >= 2 && eng->cmask_n < need_cm) {
+                        if (eng->d_cmask) (void)hipFree(eng->d_cmask);
+                        eng->d_cmask = nullptr;
+                        eng->cmask_n = 0;
+                        HIP_TRY(hipMalloc((void**)&eng->d_cmask, need_cm * sizeof(unsigned long long)));
+                        eng->cmask_n = need_cm;
+                    }
                     hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, nbg), dim3(256), 0, s, eng->pools,
                                        eng->d_perm, V, nvc, par, cnt_prev, thresh, eng->d_minDc);
                     hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur, nullptr, nullptr, eng->d_perm,
-                                       eng->d_minW64, eng->d_minDc, eng->opt_delta_colbound ? eng->d_minW : nullptr);
+                                       eng->d_minW64, eng->d_minDc, eng->opt_delta_colbound ? eng->d_minW : nullptr,
+                                       eng->opt_delta_colbound >= 2 ? eng->d_cmask : nullptr);
                     eng->st.pruned_deltas++;
                 } else {
                     // a round after one that changed few pairs walks only the chunks holding
@@ -3114,7 +3137,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     hipLaunchKernelGGL(k_relax_dense_delta_s<false>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
                                        nbg, nvc, par, thresh, cnt_prev, cnt_cur, live, nlive, nullptr, nullptr,
-                                       nullptr, nullptr);
+                                       nullptr, nullptr, nullptr);
                 }
                 eng->st.delta_sweeps++;
             }
@@ -4191,8 +4214,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (dl && dl[0] >= '0' && dl[0] <= '2') eng->opt_delta_live = dl[0] - '0';
         const char* dd = getenv("SHADOWTOPO_DELTA_LIVE_DIV");
         if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
-        const char* cb = getenv("SHADOWTOPO_DELTA_COLBOUND");  // A/B knob: 0 or 1 (default)
-        if (cb && (cb[0] == '0' || cb[0] == '1')) eng->opt_delta_colbound = cb[0] - '0';
+        const char* cb = getenv("SHADOWTOPO_DELTA_COLBOUND");  // A/B knob: 0, 1 or 2 (default)
+        if (cb && cb[0] >= '0' && cb[0] <= '2') eng->opt_delta_colbound = cb[0] - '0';
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
@@ -4238,6 +4261,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_minD) (void)hipFree(eng->d_minD);
     if (eng->d_minW64) (void)hipFree(eng->d_minW64);
     if (eng->d_minDc) (void)hipFree(eng->d_minDc);
+    if (eng->d_cmask) (void)hipFree(eng->d_cmask);
     if (eng->ev0) (void)hipEventDestroy(eng->ev0);
     if (eng->ev1) (void)hipEventDestroy(eng->ev1);
     if (eng->evm) (void)hipEventDestroy(eng->evm);
