@@ -1712,9 +1712,14 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     const int32_t v = PR ? perm[v0 + lane] : v0 + lane;  // this lane's destination vertex
     const BatchDev B = batch_view(pools, b);
     const gdouble* D = B.D;
-    for (int i = wave; i < KL; i += DW) {
-        const int32_t vi = PR ? perm[v0 + i] : v0 + i;
-        sT[lane * SWS + i] = f32_thr(D[(size_t)vi * KL + lane]);
+    {
+        // the wave's 16 threshold rows with their loads in flight together (the row vertices
+        // are the lanes' own destinations)
+        double dd[KL / DW];
+#pragma unroll
+        for (int k = 0; k < KL / DW; ++k) dd[k] = D[(size_t)__builtin_amdgcn_readlane(v, wave + k * DW) * KL + lane];
+#pragma unroll
+        for (int k = 0; k < KL / DW; ++k) sT[lane * SWS + wave + k * DW] = f32_thr(dd[k]);
     }
     const int32_t s0 = wave * SW;
     const unsigned long long srange = ((1ull << SW) - 1ull) << s0;
@@ -1732,32 +1737,44 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         // until the first slab); the live flags go to sP's bytes, wave 0 lists them in order
         __syncthreads();  // thresholds staged
         uint8_t* flags = reinterpret_cast<uint8_t*>(&sP[0][0]);
-        float* mrow = &sW[wave * SWS];
+        float* mrow = &sW[wave * 4 * SWS];  // 4 rows per wave
         const int32_t nc32 = (V + SRS - 1) / SRS;
         const float* md = minDc + (size_t)b * nvc * KL + lane;
         const float* trow = &sT[lane * SWS];
-        for (int32_t c = wave; c < nvc; c += DW) {
-            const float m0 = minWc[(size_t)(2 * c) * Vp + v0 + lane];
-            const float m1 = 2 * c + 1 < nc32 ? minWc[(size_t)(2 * c + 1) * Vp + v0 + lane] : __int_as_float(0x7f800000);
-            const float d = md[(size_t)c * KL];
-            mrow[lane] = fminf(m0, m1);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row is written
-            float g = __int_as_float(0x7fc00000);
+        // G chunks per step, their loads issued together (one chunk's dependent loads per
+        // step left every step waiting out a global load)
+        constexpr int G = 4;
+        for (int32_t c0 = wave * G; c0 < nvc; c0 += DW * G) {
+            float m0[G], m1[G], d[G];
 #pragma unroll
-            for (int j = 0; j < KL / 4; ++j) {
-                const f4 t4 = *(const f4*)&trow[4 * j];
-                const f4 w4 = *(const f4*)&mrow[4 * j];
-                g = fmaxf(fmaxf(g, t4.x - w4.x), t4.y - w4.y);
-                g = fmaxf(fmaxf(g, t4.z - w4.z), t4.w - w4.w);
+            for (int k = 0; k < G; ++k) {
+                const int32_t c = c0 + k < nvc ? c0 + k : nvc - 1;
+                m0[k] = minWc[(size_t)(2 * c) * Vp + v0 + lane];
+                m1[k] = 2 * c + 1 < nc32 ? minWc[(size_t)(2 * c + 1) * Vp + v0 + lane] : __int_as_float(0x7f800000);
+                d[k] = md[(size_t)c * KL];
             }
-            const unsigned long long bal = __ballot(d <= g);
-            if (lane == 0) {
-                flags[c] = bal != 0ull;
-                // the sources that can pass in this chunk: the walk lists only their pairs
-                if (cmask) cmask[(size_t)L * PR_CHUNKS + c] = bal;
+#pragma unroll
+            for (int k = 0; k < G; ++k) mrow[k * SWS + lane] = fminf(m0[k], m1[k]);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the rows are written
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                float g = __int_as_float(0x7fc00000);
+#pragma unroll
+                for (int j = 0; j < KL / 4; ++j) {
+                    const f4 t4 = *(const f4*)&trow[4 * j];
+                    const f4 w4 = *(const f4*)&mrow[k * SWS + 4 * j];
+                    g = fmaxf(fmaxf(g, t4.x - w4.x), t4.y - w4.y);
+                    g = fmaxf(fmaxf(g, t4.z - w4.z), t4.w - w4.w);
+                }
+                const unsigned long long bal = __ballot(d[k] <= g);
+                if (lane == 0 && c0 + k < nvc) {
+                    flags[c0 + k] = bal != 0ull;
+                    // the sources that can pass in this chunk: the walk lists only their pairs
+                    if (cmask) cmask[(size_t)L * PR_CHUNKS + c0 + k] = bal;
+                }
             }
-            __builtin_amdgcn_wave_barrier();  // every lane's reads of mrow before the next chunk's write
+            __builtin_amdgcn_wave_barrier();  // every lane's reads of the rows before the next step's writes
         }
         __syncthreads();  // flags
         if (wave == 0) {
