@@ -848,7 +848,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        const int32_t* __restrict__ ipos,
                                                        const int32_t* __restrict__ WIp,
                                                        const double* __restrict__ WRp,
-                                                       const double* __restrict__ vfac) {
+                                                       const double* __restrict__ vfac, int32_t spiral) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -947,7 +947,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     // nearest rows) first, which gives unreached and arc-less (t, s) pairs a tight threshold
     // before the far chunks are tested
     const int32_t c0 = PR ? (int32_t)((int64_t)vt * BW / SRS % nchunks) : 0;  // the chunk holding the tile
-    auto chunk_of = [&](int32_t j) { return PR ? (c0 + j) % nchunks : j; };
+    // spiral: c0, c0+1, c0-1, c0+2, c0-2, .. (the nearest rows on both sides of the tile
+    // first), then the longer side's remaining chunks; otherwise c0, c0+1, .. wrapping
+    const int32_t sL = c0, sR = nchunks - 1 - c0, sM = sL < sR ? sL : sR;
+    auto chunk_of = [&](int32_t j) {
+        if (!PR) return j;
+        if (!spiral) return (c0 + j) % nchunks;
+        if (j <= 2 * sM) return j == 0 ? c0 : ((j & 1) ? c0 + (j + 1) / 2 : c0 - j / 2);
+        return sR > sL ? c0 + j - sM : c0 - (j - sM);
+    };
     // PR: the vertices of this thread's rows of the chunk of order index j (perm, an
     // L2-resident 40 KB table).  Loaded one chunk ahead of the fetch that uses them, so the
     // D32 row loads never wait on a dependent perm load.
@@ -2551,6 +2559,7 @@ struct shadowtopo_engine {
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
     int32_t opt_delta_colbound = 2;    // pruned delta: per-destination chunk bounds (1), + per-chunk source masks (2)
+    int32_t opt_sweep_spiral = 0;      // pruned sweep: chunks outward from the tile on both sides (1) or upward, wrapping (0)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
@@ -2796,23 +2805,23 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac);
+                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral);
             // (4 logged rows in flight per wave instead of 2 measured the same, r03u)
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 2>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac);
+                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral);
             return hipGetLastError();
         }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                           eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac);
+                           eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, false>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32,
                        eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
     return hipGetLastError();
 }
 
@@ -4233,6 +4242,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
         const char* cb = getenv("SHADOWTOPO_DELTA_COLBOUND");  // A/B knob: 0, 1 or 2 (default)
         if (cb && cb[0] >= '0' && cb[0] <= '2') eng->opt_delta_colbound = cb[0] - '0';
+        const char* sp = getenv("SHADOWTOPO_SWEEP_SPIRAL");  // A/B knob: 0 (default) or 1
+        if (sp && (sp[0] == '0' || sp[0] == '1')) eng->opt_sweep_spiral = sp[0] - '0';
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
