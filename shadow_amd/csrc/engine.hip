@@ -848,7 +848,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        const int32_t* __restrict__ ipos,
                                                        const int32_t* __restrict__ WIp,
                                                        const double* __restrict__ WRp,
-                                                       const double* __restrict__ vfac, int32_t spiral) {
+                                                       const double* __restrict__ vfac, int32_t spiral,
+                                                       int32_t win1) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -1032,12 +1033,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     __syncthreads();
     int32_t cur_win = -1;
     unsigned long long cur_live = 0ull;
-    auto win_of = [&](int32_t j) { return j == 0 ? 0 : 1 + (j - 1) / 64; };
-    auto win_base = [&](int32_t wi) { return wi == 0 ? 0 : 1 + (wi - 1) * 64; };
+    // win1 > 0: window 1 is the win1 chunks next in the order (the tile's nearest
+    // neighbours), so the far windows are evaluated with the thresholds they left
+    const int32_t w1 = win1 > 0 && win1 < 64 ? win1 : 0;
+    auto win_of = [&](int32_t j) {
+        if (j == 0) return 0;
+        if (w1) return j <= w1 ? 1 : 2 + (j - 1 - w1) / 64;
+        return 1 + (j - 1) / 64;
+    };
+    auto win_base = [&](int32_t wi) {
+        if (wi == 0) return 0;
+        if (w1) return wi == 1 ? 1 : 1 + w1 + (wi - 2) * 64;
+        return 1 + (wi - 1) * 64;
+    };
+    auto win_size = [&](int32_t wi) { return wi == 0 ? 1 : (w1 && wi == 1 ? w1 : 64); };
     constexpr int WG = 8;  // chunks whose bounds are in flight at once in a window evaluation (4: +1 %)
     auto eval_window = [&](int32_t wi) -> unsigned long long {
         const int32_t base = win_base(wi);
-        const int32_t nw = wi == 0 ? 1 : (nchunks - base < 64 ? nchunks - base : 64);
+        const int32_t nw = nchunks - base < win_size(wi) ? nchunks - base : win_size(wi);
         unsigned long long wm = 0ull;
         for (int32_t j0 = 0; j0 < nw; j0 += WG) {
             float md[TB][WG], mw8[WG][TDT];
@@ -2560,6 +2573,7 @@ struct shadowtopo_engine {
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
     int32_t opt_delta_colbound = 2;    // pruned delta: per-destination chunk bounds (1), + per-chunk source masks (2)
     int32_t opt_sweep_spiral = 1;      // pruned sweep: chunks outward from the tile on both sides (1) or upward, wrapping (0)
+    int32_t opt_sweep_win1 = 0;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
@@ -2805,23 +2819,26 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral);
+                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
+                               eng->opt_sweep_win1);
             // (4 logged rows in flight per wave instead of 2 measured the same, r03u)
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 2>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral);
+                               eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
+                               eng->opt_sweep_win1);
             return hipGetLastError();
         }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
-                           eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral);
+                           eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
+                               eng->opt_sweep_win1);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, false>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32,
                        eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0);
     return hipGetLastError();
 }
 
@@ -4244,6 +4261,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (cb && cb[0] >= '0' && cb[0] <= '2') eng->opt_delta_colbound = cb[0] - '0';
         const char* sp = getenv("SHADOWTOPO_SWEEP_SPIRAL");  // A/B knob: 0 or 1 (default)
         if (sp && (sp[0] == '0' || sp[0] == '1')) eng->opt_sweep_spiral = sp[0] - '0';
+        const char* w1 = getenv("SHADOWTOPO_SWEEP_WIN1");  // A/B knob: 0 (default) .. 63
+        if (w1 && atoi(w1) >= 0 && atoi(w1) < 64) eng->opt_sweep_win1 = atoi(w1);
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
