@@ -2573,7 +2573,7 @@ struct shadowtopo_engine {
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
     int32_t opt_delta_colbound = 2;    // pruned delta: per-destination chunk bounds (1), + per-chunk source masks (2)
     int32_t opt_sweep_spiral = 1;      // pruned sweep: chunks outward from the tile on both sides (1) or upward, wrapping (0)
-    int32_t opt_sweep_win1 = 0;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none)
+    int32_t opt_sweep_win1 = 8;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
@@ -4261,7 +4261,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (cb && cb[0] >= '0' && cb[0] <= '2') eng->opt_delta_colbound = cb[0] - '0';
         const char* sp = getenv("SHADOWTOPO_SWEEP_SPIRAL");  // A/B knob: 0 or 1 (default)
         if (sp && (sp[0] == '0' || sp[0] == '1')) eng->opt_sweep_spiral = sp[0] - '0';
-        const char* w1 = getenv("SHADOWTOPO_SWEEP_WIN1");  // A/B knob: 0 (default) .. 63
+        const char* w1 = getenv("SHADOWTOPO_SWEEP_WIN1");  // A/B knob: 0 .. 63, 8 default
         if (w1 && atoi(w1) >= 0 && atoi(w1) < 64) eng->opt_sweep_win1 = atoi(w1);
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
