@@ -188,6 +188,22 @@ def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0):
     return roofline
 
 
+def host_build_ms(eng, r0, r1, A, steps, timed):
+    """SURVEY.md 8(d)'s matrix build time: rows [r0, r1) of the A x A latency / reliability /
+    hops matrix (and the pair kinds) delivered into page-locked host memory -- the shim's
+    buffers -- PCIe included, timed like the device steps (`timed`: barrier + synchronize on
+    both sides, max over ranks, exactly `steps` builds).  Every rank delivers its own row
+    block into the one host's memory, so at N ranks the node's host holds the whole matrix."""
+    from shadow_amd import engine as E
+    rows = r1 - r0
+    outs = [E.pinned_empty((rows, A), np.float64), E.pinned_empty((rows, A), np.float64),
+            E.pinned_empty((rows, A), np.uint32), E.pinned_empty((rows, A), np.uint8)]
+    eng.compute_rows_into(r0, r1, *outs)  # first touch of the buffers, untimed
+    el = timed(lambda: eng.compute_rows_into(r0, r1, *outs), steps)
+    del outs
+    return el / steps * 1e3
+
+
 def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, on_timed_start=None,
                 on_timed_end=None, on_first_step=None):
     """One sharded attached-pair matrix build per step: this rank's contiguous
@@ -290,6 +306,9 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
                               + (f" + RCCL all-gather ({len(ex.bounds)} chunks)" if world > 1 else ""),
                "rounds_per_step": st["rounds"] / steps,
                "roofline": roofline_of(st, g, "C4", 1.0, world, ex.rows, steps)}
+        rec["matrix_build_host_ms"] = host_build_ms(eng, ex.r0, ex.r1, A, steps, timed)
+        rec["matrix_build_host_note"] = ("rows of this rank's block delivered into page-locked host memory "
+                                         "(lat, rel, hops, kind), PCIe included, max over ranks")
         if world > 1:
             rec["allgather_ms"] = run["allgather_s"] / steps * 1e3
             rec["allgather_bytes_per_rank"] = run["allgather_bytes"]
@@ -315,10 +334,12 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
                     sst = eng.stats()
                     rf = roofline_of(sst, g, "C4", 1.0, W, z - a, steps)
                     shares.append({"rank": r, "rows": z - a, "ms": el / steps * 1e3,
+                                   "host_ms": host_build_ms(eng, a, z, A, steps, timed),
                                    "relax_ms": sst["relax_ms"] / steps, "roofline_frac": rf["frac"],
                                    "rounds": sst["rounds"] / steps})
                 slow = max(shares, key=lambda x: x["ms"])
-                proj[str(W)] = {"per_gpu_ms": slow["ms"], "ranks_timed": shares,
+                proj[str(W)] = {"per_gpu_ms": slow["ms"], "per_gpu_host_ms": max(x["host_ms"] for x in shares),
+                                "ranks_timed": shares,
                                 "allgather_bytes_per_gpu": 20 * A * A * (W - 1) // W,
                                 "note": "one rank's row share computed on this GPU; the all-gather over xGMI "
                                         "is not included (measured only by an N-GPU run)"}
@@ -392,8 +413,6 @@ def main():
     ap.add_argument("--no-shim", action="store_true",
                     help="skip the drop-in's in-process multi-GPU host-matrix build (C4 through topology_new)")
     ap.add_argument("--profile-counts", action="store_true", help="count relax visits/changes (slower)")
-    ap.add_argument("--delta-step", type=int, default=0,
-                    help="sparse: delta-stepping rounds, bucket width in 1/1000 latency units (0 = off, default)")
     ap.add_argument("--batches", type=int, default=0, help="source batches in flight (0 = auto)")
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
@@ -457,8 +476,6 @@ def main():
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
-    if args.delta_step:
-        eng.set_option(E.OPT_DELTA_STEP, args.delta_step)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0
@@ -491,6 +508,12 @@ def main():
     # roofline of the dominant kernel, timed with HIP events on the engine's stream around
     # every launch
     roofline = roofline_of(st, g, args.config, args.scale, world, rows, args.steps, args.dense_variant)
+
+    # SURVEY.md 8(d)'s matrix build time "delivered to host": the same steps with the rows
+    # landing in page-locked host memory (PCIe included), beside the device-resident figure
+    build_host_ms = None
+    if rows > 0 and not args.no_host_rate:
+        build_host_ms = host_build_ms(eng, r0, r1, A, args.steps, run["timed"])
 
     # the drop-in boundary hands host buffers over (topology_hip.c: MEM_HOST); its
     # PCIe-inclusive rate, measured once outside the timed region (never `value`)
@@ -560,6 +583,10 @@ def main():
             "data": "synthetic (SURVEY.md 8d generator, fixed seeds)",
             "config": {"workload": desc, "n_vertices": g.n, "n_edges": g.m, "n_arcs": st["n_arcs"],
                        "attached": A, "sources_per_gpu": rows, "matrix_build_ms": ms_per_step,
+                       "matrix_build_host_ms": build_host_ms,
+                       "matrix_build_note": "matrix_build_ms: rows left in HBM (the timed steps above); "
+                                            "matrix_build_host_ms: the same builds delivered into page-locked "
+                                            "host memory (lat, rel, hops, kind; PCIe included), timed the same way",
                        "parallelism": f"sources sharded x{world}" + (f" + RCCL all-gather ({chunks} chunks, overlapped)" if world > 1 else "")},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -110,12 +110,11 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               counts read back once per 8 rounds) when batches x vertices <= 4 Mi,
                                               2 = always, 0 = never (one host read-back per round). Results are
                                               identical. */
-#define SHADOWTOPO_OPT_DELTA_STEP 18      /* CSR FULL rounds over worklists: 0 (default) = ungated label-correcting rounds;
-                                            D > 0 = batched delta-stepping: a visit's changes are propagated only
-                                            when one of them is <= its batch's threshold T (the rest wait as
-                                            pending vertices), and T rises by D / 1000 latency units (at least to
-                                            the smallest pending value) whenever a batch has nothing active --
-                                            the north star's bucketed relaxation, measured slower */
+/* (18: retired -- batched delta-stepping rounds, measured slower and removed in r04) */
+#define SHADOWTOPO_OPT_DELTA_LIVE 19      /* dense delta rounds over live-chunk lists (only the chunks holding a
+                                            changed row): 2 (default) = when the previous round changed at most
+                                            1/64 of the delta batches' pairs, 1 = always, 0 = never. Results are
+                                            identical. */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (55 % of free HBM, at least 24 GB) this
                                               engine may take (default 1000); engines sharing one device split it */
 
@@ -174,11 +173,13 @@ typedef struct shadowtopo_stats {
     double create_build_ms;
     double order_ms;
     double create_alloc_ms;  /* of create_upload_ms: the device allocation of the edge buffers */
-    int64_t gated_final_releases; /* OPT_DELTA_STEP: groups whose closing release at an infinite
-                                     threshold still found pending work */
+    int64_t groups;          /* batch groups computed (a computation's rows in groups of batches in flight) */
     double prepare_ms;       /* cold start: the device preparation's own wall time (shadowtopo_prepare:
                                 HIP runtime and queue initialisation, staging buffers, code objects) */
     double create_prepare_wait_ms; /* of create_validate_ms: the part shadowtopo_create waited for it */
+    int64_t group_batches;   /* batches in flight per group of the last computation (its largest group) */
+    int64_t host_syncs;      /* host waits on the device inside the relaxation rounds (a round's counts
+                                read back before the next launch; device-driven rounds: once per block) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -60,6 +60,9 @@ int32_t topology_hip_vertex_of_ip(Topology* top, uint32_t ip);
 int32_t topology_hip_vertex_of_id(Topology* top, const char* id);
 /* packet counter of the cached path between two attached vertices */
 uint64_t topology_hip_packet_count(Topology* top, int32_t src_vertex, int32_t dst_vertex);
+/* the emulated path cache's cell of an attached pair (parity / race tooling): bit 0 set when
+ * (src, dst) is cached, bit 1 when (dst, src) is; both set would be a bug; -1 if unattached */
+int32_t topology_hip_cached_cell(Topology* top, int32_t src_vertex, int32_t dst_vertex);
 /* the parsed graph (for parity tooling): edge list + latency/packetloss, vertex loss (NaN
  * absent); arrays owned by the topology, valid until topology_free */
 int topology_hip_edges(Topology* top, const int32_t** src, const int32_t** dst, const double** latency,

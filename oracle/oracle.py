@@ -56,6 +56,9 @@ def lib():
         L.og_pair_rows.restype = ctypes.c_int
         L.og_pair_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint32, _i32p, ctypes.c_int32, ctypes.c_int32,
                                    ctypes.c_int32, _f64p, _f64p, _u32p, _u8p, ctypes.c_int]
+        L.og_pair_rows_list.restype = ctypes.c_int
+        L.og_pair_rows_list.argtypes = [ctypes.c_void_p, ctypes.c_uint32, _i32p, ctypes.c_int32, _i32p,
+                                        ctypes.c_int32, _f64p, _f64p, _u32p, _u8p, ctypes.c_int]
         L.og_tie_vertices.argtypes = [ctypes.c_void_p, ctypes.c_int32, _f64p, _u8p]
         L.og_self_path.restype = ctypes.c_int
         L.og_self_path.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
@@ -134,6 +137,19 @@ class OracleGraph:
         hops = np.empty(R * A, np.uint32)
         kind = np.empty(R * A, np.uint8)
         fails = lib().og_pair_rows(self._h, int(flags), att, A, row_begin, row_end, lat, rel, hops, kind, nthreads)
+        return (lat.reshape(R, A), rel.reshape(R, A), hops.reshape(R, A), kind.reshape(R, A), fails)
+
+    def pair_rows_list(self, flags, attached, rows, nthreads=1):
+        """pair_rows for an arbitrary list of source rows (output row q = rows[q])"""
+        att = np.ascontiguousarray(attached, dtype=np.int32)
+        rw = np.ascontiguousarray(rows, dtype=np.int32)
+        A, R = len(att), len(rw)
+        assert ((rw >= 0) & (rw < A)).all()
+        lat = np.empty(R * A, np.float64)
+        rel = np.empty(R * A, np.float64)
+        hops = np.empty(R * A, np.uint32)
+        kind = np.empty(R * A, np.uint8)
+        fails = lib().og_pair_rows_list(self._h, int(flags), att, A, rw, R, lat, rel, hops, kind, nthreads)
         return (lat.reshape(R, A), rel.reshape(R, A), hops.reshape(R, A), kind.reshape(R, A), fails)
 
     def tie_vertices(self, source, dist):

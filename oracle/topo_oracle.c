@@ -426,8 +426,10 @@ int og_direct_path(const og* g, int32_t s, int32_t t, double* lat_out, double* r
  * kind[i*A+j]: 0 = failure, 1 = direct, 2 = self rule, 3 = dijkstra.
  * Sources [row_begin,row_end) only; nthreads > 1 uses OpenMP over sources.
  */
-int og_pair_rows(const og* g, uint32_t flags, const int32_t* attached, int32_t A, int32_t row_begin, int32_t row_end,
-                 double* lat, double* rel, uint32_t* hops, uint8_t* kind, int nthreads) {
+/* rows[q] (or row_begin + q when rows is NULL) for q < nrows, into output row q */
+static int pair_rows_impl(const og* g, uint32_t flags, const int32_t* attached, int32_t A, const int32_t* rows,
+                          int32_t row_begin, int32_t nrows, double* lat, double* rel, uint32_t* hops, uint8_t* kind,
+                          int nthreads) {
     int complete = (flags & OG_COMPLETE) != 0;
     int prefer = (flags & OG_PREFER_DIRECT) != 0;
     int self_loop_rule = (flags & OG_SELF_DIJKSTRA_LOOP) != 0;
@@ -443,12 +445,13 @@ int og_pair_rows(const og* g, uint32_t flags, const int32_t* attached, int32_t A
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 1)
 #endif
-        for (int32_t i = row_begin; i < row_end; i++) {
+        for (int32_t q = 0; q < nrows; q++) {
+            const int32_t i = rows ? rows[q] : row_begin + q;
             int32_t s = attached[i];
             int have_sssp = 0;
             for (int32_t j = 0; j < A; j++) {
                 int32_t t = attached[j];
-                size_t o = (size_t)(i - row_begin) * (size_t)A + (size_t)j;
+                size_t o = (size_t)q * (size_t)A + (size_t)j;
                 double l = -1.0, r = -1.0;
                 uint32_t h = 0;
                 uint8_t k = 0;
@@ -490,6 +493,17 @@ int og_pair_rows(const og* g, uint32_t flags, const int32_t* attached, int32_t A
         free(path);
     }
     return failures;
+}
+
+int og_pair_rows(const og* g, uint32_t flags, const int32_t* attached, int32_t A, int32_t row_begin, int32_t row_end,
+                 double* lat, double* rel, uint32_t* hops, uint8_t* kind, int nthreads) {
+    return pair_rows_impl(g, flags, attached, A, NULL, row_begin, row_end - row_begin, lat, rel, hops, kind, nthreads);
+}
+
+/* the same for an arbitrary list of rows (parity samples spread over a large matrix) */
+int og_pair_rows_list(const og* g, uint32_t flags, const int32_t* attached, int32_t A, const int32_t* rows,
+                      int32_t nrows, double* lat, double* rel, uint32_t* hops, uint8_t* kind, int nthreads) {
+    return pair_rows_impl(g, flags, attached, A, rows, 0, nrows, lat, rel, hops, kind, nthreads);
 }
 
 /*

@@ -116,13 +116,6 @@ struct Pools {
     double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
     unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
     float* D32;         // dense mode: [slot][Vp][64] f32 filter key (distance rounded down, NaN unreached)
-    // OPT_DELTA_STEP (delta-stepping rounds, off by default): per batch the threshold and a
-    // "something is pending" flag, per (vertex, batch) a pending flag and the smallest
-    // distance whose propagation waits for the threshold
-    double* Tb;         // [slot]
-    int32_t* pflag;     // [slot]
-    uint8_t* pend;      // [slot][Vp]
-    double* pmin;       // [slot][Vp]
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -142,10 +135,6 @@ struct BatchDev {
     unsigned long long* chm0;
     unsigned long long* chm1;
     gfloat* D32;
-    const double* Tb;   // OPT_DELTA_STEP (else null): this batch's threshold, pending flags
-    int32_t* pflag;
-    gbyte* pend;
-    gdouble* pmin;
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
     __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
@@ -166,10 +155,6 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.chm0 = p.chm ? p.chm + (size_t)b * 2 * p.Vp : nullptr;
     B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
     B.D32 = p.D32 ? (gfloat*)(p.D32 + o) : nullptr;
-    B.Tb = p.Tb ? p.Tb + b : nullptr;
-    B.pflag = p.pflag ? p.pflag + b : nullptr;
-    B.pend = p.pend ? (gbyte*)(p.pend + (size_t)b * p.Vp) : nullptr;
-    B.pmin = p.pmin ? (gdouble*)(p.pmin + (size_t)b * p.Vp) : nullptr;
     return B;
 }
 
@@ -360,8 +345,6 @@ __device__ __forceinline__ void relax_arc(double du, double w, int32_t e, int32_
 // Grid: 1-D, remapped so that all blocks sharing an XCD (blockIdx % 8) work on the same
 // batch (its [V][64] state then stays in that XCD's L2).  Placement is a speed hint only.
 // one visit of destination v in batch b (the body of k_relax / k_relax_wl)
-template <bool G = false>  // G: OPT_DELTA_STEP's gated propagation (a separate instantiation: the
-                           // default rounds carry none of its registers)
 __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                             const double* __restrict__ in_w, const double* __restrict__ in_r,
                                             const int64_t* __restrict__ out_ptr, const int32_t* __restrict__ out_dst,
@@ -400,30 +383,8 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
     bool ch = false;
     if (be >= 0 && sv >= 0 && sv != v) ch = finish_vertex(B, lane, v, be, bu, bc, bdu, tie, in_r, curD, curH, curR, curP);
     if (__ballot(ch)) {
-        bool go = true;
-        if constexpr (G) {
-            // OPT_DELTA_STEP: propagate now only if a changed lane's new distance is within the
-            // batch's threshold; otherwise v waits as pending (its values are written already)
-            // (one wave vote: `go` must be wave-uniform -- the lanes share the out-list walk)
-            const double T = *B.Tb;
-            go = __ballot(ch && bc <= T) != 0ull;
-            if (!go) {
-                double dm = dinf();  // the smallest changed distance, all of them above T
-                for (unsigned long long m = __ballot(ch); m; m &= m - 1) {
-                    const double x = readlane_d(bc, __builtin_ctzll(m));
-                    dm = x < dm ? x : dm;
-                }
-                if (lane == 0) {
-                    B.pend[v] = 1;
-                    const double pm = B.pmin[v];
-                    B.pmin[v] = dm < pm ? dm : pm;
-                    *B.pflag = 1;
-                }
-            }
-        }
         gbyte* act_nxt = B.act(parity ^ 1);
-        if (go)
-            for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
         if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
         if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
     }
@@ -431,7 +392,6 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
 }
 
 // one wave per (destination, batch) of the whole grid; inactive pairs exit after their flag
-template <bool G = false>
 __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                const int64_t* __restrict__ out_ptr,
@@ -448,7 +408,7 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
     gbyte* act_cur = B.act(parity);
     if (act_cur[v] == 0) return;
     if (lane == 0) act_cur[v] = 0;
-    relax_visit<G>(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+    relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
 }
 
 // Frontier worklists (default for sparse graphs): the active destinations of each batch for
@@ -502,30 +462,6 @@ __global__ __launch_bounds__(256) void k_compact(Pools pools, int32_t V, int32_t
     }
 }
 
-// OPT_DELTA_STEP: release the pending vertices of every batch whose threshold now covers
-// them (activate their out-neighbours for the next round), and flag the batches that keep
-// pending ones; pnext[b] gets the smallest value still pending (u64 bits of a positive double)
-__global__ __launch_bounds__(256) void k_release(Pools pools, int32_t V, int32_t parity_next,
-                                                 const int64_t* __restrict__ out_ptr,
-                                                 const int32_t* __restrict__ out_dst,
-                                                 unsigned long long* __restrict__ pnext) {
-    const BatchDev B = batch_view(pools, blockIdx.y);
-    const double T = *B.Tb;
-    gbyte* act_nxt = B.act(parity_next);
-    for (int32_t v = blockIdx.x * 256 + threadIdx.x; v < V; v += gridDim.x * 256) {
-        if (!B.pend[v]) continue;
-        const double pm = B.pmin[v];
-        if (pm <= T) {
-            B.pend[v] = 0;
-            B.pmin[v] = dinf();
-            for (int64_t x = out_ptr[v]; x < out_ptr[v + 1]; ++x) act_nxt[out_dst[x]] = 1;
-        } else {
-            *B.pflag = 1;
-            atomicMin(&pnext[blockIdx.y], (unsigned long long)__double_as_longlong(pm));
-        }
-    }
-}
-
 // batch of worklist item i: the last b with prefix[b] <= i (prefix non-decreasing) -- one
 // coalesced load of the prefix per 64 batches and a wave ballot, instead of a binary search
 // of dependent loads
@@ -541,7 +477,6 @@ __device__ __forceinline__ int32_t wl_batch(const int64_t* __restrict__ prefix, 
 // one wave per listed (vertex, batch): the T items of all batches in batch-major order
 // (prefix[b] = items before batch b), XCD x (block % 8) takes the contiguous slice
 // [x*S, (x+1)*S) -- a batch's state stays in one XCD's L2, as with xcd_tile
-template <bool G = false>
 __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                   const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                   const int64_t* __restrict__ out_ptr,
@@ -560,7 +495,7 @@ __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in
     // SGPRs, as in k_relax, instead of occupying VGPRs (84 -> occupancy 5 of 8)
     const int32_t v = __builtin_amdgcn_readfirstlane(wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x);
     const BatchDev B = batch_view(pools, b);
-    relax_visit<G>(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+    relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
     // cleared after the visit (this round sets only the other parity's flags): a store ahead
     // of the arc-list loads would keep them off the scalar unit (they could alias it)
     if (lane == 0) B.act(parity)[v] = 0;
@@ -815,18 +750,6 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 //  * rows where any lane passes are collected and, at the end of the chunk, re-evaluated
 //    exactly in f64 (D and W from global memory) in row order -- the same lexicographic
 //    minimum and tie flag as a sequential scan.
-#ifdef SHADOWTOPO_PHASE_STAMPS
-// diagnostic build only (-DSHADOWTOPO_PHASE_STAMPS, _exp/build_variant.sh; never in the
-// product library): per-block wall-clock stamps (s_memrealtime, 100 MHz) of the dense
-// sweep's phases and its counts, read by shadowtopo_exp_phase (_exp/r03_phase.py)
-constexpr int PHASE_BLOCKS = 16384;
-__device__ unsigned long long g_phase[PHASE_BLOCKS][8];
-#define PHASE_STAMP(slot_) do { if (threadIdx.x == 0 && blockIdx.x < PHASE_BLOCKS) g_phase[blockIdx.x][slot_] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define PHASE_SET(slot_, val_) do { if (threadIdx.x == 0 && blockIdx.x < PHASE_BLOCKS) g_phase[blockIdx.x][slot_] = (val_); } while (0)
-#else
-#define PHASE_STAMP(slot_) do { } while (0)
-#define PHASE_SET(slot_, val_) do { } while (0)
-#endif
 constexpr int SRS = 32;  // rows per LDS chunk
 constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FTDT; 4 was slower: 4.63 vs 3.8 ms on C2)
 
@@ -882,7 +805,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     if (first < 0) return;
     const int32_t vb = vt * BW;
     if (vb >= V) return;
-    PHASE_STAMP(0);
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int32_t v0 = vb + wave * TDT;
@@ -1104,7 +1026,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         }
         return -1;
     };
-    PHASE_STAMP(1);
     // chunks in flight: itc (in LDS, filtered this iteration), itn (its loads issued this
     // iteration, staged at its end) and itn2 (its rows' perm entries loaded this iteration)
     int32_t prow_n[DQ];
@@ -1119,14 +1040,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     if (itn >= 0) perm_of(itn, prow_n);
     __syncthreads();
     int bufc = 0;
-#ifdef SHADOWTOPO_PHASE_STAMPS
-    int32_t nvisit = 0;
-    uint32_t nhit = 0;
-#endif
     while (itc >= 0) {
-#ifdef SHADOWTOPO_PHASE_STAMPS
-        ++nvisit;
-#endif
         const int32_t c = chunk_of(itc);
         const int32_t u0 = c * SRS;
         const int cur = bufc;
@@ -1158,11 +1072,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         for (int k = 0; k < TB; ++k) hits[k] = 0;
         // PH 1 (the chunk loop alone has VGPRs to spare): each row's LDS reads are issued one
         // row ahead, so they are in flight while the previous row is filtered and votes
-#ifdef SHADOWTOPO_EXP_NO_ROW_AHEAD
-        constexpr bool RP = false;  // A/B build
-#else
         constexpr bool RP = PH == 1 && NW == 4;
-#endif
         f4 wn[TDT / 4];
         float dn[TB];
         auto lds_row = [&](int r) {
@@ -1235,9 +1145,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
 #pragma unroll
             for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + (u0 / SRS)] = hits[k];
         }
-#ifdef SHADOWTOPO_PHASE_STAMPS
-        nhit += __popc(hits[0]);
-#endif
         if (more) {
             stash(cur ^ 1);
             advance();
@@ -1247,9 +1154,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         itc = itn;
         itn = itn2;
     }
-    PHASE_STAMP(2);
-    PHASE_SET(5, nvisit);
-    PHASE_SET(6, nhit);
     }  // PH != 2
     if constexpr (PH == 1) return;
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
@@ -1307,7 +1211,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
             }
         }
     }
-    PHASE_STAMP(3);
     if (v0 < V) {
 #pragma unroll
         for (int k = 0; k < TB; ++k)
@@ -1324,14 +1227,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                     cnt, b0 + k, vid, sr);
             }
     }
-    PHASE_STAMP(4);
-#ifdef SHADOWTOPO_PHASE_STAMPS
-    {
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        PHASE_SET(7, ((unsigned long long)(xcc & 0xf) << 32) | (uint32_t)grp);
-    }
-#endif
 }
 
 // Pruned full sweep (k_relax_dense_f<.., PR = true>) inputs.
@@ -2566,8 +2461,6 @@ struct shadowtopo_engine {
     bool floor_ok = false;             // default_nb: the 24 GB budget floor was found free once
     size_t pool_bytes = 0;             // device bytes the batch pools hold (ensure_batches)
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
-    double opt_delta_step = 0.0;       // OPT_DELTA_STEP: bucket width (latency units), 0 = off
-    unsigned long long* d_pnext = nullptr;  // OPT_DELTA_STEP: [nb] smallest still-pending value
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
@@ -2642,7 +2535,6 @@ void free_batches(shadowtopo_engine* eng) {
     eng->d_wlpre = nullptr;
     eng->d_live = nullptr;
     eng->d_nlive = nullptr;
-    eng->d_pnext = nullptr;
     eng->h_srcv.clear();
     eng->h_row.clear();
     eng->nb_cap = 0;
@@ -2967,6 +2859,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             HIP_TRY(hipMemcpyAsync(eng->h_tlog + r0, eng->d_tlog + r0, sizeof(int64_t) * (DEV_K + 1),
                                    hipMemcpyDeviceToHost, s));
             HIP_TRY(round_sync(eng, s));
+            eng->st.host_syncs++;
             bool done = false;
             for (int64_t round = r0; round < r0 + DEV_K; ++round) {
                 const int64_t T = eng->h_tlog[round];
@@ -2991,33 +2884,6 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             if (done) break;
         }
     } else {
-    // OPT_DELTA_STEP (sparse worklist rounds only): the pending state, thresholds at one step
-    const bool gated = use_wl && eng->opt_delta_step > 0.0;
-    std::vector<double> Th;
-    std::vector<int32_t> pf;
-    std::vector<unsigned long long> pn;
-    bool gated_final = false;
-    if (gated) {
-        Pools& P = eng->pools;
-        if (!P.pend) {
-            int rc2;
-            const size_t nb = (size_t)eng->nb_cap;
-            if ((rc2 = dev_alloc(eng->batch_allocs, (void**)&P.Tb, sizeof(double) * nb)) ||
-                (rc2 = dev_alloc(eng->batch_allocs, (void**)&P.pflag, sizeof(int32_t) * nb)) ||
-                (rc2 = dev_alloc(eng->batch_allocs, (void**)&P.pend, (size_t)eng->Vp * nb)) ||
-                (rc2 = dev_alloc(eng->batch_allocs, (void**)&P.pmin, sizeof(double) * eng->Vp * nb)) ||
-                (rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_pnext, sizeof(unsigned long long) * nb)))
-                return rc2;
-        }
-        Th.assign((size_t)nbg, eng->opt_delta_step);
-        pf.assign((size_t)nbg, 0);
-        pn.assign((size_t)nbg, 0);
-        HIP_TRY(hipMemsetAsync(P.pend, 0, (size_t)eng->Vp * nbg, s));
-        HIP_TRY(hipMemsetAsync(P.pmin, 0x7f, sizeof(double) * eng->Vp * nbg, s));  // ~1.4e306: none
-        HIP_TRY(hipMemsetAsync(P.pflag, 0, sizeof(int32_t) * nbg, s));
-        HIP_TRY(hipMemsetAsync(eng->d_pnext, 0xff, sizeof(unsigned long long) * nbg, s));
-        HIP_TRY(hipMemcpyAsync(P.Tb, Th.data(), sizeof(double) * nbg, hipMemcpyHostToDevice, s));
-    }
     if (use_wl) {
         HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
         hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, 0, eng->d_wl,
@@ -3025,67 +2891,17 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
         HIP_TRY(round_sync(eng, s));
+        eng->st.host_syncs++;
     }
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
         int64_t wl_total = 0;
-        if (gated) {
-            // a batch with nothing active but vertices pending raises its threshold (by one
-            // step, at least to its smallest pending value) and releases them; repeat until
-            // every batch has work or nothing pending
-            for (;;) {
-                HIP_TRY(hipMemcpyAsync(pf.data(), eng->pools.pflag, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipMemcpyAsync(pn.data(), eng->d_pnext, sizeof(unsigned long long) * nbg, hipMemcpyDeviceToHost, s));
-                HIP_TRY(round_sync(eng, s));
-                bool raise = false;
-                for (int32_t b = 0; b < nbg; ++b)
-                    if (eng->h_wlcnt[b] == 0 && pf[b]) {
-                        double nx = Th[b] + eng->opt_delta_step;
-                        double pm;
-                        memcpy(&pm, &pn[b], sizeof pm);
-                        if (pn[b] != ~0ull && pm > nx) nx = pm;
-                        Th[b] = nx;
-                        raise = true;
-                    }
-                if (!raise) break;
-                HIP_TRY(hipMemcpyAsync(eng->pools.Tb, Th.data(), sizeof(double) * nbg, hipMemcpyHostToDevice, s));
-                HIP_TRY(hipMemsetAsync(eng->pools.pflag, 0, sizeof(int32_t) * nbg, s));
-                HIP_TRY(hipMemsetAsync(eng->d_pnext, 0xff, sizeof(unsigned long long) * nbg, s));
-                hipLaunchKernelGGL(k_release, dim3((uint32_t)std::min<int64_t>((V + 255) / 256, 1024), nbg), dim3(256), 0,
-                                   s, eng->pools, V, (int32_t)(round & 1), g.out_ptr, g.out_dst, eng->d_pnext);
-                HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
-                hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
-                                   (int32_t)(round & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);
-                HIP_TRY(hipGetLastError());
-                HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
-            }
-        }
         if (use_wl) {
             eng->h_wlpre[0] = 0;
             for (int32_t b = 0; b < nbg; ++b) eng->h_wlpre[b + 1] = eng->h_wlpre[b] + eng->h_wlcnt[b];
             wl_total = eng->h_wlpre[nbg];
-            if (wl_total == 0 && gated && !gated_final) {
-                // nothing active or flagged pending: release whatever is still pending at an
-                // infinite threshold once, and go on if that activated anything
-                gated_final = true;
-                for (int32_t b = 0; b < nbg; ++b) Th[b] = dinf_host();
-                HIP_TRY(hipMemcpyAsync(eng->pools.Tb, Th.data(), sizeof(double) * nbg, hipMemcpyHostToDevice, s));
-                HIP_TRY(hipMemsetAsync(eng->pools.pflag, 0, sizeof(int32_t) * nbg, s));
-                HIP_TRY(hipMemsetAsync(eng->d_pnext, 0xff, sizeof(unsigned long long) * nbg, s));
-                hipLaunchKernelGGL(k_release, dim3((uint32_t)std::min<int64_t>((V + 255) / 256, 1024), nbg), dim3(256), 0,
-                                   s, eng->pools, V, (int32_t)(round & 1), g.out_ptr, g.out_dst, eng->d_pnext);
-                HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
-                hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
-                                   (int32_t)(round & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);
-                HIP_TRY(hipGetLastError());
-                HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
-                HIP_TRY(round_sync(eng, s));
-                for (int32_t b = 0; b < nbg; ++b) eng->h_wlpre[b + 1] = eng->h_wlpre[b] + eng->h_wlcnt[b];
-                wl_total = eng->h_wlpre[nbg];
-                if (wl_total > 0) eng->st.gated_final_releases++;
-            }
-            if (wl_total == 0) break;  // nothing active (and, gated, nothing pending): converged
+            if (wl_total == 0) break;  // nothing active: converged
         }
         // worklist only where it pays: a mostly-active round runs the plain grid
         const bool round_wl = use_wl && (eng->opt_worklist == 2 || wl_total * 2 < (int64_t)nbg * V);
@@ -3188,24 +3004,14 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             eng->st.relax_batches += nbg;
             eng->st.wl_launches++;
             const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
-            if (gated)
-                hipLaunchKernelGGL(k_relax_wl<true>, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src,
-                                   g.in_w, g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
-                                   eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
-            else
-                hipLaunchKernelGGL(k_relax_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
-                                   g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
-                                   eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
+            hipLaunchKernelGGL(k_relax_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                               g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
+                               eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else {
             eng->st.relax_batches += nbg;
-            if (gated)
-                hipLaunchKernelGGL(k_relax<true>, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
-                                   g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
-                                   eng->d_prof);
-            else
-                hipLaunchKernelGGL(k_relax, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
-                                   g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
-                                   eng->d_prof);
+            hipLaunchKernelGGL(k_relax, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
+                               g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
+                               eng->d_prof);
         }
         HIP_TRY(hipGetLastError());
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev1, s));
@@ -3218,6 +3024,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         }
         HIP_TRY(hipMemcpyAsync(eng->h_cnt, cnt_cur, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
         HIP_TRY(round_sync(eng, s));
+        eng->st.host_syncs++;
         eng->st.relax_launches++;
         eng->st.rounds++;
         if (eng->opt_timing) {
@@ -3253,9 +3060,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     (long long)changed, ms);
         }
         if (eng->dense && eng->opt_profile) eng->st.changes += changed;  // changed (vertex, source) pairs
-        // (gated rounds end only when nothing is active or pending: a round that changed
-        // nothing may still leave pending vertices for a higher threshold)
-        if (changed == 0 && !gated) break;
+        if (changed == 0) break;
     }
     }  // host-driven rounds
     if (eng->d_prof) {
@@ -3781,6 +3586,8 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         }
         eng->st.sources += r1 - r0;
         eng->st.batches += nbg;
+        eng->st.groups++;
+        eng->st.group_batches = std::max<int64_t>(gidx == 0 ? 0 : eng->st.group_batches, nbg);
     }
     if (pinned_out) HIP_TRY(hipStreamSynchronize(eng->copy_stream));
     return SHADOWTOPO_OK;
@@ -3811,13 +3618,6 @@ int ensure_mirrors(shadowtopo_engine* eng) {
 }  // namespace
 
 extern "C" {
-#ifdef SHADOWTOPO_PHASE_STAMPS
-int shadowtopo_exp_phase(unsigned long long* out, int nblocks) {
-    if (nblocks > PHASE_BLOCKS) nblocks = PHASE_BLOCKS;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * (size_t)nblocks) ==
-                   hipSuccess ? nblocks : -1;
-}
-#endif
 
 int shadowtopo_device_count(void) {
     int n = 0;
@@ -3940,8 +3740,10 @@ hipError_t upload_staged(int device, const std::vector<UploadPart>& parts) {
     constexpr size_t CH = StagingRing::CH;
     constexpr int NB = StagingRing::NB;
     int W = 2;
+#ifdef SHADOWTOPO_EXPERIMENTS
     if (const char* f = getenv("SHADOWTOPO_UPLOAD_FILLERS"))  // A/B knob
         if (atoi(f) >= 1 && atoi(f) <= NB) W = atoi(f);
+#endif
     const bool tr = getenv("SHADOWTOPO_TRACE_BUILD") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     GB_TRY_HIP(ring_ensure(R, device));
@@ -4251,10 +4053,10 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         return fail(SHADOWTOPO_EDEVICE, "stream/event create failed");
     }
     {
-        const char* tr = getenv("SHADOWTOPO_TRACE_ROUNDS");
+        const char* tr = getenv("SHADOWTOPO_TRACE_ROUNDS");  // diagnostics: one stderr line per round
         eng->trace_rounds = tr && tr[0] == '1';
-        const char* dl = getenv("SHADOWTOPO_DELTA_LIVE");  // A/B knob: 0, 1 or 2 (default)
-        if (dl && dl[0] >= '0' && dl[0] <= '2') eng->opt_delta_live = dl[0] - '0';
+#ifdef SHADOWTOPO_EXPERIMENTS
+        // A/B knobs of the experiments build (_exp/build_variant.sh), never read by the product
         const char* dd = getenv("SHADOWTOPO_DELTA_LIVE_DIV");
         if (dd && atoi(dd) > 0) eng->opt_delta_live_div = atoi(dd);
         const char* cb = getenv("SHADOWTOPO_DELTA_COLBOUND");  // A/B knob: 0, 1 or 2 (default)
@@ -4267,6 +4069,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
+#endif
     }
     eng->st.create_build_ms = ms_since(t_phase);
     if (getenv("SHADOWTOPO_TRACE_BUILD")) fprintf(stderr, "[create] build total %.2f ms\n", eng->st.create_build_ms);
@@ -4426,9 +4229,9 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
                 return fail(SHADOWTOPO_EINVAL, "grid x limit must be a multiple of 8 in [8, 2^23]");
             eng->opt_grid_x = value;
             return SHADOWTOPO_OK;
-        case SHADOWTOPO_OPT_DELTA_STEP:
-            if (value < 0) return fail(SHADOWTOPO_EINVAL, "delta step must be >= 0");
-            eng->opt_delta_step = (double)value / 1000.0;
+        case SHADOWTOPO_OPT_DELTA_LIVE:
+            if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "delta live must be 0, 1 or 2");
+            eng->opt_delta_live = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_WORKLIST:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "worklist must be 0, 1 or 2");

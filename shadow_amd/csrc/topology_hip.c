@@ -166,9 +166,13 @@ typedef struct matrix {
     double* rel;
     uint8_t* kind;
     /* undirected late attach: rows [0, partial) hold the reverse-direction entries in
-     * columns >= partial until an old source's own row is needed (fill_old_rows rewrites
-     * them in place, then stores 0 here with release order) */
+     * columns >= fill_col until an old source's own row is needed (fill_old_rows rewrites
+     * columns [fill_col, A) of those rows in place, then stores 0 here with release order).
+     * fill_col = partial after one late attach; after several without a fill in between it
+     * is the first unfilled column of the oldest unfilled matrix (those rows were copied
+     * from it, reverse copies included) */
     _Atomic int32_t partial;
+    int32_t fill_col;
     struct matrix* next; /* retired matrices (readers may still hold them) */
 } matrix;
 
@@ -1508,6 +1512,8 @@ static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A,
             m->kind[o] = m->kind[r];
         }
     }
+    /* an old matrix that was never filled passes its reverse copies on */
+    m->fill_col = (A0 > 0 && atomic_load_explicit(&old->partial, memory_order_acquire) > 0) ? old->fill_col : A0;
     atomic_store_explicit(&m->partial, A0, memory_order_release);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
@@ -1583,8 +1589,10 @@ static int fill_old_rows(Topology* top, matrix* m) {
             struct timespec t0, t1;
             clock_gettime(CLOCK_MONOTONIC, &t0);
             if (ensure_engine(top) == 0 && compute_rows_sharded(top, att, A, 0, P, &tmp) == 0) {
+                /* columns [fill_col, P) of rows [fill_col, P) are own entries already: the
+                 * rewrite stores the same values there */
                 for (int32_t i = 0; i < P; i++)
-                    for (int32_t t = P; t < A; t++) {
+                    for (int32_t t = m->fill_col; t < A; t++) {
                         const size_t o = (size_t)i * (size_t)A + (size_t)t;
                         cell_d_store(&m->lat[o], tmp.lat[o]);
                         cell_d_store(&m->rel[o], tmp.rel[o]);
@@ -1707,11 +1715,11 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
      * late attach's columns is swapped for the current one (filled before any of those
      * entries was cached) or filled now (an entry cached before the late attach) */
     int32_t p = atomic_load_explicit(&m->partial, memory_order_acquire);
-    if (*si < p && *sj >= p) {
+    if (*si < p && *sj >= m->fill_col) {
         matrix* cur = atomic_load_explicit(&top->mat, memory_order_acquire);
         if (cur && cur->A > (*si > *sj ? *si : *sj)) *mp = m = cur;
         p = atomic_load_explicit(&m->partial, memory_order_acquire);
-        if (*si < p && *sj >= p && fill_old_rows(top, m)) return -1;
+        if (*si < p && *sj >= m->fill_col && fill_old_rows(top, m)) return -1;
     }
     return 0;
 }
@@ -1878,6 +1886,18 @@ uint64_t topology_hip_packet_count(Topology* top, int32_t src_vertex, int32_t ds
     if (i < 0 || j < 0) return 0;
     uint64_t c = counter_peek(top, i, j);
     return c ? c - 1 : 0;
+}
+
+int32_t topology_hip_cached_cell(Topology* top, int32_t src_vertex, int32_t dst_vertex) {
+    if (!top || src_vertex < 0 || dst_vertex < 0 || src_vertex >= top->V || dst_vertex >= top->V) return -1;
+    int32_t i = atomic_load(&top->att_index[src_vertex]), j = atomic_load(&top->att_index[dst_vertex]);
+    if (i < 0 || j < 0) return -1;
+    int sh;
+    const int32_t a = i < j ? i : j, b = i < j ? j : i;
+    _Atomic uint64_t* w = cell_word(top, a, b, 0, &sh);
+    const unsigned c = w ? (unsigned)((atomic_load_explicit(w, memory_order_acquire) >> sh) & 3u) : 0u;
+    if (i <= j) return (int32_t)c;
+    return (int32_t)(((c & 1u) << 1) | ((c >> 1) & 1u)); /* bit 0 = (src, dst) */
 }
 
 int topology_hip_edges(Topology* top, const int32_t** src, const int32_t** dst, const double** latency,

@@ -48,7 +48,7 @@ OPT_WORKLIST = 14
 OPT_GRID_X = 15
 OPT_PRUNE_PENDANT = 16
 OPT_DEVICE_ROUNDS = 17
-OPT_DELTA_STEP = 18  # delta-stepping rounds, bucket width in 1/1000 latency units (0 = off)
+OPT_DELTA_LIVE = 19  # dense delta rounds over live-chunk lists: 2 when sparse (default), 1 always, 0 never
 CSR_FULL = 1  # recompute every active vertex over all in-arcs (k_relax / k_relax_wl: the only sparse family)
 
 # every symbol include/shadowtopo.h declares
@@ -81,8 +81,9 @@ class Stats(ctypes.Structure):
         ("pruned_vertices", ctypes.c_int64), ("pool_allocs", ctypes.c_int64), ("pool_alloc_ms", ctypes.c_double),
         ("create_validate_ms", ctypes.c_double), ("create_upload_ms", ctypes.c_double),
         ("create_build_ms", ctypes.c_double), ("order_ms", ctypes.c_double),
-        ("create_alloc_ms", ctypes.c_double), ("gated_final_releases", ctypes.c_int64),
+        ("create_alloc_ms", ctypes.c_double), ("groups", ctypes.c_int64),
         ("prepare_ms", ctypes.c_double), ("create_prepare_wait_ms", ctypes.c_double),
+        ("group_batches", ctypes.c_int64), ("host_syncs", ctypes.c_int64),
     ]
 
     def as_dict(self):

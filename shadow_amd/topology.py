@@ -23,7 +23,7 @@ TOPOLOGY_SYMBOLS = (
 EXT_SYMBOLS = (
     "topology_hip_set_device", "topology_hip_set_devices", "topology_hip_set_self_rule", "topology_hip_prepare", "topology_hip_get_info",
     "topology_hip_attached", "topology_hip_vertex_of_ip", "topology_hip_vertex_of_id", "topology_hip_packet_count",
-    "topology_hip_edges", "shadowtopo_address_new", "shadowtopo_address_free", "shadowtopo_random_new",
+    "topology_hip_cached_cell", "topology_hip_edges", "shadowtopo_address_new", "shadowtopo_address_free", "shadowtopo_random_new",
     "shadowtopo_random_free", "shadowtopo_last_min_time_jump", "shadowtopo_set_log_level",
 )
 
@@ -79,6 +79,8 @@ def lib():
         L.topology_hip_vertex_of_id.argtypes = [vp, cp]
         L.topology_hip_packet_count.restype = ctypes.c_uint64
         L.topology_hip_packet_count.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+        L.topology_hip_cached_cell.restype = ctypes.c_int32
+        L.topology_hip_cached_cell.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.topology_hip_edges.argtypes = [vp] + [ctypes.POINTER(vp)] * 5
         L.shadowtopo_address_new.restype = vp
         L.shadowtopo_address_new.argtypes = [cp, cp]
@@ -211,6 +213,10 @@ class Topology:
 
     def packet_count(self, src_vertex: int, dst_vertex: int) -> int:
         return int(lib().topology_hip_packet_count(self._h, src_vertex, dst_vertex))
+
+    def cached_cell(self, src_vertex: int, dst_vertex: int) -> int:
+        """bit 0: (src, dst) cached; bit 1: (dst, src) cached; -1: not attached"""
+        return int(lib().topology_hip_cached_cell(self._h, src_vertex, dst_vertex))
 
     def edges(self):
         """(src, dst, latency, packetloss, vertex_packetloss) numpy copies of the parsed graph"""

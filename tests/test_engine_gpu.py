@@ -32,17 +32,6 @@ def test_more_than_one_batch_group():
     compare(g, batches_in_flight=2)
 
 
-@pytest.mark.parametrize("delta", [500, 5000, 50000])
-def test_delta_stepping_rounds_same_results(delta):
-    """OPT_DELTA_STEP (the north star's bucketed relaxation: propagation gated by a per-batch
-    threshold, pending vertices released as it rises) reaches the same fixed point; several
-    batch groups, ties (integer latencies: the replay path), device-driven rounds off"""
-    g = synth.random_sparse(V=500, avg_deg=4, seed=21)
-    compare(g, delta_step=delta, device_rounds=0, batches_in_flight=3)
-    gi = synth.random_sparse(V=300, avg_deg=5, seed=22, int_lat=True)
-    compare(gi, delta_step=delta, device_rounds=0)
-
-
 def test_directed():
     g = synth.random_sparse(V=300, avg_deg=4, seed=5, directed=True)
     compare(g)
@@ -418,11 +407,10 @@ def test_row_exchange_with_engine_device_rows():
 
 @pytest.mark.parametrize("live", ["0", "1"])
 @pytest.mark.parametrize("case", ["ties", "geometric", "directed", "vloss_prefer"])
-def test_dense_delta_live_chunks(case, live, monkeypatch):
+def test_dense_delta_live_chunks(case, live):
     """Delta rounds that walk only the 64-row chunks holding a changed row (k_live_chunks)
     against the full walk: the same matrices, bit for bit, and the oracle's.  Forced on for
-    every delta round (SHADOWTOPO_DELTA_LIVE=1) and off (=0)."""
-    monkeypatch.setenv("SHADOWTOPO_DELTA_LIVE", live)
+    every delta round (OPT_DELTA_LIVE=1) and off (=0)."""
     if case == "ties":
         g = synth.integer_grid(rows=11, cols=12, seed=6)
     elif case == "directed":
@@ -435,7 +423,7 @@ def test_dense_delta_live_chunks(case, live, monkeypatch):
         g = synth.geometric_complete_ish(V=900, A=200)
     # (the live-chunk lists serve the unpruned order; the pruned delta rounds bound chunks
     # themselves: test_dense_prune_same_results)
-    st = compare(g, layout="dense", delta_permille=1000, dense_prune=0)
+    st = compare(g, layout="dense", delta_permille=1000, dense_prune=0, delta_live=int(live))
     assert st["dense"] == 1 and st["delta_sweeps"] > 0
     assert (st["sparse_deltas"] > 0) == (live == "1")
 

@@ -1,13 +1,14 @@
 """Full-size parity on BASELINE.json's configs C2-C5 (SURVEY.md 8d generators, fixed seeds).
 
-The engine computes whole attached rows at the real graph size (C2: every one of the 1000
-sources, i.e. the bench workload itself; C3-C5: a source block spanning several batches).
-The north-star matrix (C4: all 10^4 x 10^4 attached pairs) and the whole C3 matrix
-(7000 x 7000) are compared with the CPU oracle bit for bit, every pair; C2 and C5 one full
-64-source batch each, every row of it (the oracle over the box's CPU share: the C4 matrix
-is ~25 s of heap-exact Dijkstra on 16 threads).  Every computed row is also checked for
-size-independent properties: the reference's pair kinds, hop/latency consistency, and
-d(s, t) <= w(s, t) wherever the arc exists (a shortest path is never longer than the edge).
+The engine computes the bench's own workloads at the real graph size.  The north-star
+matrix (C4: all 10^4 x 10^4 attached pairs) and the whole C3 matrix (7000 x 7000) are
+compared with the CPU oracle bit for bit, every pair (the oracle over the box's CPU share:
+the C4 matrix is ~25 s of heap-exact Dijkstra on 16 threads); C2 (all 1000 rows) with 256
+random rows, so every 64-source batch is sampled; C5 (all 50 000 rows in one call, the
+bench's batch groups) with two rows of every group and the last ten.  Every computed row is
+also checked for size-independent properties: the reference's pair kinds, hop/latency
+consistency, and d(s, t) <= w(s, t) wherever the arc exists (a shortest path is never
+longer than the edge); C5's whole matrix also for d(s, t) = d(t, s) to rounding.
 """
 import os
 
@@ -130,7 +131,88 @@ def test_c4_north_star_whole_matrix_vs_oracle():
     _run(g, 0, A, sample=[], block=(0, A))
 
 
-def test_c5_chung_lu_full_size():
-    """C5: a 128-row block spanning two batches; its first whole batch against the oracle"""
+def _oracle_rows_check(g, rows, lat, rel, hops, kind):
+    """the oracle's rows `rows` (one OpenMP call over the list) against the engine's rows,
+    given as host arrays whose row q is matrix row rows[q]"""
+    og = oracle_for(g)
+    flags = og.flags(prefer_direct=g.prefer_direct)
+    olat, orel, ohops, okind, _ = og.pair_rows_list(flags, g.attached, rows, nthreads=_threads())
+    og.close()
+    assert_bitexact("kind", kind, okind)
+    assert_bitexact("latency", lat, olat)
+    assert_bitexact("hops", hops, ohops)
+    assert_bitexact("reliability", rel, orel)
+
+
+def test_c2_every_batch_sampled_vs_oracle():
+    """The bench workload (all 1000 sources, 16 batches of sources in locality order): 256
+    seeded random rows against the oracle, so every batch is sampled (a batch missing all 256
+    has probability (1 - 64/1000)^256 < 1e-7)"""
+    g = synth.geometric_complete_ish(V=10_000, A=1_000)
+    eng = E.Engine.from_synth(g)
+    eng.set_attached(g.attached)
+    lat, rel, hops, kind = eng.compute_rows()
+    st = eng.stats()
+    eng.close()
+    assert st["dense"] == 1 and st["batches"] == 16
+    rows = np.sort(np.random.default_rng(2024).choice(1000, 256, replace=False)).astype(np.int32)
+    _oracle_rows_check(g, rows, lat[rows], rel[rows], hops[rows], kind[rows])
+
+
+def test_c5_whole_matrix_on_device():
+    """C5 exactly as the bench times it: all 50 000 rows in one call with the default grouping
+    (batch groups sized by HBM, the pools reused across them, grids past 2^24 blocks going
+    2-D), the 50 GB of rows left on the device.  Every row is checked there for the
+    size-independent properties (kinds, hop / latency / reliability ranges, d(s, t) = d(t, s)
+    to rounding in this undirected graph, d(s, t) <= w(s, t) over every attached arc), and two
+    rows of every group plus the last ten rows against the oracle bit for bit."""
+    torch = pytest.importorskip("torch")
     g = synth.chung_lu(V=1_000_000, A=50_000)
-    _run(g, 20_000, 20_128, sample=[20_101], block=(20_000, 20_064))
+    A = len(g.attached)
+    dev = torch.device("cuda:0")
+    lat = torch.empty((A, A), dtype=torch.float64, device=dev)
+    rel = torch.empty((A, A), dtype=torch.float64, device=dev)
+    hops = torch.empty((A, A), dtype=torch.int32, device=dev)
+    kind = torch.empty((A, A), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    eng = E.Engine.from_synth(g)
+    eng.set_attached(g.attached)
+    eng.compute_rows_device(0, A, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), kind.data_ptr())
+    st = eng.stats()
+    eng.close()
+    assert st["sources"] == A and st["batches"] == (A + 63) // 64
+    assert st["groups"] >= 2, "expected several batch groups"
+    nb = st["group_batches"]
+    # every row, on the device, in blocks of 5000 rows
+    diag = torch.arange(A, device=dev)
+    assert (kind[diag, diag] == 2).all()  # the self rule on the diagonal
+    for r0 in range(0, A, 5000):
+        r1 = min(A, r0 + 5000)
+        k, l_, h, r = kind[r0:r1], lat[r0:r1], hops[r0:r1], rel[r0:r1]
+        dj = k == KIND_DIJKSTRA
+        assert int((k == 0).sum()) == 0  # the giant component: every pair routable
+        assert bool((l_[dj] > 0).all()) and bool((h[dj] >= 1).all())
+        assert bool(((r[dj] > 0) & (r[dj] <= 1)).all())
+        lt = lat[:, r0:r1].t()
+        rel_err = ((l_ - lt).abs() / torch.maximum(l_, lt))[dj & (kind[:, r0:r1].t() == KIND_DIJKSTRA)]
+        assert float(rel_err.max()) <= 1e-12  # the same shortest distance from both ends
+        del k, l_, h, r, dj, lt, rel_err
+    pos = np.full(g.n, -1, np.int64)
+    pos[g.attached] = np.arange(A)
+    pa, pb = pos[g.src], pos[g.dst]
+    keep = (pa >= 0) & (pb >= 0) & (g.src != g.dst)
+    ia = torch.as_tensor(pa[keep], device=dev)
+    ib = torch.as_tensor(pb[keep], device=dev)
+    w = torch.as_tensor(g.latency[keep], device=dev)
+    for x, y in ((ia, ib), (ib, ia)):
+        assert bool(((kind[x, y] != KIND_DIJKSTRA) | (lat[x, y] <= w)).all())
+    # the oracle: two rows of every batch group's row range, and the last ten rows
+    G = nb * 64
+    rows = []
+    for r0 in range(0, A, G):
+        r1 = min(A, r0 + G)
+        rows += [r0 + (r1 - r0) // 3, r0 + 2 * (r1 - r0) // 3]
+    rows = np.array(sorted(set(rows + list(range(A - 10, A)))), np.int32)
+    idx = torch.as_tensor(rows.astype(np.int64), device=dev)
+    _oracle_rows_check(g, rows, lat[idx].cpu().numpy(), rel[idx].cpu().numpy(),
+                       hops[idx].cpu().numpy().astype(np.uint32), kind[idx].cpu().numpy())

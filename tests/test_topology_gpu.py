@@ -260,6 +260,52 @@ def test_late_attach_keeps_counters_and_values(tmp_path, directed):
     top.free()
 
 
+def test_two_late_attaches_old_rows_get_own_entries(tmp_path):
+    """two late attaches with no old-source miss between them.  The second
+    late-attach matrix copies the first one's old rows, reverse copies included; the first
+    Dijkstra of an old source afterwards must cache its OWN entries for the middle block of
+    targets (attached by the first late attach) too, not the reverse copies."""
+    g = synth.random_sparse(V=90, avg_deg=4, seed=45, A=30)
+    g26 = _subset(g, 26)
+    lat_o, rel_o, _, kind_o, _ = oracle_matrix(g26)
+    # an old source i and a middle target t whose two directions differ in the last bits
+    pairs = [(i, t) for i in range(10) for t in range(10, 20)
+             if kind_o[i, t] == 3 and (lat_o[i, t] != lat_o[t, i] or rel_o[i, t] != rel_o[t, i])]
+    assert pairs, "fixture graph has no asymmetric old/middle pair"
+    i0, t0 = pairs[0]
+    model = ref_cache(g26, lat_o, kind_o)
+    va, ips = with_vertex_ips(g)
+    top = T.Topology.new(write(tmp_path, "l2.xml", synth.to_graphml(g, extra_vattr=va)))
+    hosts = attach_all(top, ips, g.attached[:10])
+
+    def q(i, j):
+        a, b = all_hosts[i], all_hosts[j]
+        si, sj = model.get_path_entry(i, j)
+        assert top.getLatency(a, b) == lat_o[si, sj], (i, j, si, sj)
+        model.get_path_entry(i, j)
+        assert top.getReliability(a, b) == rel_o[si, sj], (i, j, si, sj)
+
+    all_hosts = list(hosts)
+    model.A = 10
+    j0 = next(j for j in range(10) if j != i0)
+    q(j0, j0 ^ 1 if (j0 ^ 1) != i0 else (j0 + 2) % 10)  # a Dijkstra of another old source
+    all_hosts += attach_all(top, ips, g.attached[10:20], base=100)
+    model.A = 20
+    s2 = next(s for s in range(10, 20) if s != t0)
+    q(s2, j0)  # a new source: the first late-attach matrix, never filled
+    all_hosts += attach_all(top, ips, g.attached[20:26], base=200)
+    model.A = 26
+    q(20, j0)  # the second late-attach matrix, copied from the unfilled one
+    assert top.info()["computed_for"] == 26
+    q(i0, t0)  # i0's Dijkstra: its own (i0, t0) entry
+    q(t0, i0)  # answered with the cached (i0, t0) Path
+    for i in range(26):
+        for j in range(26):
+            q(i, j)
+    check_cache_state(top, model)
+    top.free()
+
+
 def test_cache_emulation_upcalls_and_teardown_log(tmp_path, capfd):
     """the drop-in's cache follows the reference's query order: the minimum handed to
     worker_updateMinTimeJump after each query, the Dijkstra / self-path run counts, and the
@@ -300,6 +346,53 @@ def test_c_harness_lookups_under_threads(tmp_path):
     res = run_harness(build_harness(tmp_path), path, 300, 8, 20000, 0)
     assert res["compute_failed"] == 0 and res["routable"] > 0
     assert res["ns_per_call_per_thread"] > 0
+
+
+def test_lock_free_cache_under_racing_workers(tmp_path):
+    """the path cache is lock-free (a CAS claim per Path, a CAS per source store
+    loop, in-place fills of old rows after a late attach).  8 C worker threads
+    (tests/c/topo_race.c) query and count packets over overlapping pairs of 32 hosts, then of
+    48 after a late attach that the workers themselves resolve.  Every returned value must be
+    the oracle's entry of the direction the pair is cached in, no unordered pair may be cached
+    in both directions, cached_paths must equal the cached cells, and no increment is lost."""
+    import subprocess
+    from test_topology_shim import INCLUDE
+    from shadow_amd import engine as E
+    g = synth.random_sparse(V=160, avg_deg=4, seed=51, A=48)
+    assert len(set(g.attached)) == 48
+    va, ips = with_vertex_ips(g)
+    path = write(tmp_path, "r.xml", synth.to_graphml(g, extra_vattr=va))
+    hints = write(tmp_path, "hints.txt", "\n".join(ips[v] for v in g.attached) + "\n")
+    src = os.path.join(os.path.dirname(__file__), "c", "topo_race.c")
+    lib_dir = os.path.dirname(E.LIB_PATH)
+    exe = str(tmp_path / "topo_race")
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-pthread", "-I", INCLUDE, src, "-o", exe, "-L", lib_dir,
+                    "-lshadowtopo_hip", f"-Wl,-rpath,{lib_dir}"], check=True)
+    out = str(tmp_path / "recs.bin")
+    res = subprocess.run([exe, path, hints, "32", "16", "8", "3000", out], check=True, capture_output=True,
+                         text=True, timeout=300)
+    lines = res.stdout.strip().splitlines()
+    head = json.loads(lines[0])
+    assert head["compute_failed"] == 0
+    cells = {}
+    total = 0
+    for ln in lines[1:]:
+        _, a, b, cell, cnt = ln.split()
+        a, b, cell, cnt = int(a), int(b), int(cell), int(cnt)
+        assert cell in (0, 1, 2) or (a == b and cell == 1), (a, b, cell)
+        if cell:
+            cells[(a, b)] = (a, b) if (cell == 1) else (b, a)
+        total += cnt
+    assert head["cached_paths"] == len(cells)
+    assert total == head["increments"]
+    rec = np.fromfile(out, dtype=[("phase", "<i4"), ("i", "<i4"), ("j", "<i4"), ("pad", "<i4"),
+                                  ("lat", "<f8"), ("rel", "<f8")])
+    assert len(rec) == 2 * 8 * 3000
+    lat_o, rel_o, _, kind_o, _ = oracle_matrix(g)
+    for r in rec:
+        i, j = int(r["i"]), int(r["j"])
+        si, sj = cells[(min(i, j), max(i, j))]  # every answered pair is cached, one direction for good
+        assert r["lat"] == lat_o[si, sj] and r["rel"] == rel_o[si, sj], (int(r["phase"]), i, j, si, sj)
 
 
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
