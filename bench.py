@@ -151,7 +151,7 @@ def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0):
     else:
         # every relax round of the step (grid and worklist launches alike): achieved = the
         # step's compulsory bytes / the relax kernels' time in the step
-        kname = "k_relax"
+        kname = "k_push+k_pred_pass+k_fold" if st.get("push_rounds") else "k_relax"
         launches, kms = max(1, st["relax_launches"]), st["relax_ms"]
         bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * steps / launches
         batches_per_launch = st["relax_batches"] / launches
@@ -419,6 +419,7 @@ def main():
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
+    ap.add_argument("--csr-variant", type=int, default=1, help="sparse rounds: 1 = pull (default), 2 = push (u64 atomicMin)")
     ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists when under half the pairs are active (1, default), "
                          "always (2), or the full grid (0)")
     args = ap.parse_args()
@@ -476,6 +477,8 @@ def main():
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
+    if not eng.complete and args.csr_variant != 1:
+        eng.set_option(E.OPT_CSR_VARIANT, args.csr_variant)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
         f"complete={eng.complete}")
     rows = r1 - r0
@@ -601,6 +604,13 @@ def main():
                        "visits_per_step": st["visits"] / args.steps, "changes_per_step": st["changes"] / args.steps,
                        "full_sweeps_per_step": st["full_sweeps"] / args.steps,
                        "delta_sweeps_per_step": st["delta_sweeps"] / args.steps,
+                       "host_syncs_per_step": st["host_syncs"] / args.steps,
+                       "groups_per_step": st["groups"] / args.steps,
+                       "push_phases_ms_per_step": ({"push": st["push_ms"] / args.steps, "pred": st["pred_ms"] / args.steps,
+                                                    "fold": st["fold_ms"] / args.steps,
+                                                    "push_rounds": st["push_rounds"] / args.steps,
+                                                    "fold_rounds": st["fold_rounds"] / args.steps}
+                                                   if st["push_rounds"] else None),
                        "host_buffers_ms": host_ms, "host_buffers_pageable_ms": host_pageable_ms,
                        "cold_start_ms": cold_start_ms,
                        # where the cold start goes: shadowtopo_create (edge validation, upload,

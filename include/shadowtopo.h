@@ -78,7 +78,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
                                               (vertex, source) pairs gets a change-mask delta round instead of a full
                                               sweep (default 125; 0 = always full sweeps) */
-#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (the only one) */
+#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernels: SHADOWTOPO_CSR_FULL (pull, default) or _PUSH */
 #define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
 #define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Hilbert
                                               order of the top two principal axes of the distances to eight
@@ -124,6 +124,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
  * read fewer rows but issued more instructions and were slower on every config;
  * they were removed in r03. */
 #define SHADOWTOPO_CSR_FULL 1
+/* push rounds (undirected graphs): distances pushed from changed (vertex, source) pairs along
+ * their out-arcs with a 64-bit atomicMin on the f64 bit pattern, then one exact pull pass for
+ * the predecessors and level rounds for hops / reliability */
+#define SHADOWTOPO_CSR_PUSH 2
 
 typedef struct shadowtopo_stats {
     int64_t n_vertices;
@@ -180,6 +184,11 @@ typedef struct shadowtopo_stats {
     int64_t group_batches;   /* batches in flight per group of the last computation (its largest group) */
     int64_t host_syncs;      /* host waits on the device inside the relaxation rounds (a round's counts
                                 read back before the next launch; device-driven rounds: once per block) */
+    double push_ms;          /* OPT_TIMING, CSR_PUSH: distance push rounds, predecessor pass, fold rounds */
+    double pred_ms;
+    double fold_ms;
+    int64_t push_rounds;
+    int64_t fold_rounds;
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -572,6 +572,237 @@ __global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ i
     }
 }
 
+// ---------------------------------------------------------------- push rounds (CSR_PUSH)
+// SHADOWTOPO_CSR_PUSH (undirected CSR graphs): the north star's push relaxation, as an
+// alternative to the pull rounds above.  Three phases:
+//  1. distances only: every (u, source) pair that changed last round pushes fl(d(u) + w)
+//     along u's out-arcs (= its in-list, undirected) with a 64-bit atomicMin on the f64 bit
+//     pattern (non-negative doubles order like their bits); a plain load of the head's row
+//     first, so only lanes that improve on what they see reach the atomic unit (a stale
+//     value is never lower than the current one: values only fall).  The lanes that changed
+//     are OR-ed into the head's change mask for the next round (chm, the dense mode's masks).
+//     Same least fixed point as the pull rounds, so the same distances.
+//  2. k_pred_pass: one exact pull pass over every reached (vertex, batch) with the final
+//     distances: the lexicographic (fl(d(u)+w), d(u)) minimum and the heap-order tie flag,
+//     exactly relax_visit's, gives P and the local tie bit (H = HNOT | LTIE until folded).
+//  3. k_fold level rounds: round k finishes every pair whose predecessor finished before round
+//     k (its hop count is < k: a pair finished in round k has k hops, so a same-round write is
+//     never used), carrying hops, taint and the reliability product down the tree as
+//     finish_vertex does; a pair that finishes activates its out-neighbours.
+constexpr uint32_t HNOT = HMASK;  // H hop field of a reached pair whose tree fold is pending
+
+__device__ __forceinline__ unsigned long long* gen_u64(gdouble* p) {
+    return (unsigned long long*)(double*)p;
+}
+
+__device__ __forceinline__ void push_visit(const int32_t* __restrict__ in_src, const double* __restrict__ in_w,
+                                           int32_t beg, int32_t end, const BatchDev& B, int32_t b, int32_t u, int lane,
+                                           int32_t parity, int32_t* __restrict__ cnt) {
+    unsigned long long* chm_cur = B.chm(parity);
+    const unsigned long long m = readlane_u64(chm_cur[u], 0);
+    if (m == 0ull) return;
+    if (lane == 0) chm_cur[u] = 0ull;  // reused two rounds on; this round's pushes go to the other parity
+    const bool on = (m >> lane) & 1ull;
+    const double du = B.D[(size_t)u * KL + lane];
+    unsigned long long* chm_nxt = B.chm(parity ^ 1);
+    gbyte* act_nxt = B.act(parity ^ 1);
+    bool any = false;
+    for (int32_t e = beg; e < end; e += 8) {
+        int32_t v[8];
+        double w[8], dv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            v[k] = in_src[e + k];
+            w[k] = in_w[e + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dv[k] = (on && e + k < end) ? B.D[(size_t)v[k] * KL + lane] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double c = du + w[k];
+            bool imp = on && e + k < end && c < dv[k];
+            if (imp) {
+                const unsigned long long cb = (unsigned long long)__double_as_longlong(c);
+                const unsigned long long old = __hip_atomic_fetch_min(gen_u64(B.D + (size_t)v[k] * KL + lane), cb,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                imp = cb < old;
+            }
+            const unsigned long long bal = __ballot(imp);
+            if (bal) {
+                any = true;
+                if (lane == 0) {
+                    atomicOr(&chm_nxt[v[k]], bal);
+                    act_nxt[v[k]] = 1;
+                }
+            }
+        }
+    }
+    if (any && lane == 0) cnt[b] = 1;
+}
+
+__global__ __launch_bounds__(256) void k_push(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                              const double* __restrict__ in_w, Pools pools, int32_t V, int32_t nb,
+                                              int32_t nvb, int32_t parity, int32_t* __restrict__ cnt) {
+    int32_t b, vt;
+    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t u = vt * 4 + wave;
+    if (u >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    gbyte* act_cur = B.act(parity);
+    if (act_cur[u] == 0) return;
+    if (lane == 0) act_cur[u] = 0;
+    push_visit(in_src, in_w, (int32_t)in_ptr[u], (int32_t)in_ptr[u + 1], B, b, u, lane, parity, cnt);
+}
+
+__global__ __launch_bounds__(256) void k_push_wl(const int32_t* __restrict__ in_src, const double* __restrict__ in_w,
+                                                 Pools pools, int32_t parity, const int4* __restrict__ wl,
+                                                 const int64_t* __restrict__ prefix, int32_t nb, int64_t S,
+                                                 int32_t* __restrict__ cnt) {
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t L = flat_block();
+    const int64_t i = (L & 7) * S + (L >> 3) * 4 + wave;
+    const int64_t T = prefix[nb];
+    if ((L >> 3) * 4 + wave >= S || i >= T) return;
+    const int lane = threadIdx.x & 63;
+    const int32_t b = __builtin_amdgcn_readfirstlane(wl_batch(prefix, nb, i, lane));
+    const int4 it = wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])];
+    const int32_t u = __builtin_amdgcn_readfirstlane(it.x);
+    const int32_t beg = __builtin_amdgcn_readfirstlane(it.y), end = __builtin_amdgcn_readfirstlane(it.z);
+    const BatchDev B = batch_view(pools, b);
+    push_visit(in_src, in_w, beg, end, B, b, u, lane, parity, cnt);
+    if (lane == 0) B.act(parity)[u] = 0;
+}
+
+// phase 1 seed: d(s) = 0, the source's tree record (k_seed's), its lane in the change mask
+__global__ void k_seed_push(GraphDev g, Pools pools) {
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int j = threadIdx.x;
+    if (j >= KL) return;
+    const int32_t s = B.srcv[j];
+    if (s < 0) return;
+    const size_t idx = (size_t)s * KL + j;
+    B.D[idx] = 0.0;
+    B.H[idx] = 0;
+    B.R[idx] = g.vfac[s];
+    B.P[idx] = -1;
+    atomicOr(&B.chm0[s], 1ull << j);
+    B.act0[s] = 1;
+}
+
+// phase 2: P and the local tie bit of every reached (vertex, source) pair from the final
+// distances; the sources activate their out-neighbours for fold round 1 (act parity 1)
+__global__ __launch_bounds__(256) void k_pred_pass(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                   const double* __restrict__ in_w, Pools pools, int32_t V, int32_t nb,
+                                                   int32_t nvb) {
+    int32_t b, vt;
+    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v = vt * 4 + wave;
+    if (v >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    const int32_t sv = B.srcv[lane];
+    const size_t idx = (size_t)v * KL + lane;
+    const double dv = B.D[idx];
+    const bool src = sv == v;
+    if (__ballot(src)) {  // a source vertex of some lane: fold round 1 starts at its out-neighbours
+        for (int64_t x = in_ptr[v] + lane; x < in_ptr[v + 1]; x += 64) B.act1[in_src[x]] = 1;
+    }
+    if (!__ballot(dv < dinf() && !src)) return;
+    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
+    const gdouble* Dl = B.D + lane;
+    double bc = dmax(), bdu = dinf();
+    int32_t be = -1, bu = -1;
+    bool tie = false;
+    for (int32_t e = beg; e < end; e += 8) {
+        int32_t u[8];
+        double w[8], du[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u[k] = in_src[e + k];
+            w[k] = in_w[e + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (e + k >= end) w[k] = dinf();
+            du[k] = e + k < end ? Dl[(size_t)u[k] * KL] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) relax_arc(du[k], w[k], e + k, u[k], bc, bdu, be, bu, tie);
+    }
+    if (dv < dinf() && !src && sv >= 0) {
+        // bc == dv: the distances are the fixed point of exactly this minimum
+        B.P[idx] = be;
+        B.H[idx] = HNOT | ((tie || bdu == bc) ? LTIE : 0u);
+    }
+}
+
+// phase 3, fold round k: pairs whose predecessor's hop count is < k (finished in an earlier
+// round; its H / R written by an earlier launch) take H = H(u) + 1 (+ taint) and
+// R = R(u) * r(arc); a vertex with a finished lane activates its out-neighbours
+__device__ __forceinline__ void fold_visit(const int32_t* __restrict__ in_src, const double* __restrict__ in_r,
+                                           const int64_t* __restrict__ out_ptr, const int32_t* __restrict__ out_dst,
+                                           const BatchDev& B, int32_t b, int32_t v, int lane, int32_t parity,
+                                           uint32_t k, int32_t* __restrict__ cnt) {
+    const size_t idx = (size_t)v * KL + lane;
+    const uint32_t hv = B.H[idx];
+    bool fin = false;
+    if ((hv & HMASK) == HNOT && B.D[idx] < dinf()) {
+        const int32_t arc = B.P[idx];
+        const int32_t u = in_src[arc];
+        const size_t uidx = (size_t)u * KL + lane;
+        const uint32_t hu = B.H[uidx];
+        if ((hu & HMASK) < k) {
+            const uint32_t taint = (hu & TAINT) | ((hv & LTIE) ? (TAINT | LTIE) : 0u);
+            B.H[idx] = (((hu & HMASK) + 1u) & HMASK) | taint;
+            B.R[idx] = B.R[uidx] * in_r[arc];
+            fin = true;
+        }
+    }
+    if (__ballot(fin)) {
+        gbyte* act_nxt = B.act(parity ^ 1);
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) cnt[b] = 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fold(const int32_t* __restrict__ in_src, const double* __restrict__ in_r,
+                                              const int64_t* __restrict__ out_ptr, const int32_t* __restrict__ out_dst,
+                                              Pools pools, int32_t V, int32_t nb, int32_t nvb, int32_t parity, uint32_t k,
+                                              int32_t* __restrict__ cnt) {
+    int32_t b, vt;
+    if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int32_t v = vt * 4 + wave;
+    if (v >= V) return;
+    const int lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, b);
+    gbyte* act_cur = B.act(parity);
+    if (act_cur[v] == 0) return;
+    if (lane == 0) act_cur[v] = 0;
+    fold_visit(in_src, in_r, out_ptr, out_dst, B, b, v, lane, parity, k, cnt);
+}
+
+__global__ __launch_bounds__(256) void k_fold_wl(const int32_t* __restrict__ in_src, const double* __restrict__ in_r,
+                                                 const int64_t* __restrict__ out_ptr, const int32_t* __restrict__ out_dst,
+                                                 Pools pools, int32_t parity, uint32_t k, const int4* __restrict__ wl,
+                                                 const int64_t* __restrict__ prefix, int32_t nb, int64_t S,
+                                                 int32_t* __restrict__ cnt) {
+    const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t L = flat_block();
+    const int64_t i = (L & 7) * S + (L >> 3) * 4 + wave;
+    const int64_t T = prefix[nb];
+    if ((L >> 3) * 4 + wave >= S || i >= T) return;
+    const int lane = threadIdx.x & 63;
+    const int32_t b = __builtin_amdgcn_readfirstlane(wl_batch(prefix, nb, i, lane));
+    const int32_t v = __builtin_amdgcn_readfirstlane(wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x);
+    const BatchDev B = batch_view(pools, b);
+    fold_visit(in_src, in_r, out_ptr, out_dst, B, b, v, lane, parity, k, cnt);
+    if (lane == 0) B.act(parity)[v] = 0;
+}
+
 // Lexicographic (candidate, d(u)) minimum with heap-order tie detection, branch-free so the
 // compiler keeps the per-destination state in scalars (a branchy form made it copy whole
 // <8 x double> vectors around the control flow).
@@ -2461,6 +2692,7 @@ struct shadowtopo_engine {
     bool floor_ok = false;             // default_nb: the 24 GB budget floor was found free once
     size_t pool_bytes = 0;             // device bytes the batch pools hold (ensure_batches)
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
+    int32_t opt_csr_variant = SHADOWTOPO_CSR_FULL;  // CSR rounds: pull (FULL) or push (PUSH, undirected)
     int32_t trace_rounds = 0;          // SHADOWTOPO_TRACE_ROUNDS=1: one stderr line per relax round
     int32_t opt_delta_live = 2;        // dense delta rounds over live-chunk lists: 0 never, 1 always, 2 when sparse
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
@@ -2766,10 +2998,110 @@ dim3 grid_of(const shadowtopo_engine* eng, int64_t n) {
     return dim3((uint32_t)GX, (uint32_t)((n + GX - 1) / GX));
 }
 
+// SHADOWTOPO_CSR_PUSH rounds (k_push / k_pred_pass / k_fold): frontier rounds over the
+// activity flags (worklists when under half the pairs are active, the grid otherwise), one
+// host read-back of the next round's worklist counts per round
+int run_push_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
+    const int32_t V = eng->V;
+    const GraphDev& g = eng->rg ? *eng->rg : eng->g;
+    const size_t total = (size_t)eng->Vp * KL;
+    const int32_t gx = (int32_t)std::min<size_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_init, dim3(gx, nbg), dim3(256), 0, s, eng->pools, eng->Vp, 0);
+    hipLaunchKernelGGL(k_seed_push, dim3(1, nbg), dim3(64), 0, s, g, eng->pools);
+    HIP_TRY(hipGetLastError());
+    const int32_t nvb = (V + 3) / 4;
+    const int64_t nblocks = 8 * (((int64_t)nbg * nvb + 7) / 8);
+    const int32_t ncb = (V + WL_SPAN - 1) / WL_SPAN;
+    const int64_t max_rounds = eng->opt_max_rounds > 0 ? eng->opt_max_rounds : 4LL * V + 64;
+    auto compact = [&](int32_t par) -> int {
+        HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
+        hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, par, eng->d_wl,
+                           eng->d_wlcnt, g.in_ptr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
+        HIP_TRY(round_sync(eng, s));
+        eng->st.host_syncs++;
+        return SHADOWTOPO_OK;
+    };
+    int32_t* cnt = eng->d_cnt;  // written by the kernels (a batch changed), not read back
+    for (int phase = 0; phase < 2; ++phase) {
+        // phase 0: distance pushes from act parity 0 (the sources); phase 1: fold rounds from
+        // act parity 1 (set by k_pred_pass for the sources' out-neighbours)
+        if (phase == 1) {
+            if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
+            hipLaunchKernelGGL(k_pred_pass, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                               eng->pools, V, nbg, nvb);
+            HIP_TRY(hipGetLastError());
+            if (eng->opt_timing) {
+                HIP_TRY(hipEventRecord(eng->ev1, s));
+                HIP_TRY(hipEventSynchronize(eng->ev1));
+                float ms = 0;
+                HIP_TRY(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
+                eng->st.relax_ms += ms;
+                eng->st.pred_ms += ms;
+            }
+            eng->st.relax_launches++;
+            eng->st.relax_batches += nbg;
+        }
+        const int32_t par0 = phase;
+        int rc;
+        if ((rc = compact(par0))) return rc;
+        for (int64_t r = 0;; ++r) {
+            if (r > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "push rounds did not converge in %lld rounds", (long long)max_rounds);
+            const int32_t par = (int32_t)((par0 + r) & 1);
+            eng->h_wlpre[0] = 0;
+            for (int32_t b = 0; b < nbg; ++b) eng->h_wlpre[b + 1] = eng->h_wlpre[b] + eng->h_wlcnt[b];
+            const int64_t wl_total = eng->h_wlpre[nbg];
+            if (wl_total == 0) break;
+            const bool round_wl = eng->opt_worklist == 2 || (eng->opt_worklist == 1 && wl_total * 2 < (int64_t)nbg * V);
+            if (round_wl)
+                HIP_TRY(hipMemcpyAsync(eng->d_wlpre, eng->h_wlpre, sizeof(int64_t) * (nbg + 1), hipMemcpyHostToDevice, s));
+            if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
+            const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;
+            if (phase == 0) {
+                if (round_wl)
+                    hipLaunchKernelGGL(k_push_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_src, g.in_w,
+                                       eng->pools, par, eng->d_wl, eng->d_wlpre, nbg, S, cnt);
+                else
+                    hipLaunchKernelGGL(k_push, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                                       eng->pools, V, nbg, nvb, par, cnt);
+            } else {
+                const uint32_t k = (uint32_t)(r + 1);
+                if (round_wl)
+                    hipLaunchKernelGGL(k_fold_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_src, g.in_r,
+                                       g.out_ptr, g.out_dst, eng->pools, par, k, eng->d_wl, eng->d_wlpre, nbg, S, cnt);
+                else
+                    hipLaunchKernelGGL(k_fold, grid_of(eng, nblocks), dim3(256), 0, s, g.in_src, g.in_r, g.out_ptr,
+                                       g.out_dst, eng->pools, V, nbg, nvb, par, k, cnt);
+            }
+            HIP_TRY(hipGetLastError());
+            if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev1, s));
+            if ((rc = compact(par ^ 1))) return rc;
+            float ms = 0;
+            if (eng->opt_timing) {
+                HIP_TRY(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
+                eng->st.relax_ms += ms;
+                if (round_wl) eng->st.wl_ms += ms;
+                (phase == 0 ? eng->st.push_ms : eng->st.fold_ms) += ms;
+            }
+            eng->st.rounds++;
+            eng->st.relax_launches++;
+            eng->st.relax_batches += nbg;
+            if (round_wl) eng->st.wl_launches++;
+            (phase == 0 ? eng->st.push_rounds : eng->st.fold_rounds)++;
+            if (eng->trace_rounds)
+                fprintf(stderr, "[shadowtopo] %s round %lld batches %d items %lld%s %.3f ms\n", phase ? "fold" : "push",
+                        (long long)r, nbg, (long long)wl_total, round_wl ? " (worklist)" : "", ms);
+        }
+    }
+    return SHADOWTOPO_OK;
+}
+
 // relax rounds for the batch slots [0, nbg) until no vertex changes
 int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = eng->V;
     const GraphDev& g = eng->rg ? *eng->rg : eng->g;
+    if (!eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_PUSH && eng->d_wl) return run_push_rounds(eng, nbg, s);
     const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->d_WR && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
     if (fused_seed) {
         hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / SEED_T, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
@@ -4197,8 +4529,11 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             // one sparse kernel family (k_relax / k_relax_wl / k_relax_wlp); the r01-r02
             // cross-check variants (changed-tail delta, stamped f32 keys, change records) were
             // slower on every config and are gone
-            if (value != SHADOWTOPO_CSR_FULL)
-                return fail(SHADOWTOPO_EINVAL, "CSR variant %lld: only SHADOWTOPO_CSR_FULL exists", (long long)value);
+            if (value != SHADOWTOPO_CSR_FULL && value != SHADOWTOPO_CSR_PUSH)
+                return fail(SHADOWTOPO_EINVAL, "unknown CSR variant %lld", (long long)value);
+            if (value == SHADOWTOPO_CSR_PUSH && (eng->flags & SHADOWTOPO_F_DIRECTED))
+                return fail(SHADOWTOPO_EINVAL, "CSR_PUSH pushes along the in-lists: undirected graphs only");
+            eng->opt_csr_variant = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SOURCE_ORDER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "source order must be 0 or 1");

@@ -49,7 +49,8 @@ OPT_GRID_X = 15
 OPT_PRUNE_PENDANT = 16
 OPT_DEVICE_ROUNDS = 17
 OPT_DELTA_LIVE = 19  # dense delta rounds over live-chunk lists: 2 when sparse (default), 1 always, 0 never
-CSR_FULL = 1  # recompute every active vertex over all in-arcs (k_relax / k_relax_wl: the only sparse family)
+CSR_FULL = 1  # pull: recompute every active vertex over all in-arcs (k_relax / k_relax_wl, default)
+CSR_PUSH = 2  # push: distance pushes with a u64 atomicMin, then a predecessor pass and fold rounds (undirected)
 
 # every symbol include/shadowtopo.h declares
 ENGINE_SYMBOLS = (
@@ -84,6 +85,8 @@ class Stats(ctypes.Structure):
         ("create_alloc_ms", ctypes.c_double), ("groups", ctypes.c_int64),
         ("prepare_ms", ctypes.c_double), ("create_prepare_wait_ms", ctypes.c_double),
         ("group_batches", ctypes.c_int64), ("host_syncs", ctypes.c_int64),
+        ("push_ms", ctypes.c_double), ("pred_ms", ctypes.c_double), ("fold_ms", ctypes.c_double),
+        ("push_rounds", ctypes.c_int64), ("fold_rounds", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -445,3 +445,46 @@ def test_prepare_then_create_same_results():
     rb = b.compute_rows(0, len(g.attached))
     for x, y in zip(ra, rb):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("case", ["sparse", "groups", "ties", "vloss_prefer", "multigraph", "pendant", "worklist", "grid"])
+def test_push_rounds_same_results(case):
+    """SHADOWTOPO_CSR_PUSH (distance pushes with a u64 atomicMin, the exact predecessor pass,
+    the fold rounds) against the oracle, bit for bit: several batch groups, integer-latency
+    ties (the replay path), vertex loss + prefer-direct, parallel edges, pendant trees, and the
+    worklist / grid round forms forced"""
+    opts = {}
+    if case == "groups":
+        g = synth.random_sparse(V=500, avg_deg=4, seed=21)
+        opts["batches_in_flight"] = 3
+    elif case == "ties":
+        g = synth.integer_grid(rows=12, cols=12, seed=3)
+    elif case == "vloss_prefer":
+        rng = np.random.default_rng(4)
+        g = synth.random_sparse(V=200, avg_deg=5, seed=19, vloss=rng.uniform(0, 0.05, 200))
+        g.prefer_direct = True
+    elif case == "multigraph":
+        g = synth.random_sparse(V=150, avg_deg=4, seed=17)
+        rng = np.random.default_rng(0)
+        pick = rng.choice(np.nonzero(g.src != g.dst)[0], 40, replace=False)
+        g.src = np.concatenate([g.src, g.dst[pick]])
+        g.dst = np.concatenate([g.dst, g.src[pick]])
+        g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.3, 1.7, 40)])
+        g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 40)])
+    elif case == "pendant":
+        g = synth.chung_lu(V=3000, A=300, seeds=(7, 8))
+    else:
+        g = synth.random_sparse(V=600, avg_deg=3, seed=23, A=200)
+        opts["worklist"] = 2 if case == "worklist" else 0
+    st = compare(g, layout="csr", csr_variant=E.CSR_PUSH, **opts)
+    assert st["push_rounds"] > 0 and st["fold_rounds"] > 0
+    if case == "ties":
+        assert st["replayed_sources"] > 0
+
+
+def test_push_rounds_rejects_directed():
+    g = synth.random_sparse(V=100, avg_deg=4, seed=5, directed=True)
+    eng = E.Engine.from_synth(g)
+    with pytest.raises(E.ShadowTopoError):
+        eng.set_option(E.OPT_CSR_VARIANT, E.CSR_PUSH)
+    eng.close()
