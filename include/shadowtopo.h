@@ -257,6 +257,13 @@ void shadowtopo_host_free(void* p);
 int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_sources, double* dist, int32_t* pred,
                     uint32_t* hops, uint8_t* tie);
 
+/* The version-independent self-path rule (_topology_computeShortestPathToSelf,
+ * topology.c:1545-1653) for every attached vertex, host buffers of `count` entries (kind
+ * SHADOWTOPO_KIND_SELF, or _NONE without an incident edge), whatever the engine's
+ * F_SELF_DIJKSTRA_LOOP flag: under that flag the shim needs both values, because the
+ * reference caches a self pair from whichever of the two rules runs first. */
+int shadowtopo_self_rule_paths(shadowtopo_engine* eng, double* lat, double* rel, uint8_t* kind);
+
 int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out);
 void shadowtopo_reset_stats(shadowtopo_engine* eng);
 

@@ -17,7 +17,12 @@ It follows /root/reference/src/main/routing/topology.c:
 
 The path VALUES come from the caller (the oracle's own-row matrix: entry (s, t) is what
 s's own computation gives), so this module decides only which entry a query sees.
-Self pairs reached from a Dijkstra run take the configured self value.
+Self pairs: igraph's path to the source itself is [] or [s] by version.  With
+[] (the default rule) a Dijkstra run stores nothing for the source (topology.c:1815) and a
+self pair is cached only by a query (s, s), through the self-path rule.  With [s]
+(self_loop_rule) the run stores the source's self-loop path (the matrix diagonal), and fails
+(after storing the rest) when the source has no self-loop; a query (s, s) that comes first
+caches the self-path rule's value instead (self_lat / self_rel / self_kind).
 """
 from __future__ import annotations
 
@@ -25,7 +30,8 @@ import numpy as np
 
 
 class RefPathCache:
-    def __init__(self, lat, kind, *, directed, complete, prefer_direct, adjacent):
+    def __init__(self, lat, kind, *, directed, complete, prefer_direct, adjacent, self_loop_rule=False,
+                 self_lat=None, self_kind=None):
         """lat / kind: [A, A] oracle matrices over attached indices (kind 0 = unroutable);
         adjacent(i, j): the graph has an edge i -> j (either way when undirected; i == j:
         a self-loop).  In a directed graph too, _topology_shouldStorePath refuses (s, t) once
@@ -37,6 +43,11 @@ class RefPathCache:
         self.A = self.lat.shape[0]
         self.directed, self.complete, self.prefer_direct = directed, complete, prefer_direct
         self.adjacent = adjacent
+        self.self_loop_rule = self_loop_rule
+        self.self_lat = None if self_lat is None else np.asarray(self_lat)
+        self.self_rel = None
+        self.self_kind = None if self_kind is None else np.asarray(self_kind)
+        self.self_claimed = set()  # self pairs cached by the self-path rule (self_loop_rule)
         self.cache = {}          # (s, t) -> latency of the stored Path
         self.min_latency = 0.0   # topology.c minimumPathLatency
         self.upcalls = []        # every value handed to worker_updateMinTimeJump
@@ -56,11 +67,13 @@ class RefPathCache:
             return False
         return True
 
-    def _store(self, is_direct, s, t):
+    def _store(self, is_direct, s, t, via_self=False):
         if not self._should_store(is_direct, s, t):
             return
-        latency = float(self.lat[s, t])
+        latency = float(self.self_lat[s] if via_self else self.lat[s, t])
         self.cache[(s, t)] = latency
+        if via_self:
+            self.self_claimed.add(s)
         if self.min_latency == 0 or latency < self.min_latency:
             self.min_latency = latency
             self.upcalls.append(latency)
@@ -75,20 +88,28 @@ class RefPathCache:
 
     def _self_path(self, s):  # :1545-1653 (no incident edge: no path)
         self.self_paths += 1
-        if self.kind[s, s] == 0:
+        k = self.self_kind[s] if self.self_loop_rule else self.kind[s, s]
+        if k == 0:
             return False
-        self._store(False, s, s)
+        self._store(False, s, s, via_self=self.self_loop_rule)
         return True
 
     def _compute_source_paths(self, s, t):  # :1655-1875
         if s == t:
             return self._self_path(s)
         self.dijkstra_runs += 1
+        ok = True
         for position in range(self.A):  # the unique attached targets
+            if position == s:
+                if not self.self_loop_rule:
+                    continue  # igraph's [] for the source: nothing stored (:1815)
+                if self.kind[s, s] == 0:
+                    ok = False  # [s] without a self-loop: get_eid fails (:1490-1495), the run is FALSE
+                    continue
             if self.kind[s, position] == 0:  # igraph returns an empty path: nothing stored
                 continue
             self._store(False, s, position)
-        return True
+        return ok
 
     # ---------------------------------------------------------------- :1969-2051
     def get_path_entry(self, s, t):
@@ -104,6 +125,15 @@ class RefPathCache:
             if success:  # :2033-2038, directed or not
                 path = self._from_cache(s, t) or self._from_cache(t, s)
         return path
+
+
+def entry_value(model, path, lat, rel):
+    """(latency, reliability) of the cached Path `path` = (row, column): the matrices' entry,
+    or the self-path rule's value for a self pair that rule cached"""
+    si, sj = path
+    if si == sj and si in model.self_claimed:
+        return float(model.self_lat[si]), float(model.self_rel[si])
+    return float(lat[si, sj]), float(rel[si, sj])
 
 
 def adjacency_of(g, attached=None):

@@ -620,12 +620,13 @@ __device__ __forceinline__ void push_visit(const int32_t* __restrict__ in_src, c
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const double c = du + w[k];
-            bool imp = on && e + k < end && c < dv[k];
+            const bool imp = on && e + k < end && c < dv[k];
             if (imp) {
-                const unsigned long long cb = (unsigned long long)__double_as_longlong(c);
-                const unsigned long long old = __hip_atomic_fetch_min(gen_u64(B.D + (size_t)v[k] * KL + lane), cb,
-                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                imp = cb < old;
+                // no-return atomic: the lane is marked changed whether or not a concurrent push
+                // got lower first (it then pushes its current, lower value next round: harmless)
+                (void)__hip_atomic_fetch_min(gen_u64(B.D + (size_t)v[k] * KL + lane),
+                                             (unsigned long long)__double_as_longlong(c), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
             }
             const unsigned long long bal = __ballot(imp);
             if (bal) {
@@ -710,6 +711,7 @@ __global__ __launch_bounds__(256) void k_pred_pass(const int64_t* __restrict__ i
     if (__ballot(src)) {  // a source vertex of some lane: fold round 1 starts at its out-neighbours
         for (int64_t x = in_ptr[v] + lane; x < in_ptr[v + 1]; x += 64) B.act1[in_src[x]] = 1;
     }
+    if (!(dv < dinf()) && !src) B.H[idx] = 0u;  // unreached: never folded (k_fold tests H alone)
     if (!__ballot(dv < dinf() && !src)) return;
     const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
     const gdouble* Dl = B.D + lane;
@@ -749,7 +751,7 @@ __device__ __forceinline__ void fold_visit(const int32_t* __restrict__ in_src, c
     const size_t idx = (size_t)v * KL + lane;
     const uint32_t hv = B.H[idx];
     bool fin = false;
-    if ((hv & HMASK) == HNOT && B.D[idx] < dinf()) {
+    if ((hv & HMASK) == HNOT) {
         const int32_t arc = B.P[idx];
         const int32_t u = in_src[arc];
         const size_t uidx = (size_t)u * KL + lane;
@@ -4665,6 +4667,33 @@ int shadowtopo_host_alloc(size_t bytes, void** out) {
 
 void shadowtopo_host_free(void* p) {
     if (p) (void)hipHostFree(p);
+}
+
+int shadowtopo_self_rule_paths(shadowtopo_engine* eng, double* lat, double* rel, uint8_t* kind) {
+    if (!eng || !lat || !rel || !kind) return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    if (!eng->d_attached) return fail(SHADOWTOPO_ESTATE, "set_attached first");
+    HIP_TRY(hipSetDevice(eng->device));
+    const int32_t A = eng->A;
+    if (A == 0) return SHADOWTOPO_OK;
+    // k_self with the version-independent rule, whatever the engine's self-pair flag
+    GraphDev g = eng->g;
+    g.flags &= ~SHADOWTOPO_F_SELF_DIJKSTRA_LOOP;
+    void* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, (size_t)A * 21));
+    double* dl = (double*)buf;
+    double* dr = dl + A;
+    uint32_t* dh = (uint32_t*)(dr + A);
+    uint8_t* dk = (uint8_t*)(dh + A);
+    hipStream_t s = eng->own_stream;
+    hipLaunchKernelGGL(k_self, dim3((A + 3) / 4), dim3(256), 0, s, g, eng->d_attached, A, dl, dr, dh, dk);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(lat, dl, sizeof(double) * A, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(rel, dr, sizeof(double) * A, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(kind, dk, A, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(buf);
+    if (e != hipSuccess) return fail(SHADOWTOPO_EDEVICE, "self-rule paths: %s", hipGetErrorString(e));
+    return SHADOWTOPO_OK;
 }
 
 int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out) {

@@ -173,6 +173,12 @@ typedef struct matrix {
      * from it, reverse copies included) */
     _Atomic int32_t partial;
     int32_t fill_col;
+    /* self_rule (the [s]-path igraph): the matrix diagonal holds the [s] path's value; these
+     * hold the version-independent self-path rule's per attached index, which a self pair
+     * takes when a query (s, s) cached it before s's Dijkstra did (else NULL) */
+    double* srl_lat;
+    double* srl_rel;
+    uint8_t* srl_kind;
     struct matrix* next; /* retired matrices (readers may still hold them) */
 } matrix;
 
@@ -691,6 +697,9 @@ static void free_matrix(matrix* m) {
     mat_free(m, m->lat);
     mat_free(m, m->rel);
     mat_free(m, m->kind);
+    free(m->srl_lat);
+    free(m->srl_rel);
+    free(m->srl_kind);
     free(m);
 }
 
@@ -832,17 +841,28 @@ static int cached_dir(const Topology* top, int32_t i, int32_t j) {
 
 /* cache (i, j) unless the pair is cached already in either direction (directed graphs too,
  * topology.c:1311-1317); 1 when this call stored it */
-static int cache_claim(Topology* top, int32_t i, int32_t j) {
+static int cache_claim_bit(Topology* top, int32_t i, int32_t j, unsigned diag_bit) {
     int sh;
     const int32_t a = i < j ? i : j, b = i < j ? j : i;
     _Atomic uint64_t* w = cell_word(top, a, b, 1, &sh);
     if (!w) return 0;
-    const uint64_t bit = (i <= j ? 1ull : 2ull) << sh;
+    /* a self pair's cell: bit 0 = cached by s's Dijkstra (the [s] path) or by the default
+     * rule's self path, bit 1 = cached by the self-path rule under self_rule */
+    const uint64_t bit = (uint64_t)(i == j ? diag_bit : (i < j ? 1u : 2u)) << sh;
     uint64_t cur = atomic_load_explicit(w, memory_order_acquire);
     while (!((cur >> sh) & 3u))
         if (atomic_compare_exchange_weak_explicit(w, &cur, cur | bit, memory_order_acq_rel, memory_order_acquire))
             return 1;
     return 0;
+}
+static int cache_claim(Topology* top, int32_t i, int32_t j) { return cache_claim_bit(top, i, j, 1u); }
+
+/* the self pair (i, i) was cached by the self-path rule under self_rule: it reads the
+ * matrix's srl_* values instead of the diagonal */
+static int diag_self_rule(const Topology* top, int32_t i) {
+    int sh;
+    _Atomic uint64_t* w = cell_word((Topology*)top, i, i, 0, &sh);
+    return w && ((atomic_load_explicit(w, memory_order_acquire) >> sh) & 2u);
 }
 
 /* matrix cells are read by the getters while a late attach's fill_old_rows rewrites
@@ -861,13 +881,14 @@ static inline void cell_d_store(double* p, double d) {
 static inline uint8_t cell_k(const uint8_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 
 static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix* m, int32_t i, int32_t j,
-                         uint64_t count, char* buf, size_t len) {
-    /* path_toString, path.c:62-75 */
+                         int srl, uint64_t count, char* buf, size_t len) {
+    /* path_toString, path.c:62-75 (srl: a self pair cached by the self-path rule under
+     * self_rule, whose values are the matrix's srl_*) */
     size_t o = (size_t)i * m->A + j;
     snprintf(buf, len,
              "SourceIndex=%ld DestinationIndex=%ld Latency=%f Reliability=%f PacketCount=%lu isDirect=%s", (long)s,
-             (long)t, cell_d(&m->lat[o]), cell_d(&m->rel[o]), (unsigned long)count,
-             cell_k(&m->kind[o]) == SHADOWTOPO_KIND_DIRECT ? "True" : "False");
+             (long)t, srl ? m->srl_lat[i] : cell_d(&m->lat[o]), srl ? m->srl_rel[i] : cell_d(&m->rel[o]),
+             (unsigned long)count, (!srl && cell_k(&m->kind[o]) == SHADOWTOPO_KIND_DIRECT) ? "True" : "False");
     (void)top;
     return buf;
 }
@@ -892,8 +913,9 @@ void topology_free(Topology* top) {
                         if (i >= m->A || j >= m->A) continue;
                         uint64_t c = counter_peek(top, i, j);
                         int32_t s = top->attached[i], t = top->attached[j];
+                        const int srl = i == j && (bit & 1) && m->srl_lat != NULL;
                         st_info("Found path %s%s%s in cache: %s", vid(top, s), top->directed ? "->" : "<->",
-                                vid(top, t), path_string(top, s, t, m, i, j, c ? c - 1 : 0, buf, sizeof buf));
+                                vid(top, t), path_string(top, s, t, m, i, j, srl, c ? c - 1 : 0, buf, sizeof buf));
                     }
                 }
             }
@@ -1500,6 +1522,17 @@ static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A,
         free_matrix(m);
         return NULL;
     }
+    if (top->self_rule) {
+        m->srl_lat = malloc(sizeof(double) * (size_t)(A ? A : 1));
+        m->srl_rel = malloc(sizeof(double) * (size_t)(A ? A : 1));
+        m->srl_kind = malloc((size_t)(A ? A : 1));
+        if (!m->srl_lat || !m->srl_rel || !m->srl_kind ||
+            shadowtopo_self_rule_paths(top->engs[0], m->srl_lat, m->srl_rel, m->srl_kind) != SHADOWTOPO_OK) {
+            st_critical("self-path rule values: %s", shadowtopo_last_error());
+            free_matrix(m);
+            return NULL;
+        }
+    }
     for (int32_t i = 0; i < A0; i++) {
         const size_t src = (size_t)i * (size_t)A0, dst = (size_t)i * (size_t)A;
         memcpy(m->lat + dst, old->lat + src, sizeof(double) * (size_t)A0);
@@ -1673,11 +1706,14 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
                 stored = 1;
             }
         } else if (i == j) {
+            /* _topology_computeShortestPathToSelf (topology.c:1545-1653); under self_rule the
+             * diagonal holds the [s] path's value, the self rule's is in srl_* */
             atomic_fetch_add_explicit(&top->self_count, 1, memory_order_relaxed);
-            if (k == SHADOWTOPO_KIND_NONE)
+            const uint8_t ks = top->self_rule ? m->srl_kind[i] : k;
+            if (ks == SHADOWTOPO_KIND_NONE)
                 success = 0; /* no incident edge: no self path */
-            else if (cache_claim(top, i, i)) {
-                mn = cell_d(&m->lat[(size_t)i * A + i]);
+            else if (cache_claim_bit(top, i, i, top->self_rule ? 2u : 1u)) {
+                mn = top->self_rule ? m->srl_lat[i] : cell_d(&m->lat[(size_t)i * A + i]);
                 stored = 1;
             }
         } else {
@@ -1691,6 +1727,10 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
             const uint8_t* kr = m->kind + (size_t)i * A;
             const int32_t t0 = mine ? 0 : j, t1 = mine ? A : j + 1;
             for (int32_t t = t0; t < t1; t++) {
+                /* the source itself: the igraph that returns [] for it stores nothing
+                 * (topology.c:1815, the default rule); the one that returns [s] stores its
+                 * self-loop path (self_rule) */
+                if (t == i && !top->self_rule) continue;
                 /* reachable targets only (an empty igraph path is never stored); a pair whose
                  * rule is the direct edge is not stored from a Dijkstra run */
                 const uint8_t kt = cell_k(&kr[t]);
@@ -1700,6 +1740,10 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
                 if (!stored || l < mn) mn = l;
                 stored++;
             }
+            /* [s] without a self-loop: _topology_computePathProperties fails for the source's
+             * own target, so every Dijkstra run of s returns FALSE (:1857) after storing the
+             * rest, and the query fails (:2040-2045) */
+            if (top->self_rule && cell_k(&kr[i]) == SHADOWTOPO_KIND_NONE) success = 0;
         }
         if (stored) {
             atomic_fetch_add_explicit(&top->cached_paths, stored, memory_order_relaxed);
@@ -1732,7 +1776,8 @@ static int32_t connected_vertex(Topology* top, Address* a) {
 }
 
 /* _topology_getPathEntry, topology.c:1969-2051: returns the matrix and pair offset */
-static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off, int32_t* ri, int32_t* rj) {
+static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off, int32_t* ri, int32_t* rj,
+                          int* srl) {
     int32_t vs = connected_vertex(top, src);
     if (vs < 0) {
         st_critical("invalid vertex %i, source address %s is not connected to topology", (int)vs,
@@ -1753,6 +1798,7 @@ static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off
         *off = (size_t)si * (size_t)m->A + (size_t)sj;
         if (ri) *ri = si;
         if (rj) *rj = sj;
+        if (srl) *srl = si == sj && m->srl_lat && diag_self_rule(top, si);
         return m;
     }
     st_error("unable to find path between node %s at %s (vertex %i) and node %s at %s (vertex %i)",
@@ -1762,14 +1808,18 @@ static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off
 
 double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddress) {
     size_t o;
-    matrix* m = path_entry(top, srcAddress, dstAddress, &o, NULL, NULL);
-    return m ? cell_d(&m->lat[o]) : -1.0;
+    int32_t i;
+    int srl = 0;
+    matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, NULL, &srl);
+    return m ? (srl ? m->srl_lat[i] : cell_d(&m->lat[o])) : -1.0;
 }
 
 double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress) {
     size_t o;
-    matrix* m = path_entry(top, srcAddress, dstAddress, &o, NULL, NULL);
-    return m ? cell_d(&m->rel[o]) : -1.0;
+    int32_t i;
+    int srl = 0;
+    matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, NULL, &srl);
+    return m ? (srl ? m->srl_rel[i] : cell_d(&m->rel[o])) : -1.0;
 }
 
 int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress) {
@@ -1779,7 +1829,7 @@ int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress)
 void topology_incrementPathPacketCounter(Topology* top, Address* srcAddress, Address* dstAddress) {
     size_t o;
     int32_t i, j;
-    matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, &j);
+    matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, &j, NULL);
     if (!m) {
         st_error("unable to find path between node %s and node %s", address_toString(srcAddress),
                  address_toString(dstAddress));

@@ -57,7 +57,7 @@ ENGINE_SYMBOLS = (
     "shadowtopo_device_count", "shadowtopo_prepare", "shadowtopo_last_error", "shadowtopo_create", "shadowtopo_destroy",
     "shadowtopo_set_attached", "shadowtopo_set_option", "shadowtopo_compute_rows", "shadowtopo_sssp",
     "shadowtopo_get_stats", "shadowtopo_reset_stats", "shadowtopo_is_complete", "shadowtopo_get_eid",
-    "shadowtopo_host_alloc", "shadowtopo_host_free",
+    "shadowtopo_host_alloc", "shadowtopo_host_free", "shadowtopo_self_rule_paths",
 )
 
 
@@ -120,6 +120,7 @@ def lib():
         L.shadowtopo_compute_rows.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int32, vp]
         L.shadowtopo_sssp.argtypes = [vp, vp, ctypes.c_int32, vp, vp, vp, vp]
         L.shadowtopo_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+        L.shadowtopo_self_rule_paths.argtypes = [vp, vp, vp, vp]
         L.shadowtopo_reset_stats.argtypes = [vp]
         L.shadowtopo_is_complete.argtypes = [vp]
         L.shadowtopo_get_eid.restype = ctypes.c_int64
@@ -283,6 +284,14 @@ class Engine:
         tie = np.empty((k, self.n), np.uint8)
         _check(lib().shadowtopo_sssp(self._h, _ptr(s), k, _ptr(dist), _ptr(pred), _ptr(hops), _ptr(tie)))
         return dist, pred, hops, tie
+
+    def self_rule_paths(self):
+        """the version-independent self-path rule for every attached vertex (lat, rel, kind)"""
+        lat = np.empty(self.A, np.float64)
+        rel = np.empty(self.A, np.float64)
+        kind = np.empty(self.A, np.uint8)
+        _check(lib().shadowtopo_self_rule_paths(self._h, _ptr(lat), _ptr(rel), _ptr(kind)))
+        return lat, rel, kind
 
     def stats(self):
         st = Stats()

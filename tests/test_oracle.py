@@ -223,10 +223,26 @@ def test_path_cache_model_reference_quirks():
     assert und.get_path_entry(1, 0) == (1, 0)
     assert und.get_path_entry(0, 1) == (1, 0)  # served by the reverse Path
     assert und.get_path_entry(0, 2) == (0, 2)  # source 0's Dijkstra: its own row
-    # source 1's run stored (1,0)=6 then (1,1)=2: two upcalls; source 0's run nothing lower
-    assert und.dijkstra_runs == 2 and und.upcalls == [6.0, 2.0] and und.min_latency == 2.0
-    assert und.get_path_entry(0, 0) == (0, 0) and und.self_paths == 0  # cached by source 0's run
-    assert und.get_path_entry(2, 2) == (2, 2) and und.self_paths == 1  # a self-path run
+    # source 1's run stored (1,0)=6 and (1,2)=4, not (1,1): igraph's path to the source itself
+    # is [] (topology.c:1815); source 0's run stored nothing lower
+    assert und.dijkstra_runs == 2 and und.upcalls == [6.0, 4.0] and und.min_latency == 4.0
+    assert (0, 0) not in und.cache and (1, 1) not in und.cache
+    assert und.get_path_entry(0, 0) == (0, 0) and und.self_paths == 1  # a self-path run
+    assert und.upcalls == [6.0, 4.0, 2.0]
+    assert und.get_path_entry(0, 0) == (0, 0) and und.self_paths == 1  # now a hit
+    # the [s]-path igraph (self_loop_rule): the run stores the source's self-loop path (the
+    # diagonal); a query (s, s) that comes first caches the self-path rule's value instead,
+    # and a source without a self-loop fails its Dijkstra run (after storing the rest)
+    slat, skind = np.array([9.0, 8.0, 7.0]), np.array([2, 2, 2])
+    lk = kind.copy()
+    lk[2, 2] = 0  # vertex 2 has no self-loop
+    sl = RefPathCache(lat, lk, directed=False, complete=False, prefer_direct=False, adjacent=adj,
+                      self_loop_rule=True, self_lat=slat, self_kind=skind)
+    assert sl.get_path_entry(0, 0) == (0, 0) and 0 in sl.self_claimed and sl.cache[(0, 0)] == 9.0
+    assert sl.get_path_entry(1, 2) == (1, 2) and (1, 1) in sl.cache and 1 not in sl.self_claimed
+    assert sl.cache[(1, 1)] == 2.0  # the [s] path's value
+    assert sl.get_path_entry(2, 0) is None and (2, 0) in sl.cache  # stored, but the run failed
+    assert sl.get_path_entry(2, 0) == (2, 0)  # a hit afterwards
     d = RefPathCache(lat, kind, directed=True, complete=False, prefer_direct=False, adjacent=adj)
     assert d.get_path_entry(1, 0) == (1, 0) and d.dijkstra_runs == 1
     assert d.get_path_entry(0, 1) == (1, 0) and d.dijkstra_runs == 2  # the reverse Path

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from oracle.path_cache_ref import RefPathCache, adjacency_of
+from oracle.path_cache_ref import RefPathCache, adjacency_of, entry_value
 from paritylib import oracle_matrix
 from shadow_amd import synth
 from shadow_amd import topology as T
@@ -346,6 +346,61 @@ def test_c_harness_lookups_under_threads(tmp_path):
     res = run_harness(build_harness(tmp_path), path, 300, 8, 20000, 0)
     assert res["compute_failed"] == 0 and res["routable"] > 0
     assert res["ns_per_call_per_thread"] > 0
+
+
+def test_self_pairs_follow_query_order_under_the_s_path_rule(tmp_path):
+    """The [s]-path igraph (topology_hip_set_self_rule(1)): a self pair is
+    cached by whichever of the two rules runs first -- a query (s, s) caches the self-path
+    rule's value (topology.c:1545-1653), s's Dijkstra run caches its self-loop path
+    (:1456-1499); a source without a self-loop fails its Dijkstra run after storing the
+    rest, so the first query from it fails and the next one hits.  Driven in both orders
+    against the cache model (oracle/path_cache_ref.py), values, counts and upcalls included."""
+    g = synth.random_sparse(V=120, avg_deg=4, seed=52, A=30)
+    noloop = [int(g.attached[3]), int(g.attached[7])]  # two attached vertices lose their self-loop
+    keep = ~((g.src == g.dst) & np.isin(g.src, noloop))
+    g.src, g.dst, g.latency, g.packetloss = g.src[keep], g.dst[keep], g.latency[keep], g.packetloss[keep]
+    lat_o, rel_o, _, kind_o, og = oracle_matrix(g, self_loop_rule=True)
+    sp = [og.self_path(int(v)) for v in g.attached]
+    model = ref_cache(g, lat_o, kind_o)
+    model.self_loop_rule = True
+    model.self_lat = np.array([x[0] if x else -1.0 for x in sp])
+    model.self_rel = np.array([x[1] if x else -1.0 for x in sp])
+    model.self_kind = np.array([2 if x else 0 for x in sp])
+    assert kind_o[3, 3] == 0 and kind_o[0, 0] == 3 and model.self_lat[0] != lat_o[0, 0]
+    va, ips = with_vertex_ips(g)
+    top = T.Topology.new(write(tmp_path, "s.xml", synth.to_graphml(g, extra_vattr=va)))
+    top.set_self_rule(True)
+    hosts = attach_all(top, ips, g.attached)
+
+    def q(i, j):
+        a, b = hosts[i], hosts[j]
+        path = model.get_path_entry(i, j)
+        got = top.getLatency(a, b)
+        path2 = model.get_path_entry(i, j)
+        gotr = top.getReliability(a, b)
+        if path is None:
+            assert got == -1.0, (i, j)
+        else:
+            assert got == entry_value(model, path, lat_o, rel_o)[0], (i, j, path)
+        if path2 is None:
+            assert gotr == -1.0, (i, j)
+        else:
+            assert gotr == entry_value(model, path2, lat_o, rel_o)[1], (i, j, path2)
+        return path
+
+    assert q(0, 0) == (0, 0) and 0 in model.self_claimed  # the self rule first
+    q(0, 5)  # 0's Dijkstra: (0, 0) stays the self rule's
+    assert top.getLatency(hosts[0], hosts[0]) == model.self_lat[0]
+    model.get_path_entry(0, 0)
+    q(1, 5)  # 1's Dijkstra first: (1, 1) is its self-loop path
+    assert q(1, 1) == (1, 1) and 1 not in model.self_claimed
+    assert q(3, 4) is None  # no self-loop: the run fails, after storing (3, t)
+    assert q(3, 4) == (3, 4)  # a hit
+    for i in range(len(hosts)):
+        for j in range(len(hosts)):
+            q(i, j)
+    check_cache_state(top, model)
+    top.free()
 
 
 def test_lock_free_cache_under_racing_workers(tmp_path):
