@@ -1,0 +1,244 @@
+/*
+ * shadowtopo.h -- C ABI of libshadowtopo_hip, the MI355X (gfx950) engine behind
+ * Shadow's topology path computation.
+ *
+ * It replaces, below the unchanged topology.h API (topology_hip.h in this repo), the
+ * reference's igraph-based per-source lazy path computation:
+ *   - igraph_get_shortest_paths_dijkstra call      /root/reference/src/main/routing/topology.c:1754-1775
+ *   - _topology_computeSourcePaths                  topology.c:1655-1875
+ *   - _topology_computePathProperties               topology.c:1407-1523
+ *   - _topology_computeShortestPathToSelf           topology.c:1545-1653
+ *   - _topology_lookupDirectPath                    topology.c:1877-1927
+ *   - the dispatch of _topology_getPathEntry        topology.c:2019-2031
+ *   - the two-level path cache                      topology.c:42-47, 1284-1386
+ * with one eager, batched, many-source computation of the attached-pair matrix
+ * (A x A latency / reliability / hop count) on the GPU.
+ *
+ * Plain C: int status codes, no exceptions, caller-owned buffers, no torch types.
+ * Not thread-safe per engine: callers serialise calls on one engine (the topology shim
+ * does so with a mutex / pthread_once).
+ */
+#ifndef SHADOWTOPO_H
+#define SHADOWTOPO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct shadowtopo_engine shadowtopo_engine;
+
+/* status codes */
+#define SHADOWTOPO_OK 0
+#define SHADOWTOPO_EINVAL (-1)   /* bad argument / malformed graph */
+#define SHADOWTOPO_ENOMEM (-2)   /* host or device allocation failed */
+#define SHADOWTOPO_EDEVICE (-3)  /* HIP runtime error, or no GPU */
+#define SHADOWTOPO_ESTATE (-4)   /* call out of order (e.g. compute before set_attached) */
+#define SHADOWTOPO_EINTERNAL (-5) /* iteration guard tripped */
+
+/* graph flags (topology.c:751-790: isDirected, isComplete, prefersDirectPaths) */
+#define SHADOWTOPO_F_DIRECTED 0x1u
+#define SHADOWTOPO_F_COMPLETE 0x2u
+#define SHADOWTOPO_F_PREFER_DIRECT 0x4u
+/* alternative self-pair rule: the [s] path igraph >= 0.7 returns for the
+ * source itself, i.e. the source's self-loop edge (topology.c:1456-1499); default is the
+ * version-independent _topology_computeShortestPathToSelf rule (topology.c:1545-1653). */
+#define SHADOWTOPO_F_SELF_DIJKSTRA_LOOP 0x8u
+/* let the engine decide F_COMPLETE with the reference's rule (_topology_isComplete,
+ * topology.c:450-552) instead of trusting the caller's F_COMPLETE bit */
+#define SHADOWTOPO_F_AUTO_COMPLETE 0x10u
+/* relaxation layout: default picks the dense-tile form when arcs >= V^2/4 (and the
+ * V x V tables fit), the CSR form otherwise; these force one (testing / tuning) */
+#define SHADOWTOPO_F_FORCE_DENSE 0x20u
+#define SHADOWTOPO_F_FORCE_CSR 0x40u
+
+/* where compute_rows' output buffers live */
+#define SHADOWTOPO_MEM_HOST 0
+#define SHADOWTOPO_MEM_DEVICE 1
+
+/* per-pair kind codes (optional output) */
+#define SHADOWTOPO_KIND_NONE 0     /* unroutable: lat = rel = -1 (topology.c:2073, 2085) */
+#define SHADOWTOPO_KIND_DIRECT 1   /* _topology_lookupDirectPath, isDirect = TRUE */
+#define SHADOWTOPO_KIND_SELF 2     /* _topology_computeShortestPathToSelf */
+#define SHADOWTOPO_KIND_DIJKSTRA 3 /* shortest path */
+
+/* options for shadowtopo_set_option */
+#define SHADOWTOPO_OPT_BATCHES_IN_FLIGHT 1 /* source batches (64 sources each) relaxed together */
+#define SHADOWTOPO_OPT_TIMING 2            /* 1 = record HIP events around every relax launch */
+#define SHADOWTOPO_OPT_MAX_ROUNDS 3        /* iteration guard (default 4*V+64) */
+#define SHADOWTOPO_OPT_FORCE_REPLAY 4      /* 1 = run the heap-exact kernel for every source (testing) */
+#define SHADOWTOPO_OPT_PROFILE 5           /* 1 = count visits and changes per round (see shadowtopo_stats) */
+#define SHADOWTOPO_OPT_DENSE_VARIANT 6     /* dense relax kernels: SHADOWTOPO_DENSE_F32 (default) or _F64 */
+/* dense relaxation kernels (both exact; F32 pre-filters every candidate in f32 against a
+ * conservative threshold and re-evaluates the survivors in f64, F64 evaluates everything in f64) */
+#define SHADOWTOPO_DENSE_F32 0
+#define SHADOWTOPO_DENSE_F64 1
+#define SHADOWTOPO_OPT_DELTA_PERMILLE 7    /* dense: a batch whose last round changed <= this many per mille of its
+                                              (vertex, source) pairs gets a change-mask delta round instead of a full
+                                              sweep (default 125; 0 = always full sweeps) */
+#define SHADOWTOPO_OPT_CSR_VARIANT 8       /* sparse relax kernel: SHADOWTOPO_CSR_FULL (default), _MASKED, _FILTERED or _DELTA */
+#define SHADOWTOPO_OPT_DENSE_BATCHES_PER_WAVE 9 /* f32 dense full sweep: batches one wave filters at once (1 = default, 2, 4) */
+#define SHADOWTOPO_OPT_SOURCE_ORDER 10     /* CSR rounds: 1 (default) = sources batched in locality order (Hilbert
+                                              order of the top two principal axes of the distances to eight
+                                              attached landmarks), 0 = attach order.
+                                              Results are identical; only which sources share a wave changes. */
+#define SHADOWTOPO_OPT_DENSE_SEED 11       /* dense round 0: 1 (default) = one fused pass writing every (vertex,
+                                              source) state once (k_seed_dense_t), 0 = init, source seed and arc seed
+                                              kernels in turn. Results are identical. */
+#define SHADOWTOPO_OPT_DENSE_PRUNE 12      /* f32 dense full sweep: 1 (default) = rows and destinations in a vertex
+                                              locality order (the same landmark embedding over all vertices, built on
+                                              the first computation), sources batched in locality order, and a wave
+                                              skips a 32-row chunk when no lane can pass any of its rows (bound: min
+                                              D32 of the chunk vs max over its columns of threshold - the
+                                              column's min W32 over the chunk);
+                                              0 = every chunk filtered, original order. Results are identical. */
+
+#define SHADOWTOPO_OPT_WORKLIST 14         /* CSR FULL rounds: 1 (default) = over compacted frontier worklists (one
+                                              wave per active (vertex, batch) pair) when under half the pairs are
+                                              active, the grid otherwise; 2 = worklists always; 0 = one wave per pair
+                                              of the grid */
+#define SHADOWTOPO_OPT_GRID_X 15           /* testing: largest x dimension (blocks, a multiple of 8) of the sparse
+                                              relax grids before they go 2-D (default 2^23: 2^31 work-items per
+                                              launch, under the dispatch packet's 32-bit count) */
+#define SHADOWTOPO_OPT_PRUNE_PENDANT 16   /* CSR rows of an undirected graph: 1 (default) = relax without the
+                                              pendant trees that hold no attached vertex (peeled non-attached
+                                              vertices with one neighbour; they lie on no attached-pair path);
+                                              0 = every vertex. Results are identical. */
+#define SHADOWTOPO_OPT_DEVICE_ROUNDS 17   /* CSR FULL worklist rounds: 1 (default) = driven from the device (item
+                                              counts read back once per 8 rounds) when batches x vertices <= 4 Mi,
+                                              2 = always, 0 = never (one host read-back per round). Results are
+                                              identical. */
+#define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (40 % of free HBM) this
+                                              engine may take (default 1000); engines sharing one device split it */
+
+/* sparse (CSR) relaxation rounds (all exact, same fixed point):
+ *   FULL (default): recompute every active vertex's minimum over all its in-arcs' 512-byte
+ *     distance rows (k_relax; rounds with few active pairs run over frontier worklists);
+ *   MASKED: over frontier worklists, fold only the (in-neighbour, source) pairs whose state
+ *     changed, found through per-vertex round-stamped change records; the wave compacts the
+ *     changed in-arcs with a ballot and loads their distance rows masked to the changed
+ *     lanes; the vertex's own state is read only for lanes with a candidate (k_relax_cm);
+ *   FILTERED: fold only the in-neighbours whose state changed, found through round stamps
+ *     in 256-byte f32 key rows, settling the f32-filter survivors in f64 (k_relax_st);
+ *   DELTA: fold only changed in-neighbours, found through 64-bit change masks, in f64,
+ *     over the whole grid.
+ * MASKED, FILTERED and DELTA read fewer rows but issue more instructions: on C4 MASKED
+ * fetches 12 % fewer bytes at 2.2x the VALU instructions and runs 1.3x longer than FULL
+ * (DESIGN.md 4); they are kept as cross-checks. */
+#define SHADOWTOPO_CSR_DELTA 0
+#define SHADOWTOPO_CSR_FULL 1
+#define SHADOWTOPO_CSR_FILTERED 2
+#define SHADOWTOPO_CSR_MASKED 3
+
+typedef struct shadowtopo_stats {
+    int64_t n_vertices;
+    int64_t n_edges;
+    int64_t n_arcs;          /* non-loop arcs of the relaxation in-CSR after merging parallel edges */
+    int64_t n_attached;
+    int64_t sources;         /* source rows computed since the last reset */
+    int64_t batches;
+    int64_t rounds;          /* relaxation rounds (summed over batch groups) */
+    int64_t relax_launches;
+    int64_t replayed_sources;/* sources resolved by the heap-exact kernel (tie-tainted) */
+    int64_t tainted_pairs;
+    double relax_ms;         /* HIP-event time of relax launches (OPT_TIMING=1) */
+    double compose_ms;
+    double replay_ms;
+    double wall_ms;          /* host wall time inside compute calls */
+    int32_t device;
+    int32_t multigraph;
+    int32_t dense;           /* 1 = dense-tile relaxation in use */
+    int32_t reserved;
+    int64_t visits;          /* OPT_PROFILE, CSR: active (vertex, batch) waves processed */
+    int64_t changes;         /* OPT_PROFILE: CSR: (vertex, batch) waves that changed;
+                                dense: (vertex, source) pairs that changed */
+    int64_t full_sweeps;     /* dense: full-sweep relax launches */
+    int64_t delta_sweeps;    /* dense: change-mask (delta) relax launches */
+    double full_ms;          /* OPT_TIMING: HIP-event time of the dense full sweeps (k_relax_dense) */
+    double delta_ms;         /* OPT_TIMING: HIP-event time of the delta rounds (k_relax_dense_delta) */
+    /* launch shapes, for the per-launch rooflines (bench.py) */
+    int64_t full_batches;    /* dense: batches swept by full-sweep launches (summed over launches) */
+    int64_t full_changes;    /* dense: (vertex, source) pairs those full sweeps changed */
+    int64_t relax_batches;   /* sparse: batches in flight, summed over relax launches */
+    int64_t wl_launches;     /* sparse: relax launches over frontier worklists (k_relax_wl), included above */
+    double wl_ms;            /* OPT_TIMING: their HIP-event time, included in relax_ms */
+    int64_t sparse_deltas;   /* dense: delta launches that walked live-chunk lists only */
+    double self_ms;          /* host wall time of the self-path rule (k_self), once per attached set
+                                (the reference's selfPathTotalTime, topology.c:1608-1617) */
+    int64_t self_paths;      /* attached vertices the self-path rule ran for */
+    int64_t pruned_deltas;   /* dense: delta launches in the locality order with chunk bounds (OPT_DENSE_PRUNE) */
+    int64_t pruned_vertices; /* CSR: vertices the relaxation view leaves out (OPT_PRUNE_PENDANT) */
+} shadowtopo_stats;
+
+/* Number of visible HIP devices (0 if none). */
+int shadowtopo_device_count(void);
+
+/* Message for the last failing call on this thread. */
+const char* shadowtopo_last_error(void);
+
+/*
+ * Build the device-resident graph from the GraphML edge list, in the reference's edge
+ * order (edge index = <edge> element order, igraph_read_graph_graphml at topology.c:386).
+ *   edge_source/edge_target : vertex indices in [0, n_vertices)
+ *   edge_latency            : ms, > 0 (validated as topology.c:1066-1082 does)
+ *   edge_packetloss         : in [0,1]
+ *   vertex_packetloss       : nullable; NaN = attribute absent on that vertex
+ *                             (topology.c:330-347, 1441-1462)
+ *   flags                   : SHADOWTOPO_F_*
+ *   device                  : HIP device ordinal
+ */
+int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_source, const int32_t* edge_target,
+                      const double* edge_latency, const double* edge_packetloss, const double* vertex_packetloss,
+                      uint32_t flags, int32_t device, shadowtopo_engine** out);
+
+void shadowtopo_destroy(shadowtopo_engine* eng);
+
+/* The unique attached vertices (sources and targets), topology.c:1525-1543.  Row/column
+ * i of every matrix refers to attached[i]. */
+int shadowtopo_set_attached(shadowtopo_engine* eng, const int32_t* attached, int32_t count);
+
+int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value);
+
+/*
+ * Attached-pair rows [row_begin, row_end) x count: lat (ms), rel, hops, kind.
+ * Buffers are row-major with leading dimension `count`; hops and kind may be NULL.
+ * mem = SHADOWTOPO_MEM_DEVICE: device pointers on the engine's device, written on
+ * `stream` (a hipStream_t, NULL = the engine's own stream); the call returns after the
+ * stream work is complete.  mem = SHADOWTOPO_MEM_HOST: host pointers; when they are all
+ * page-locked (shadowtopo_host_alloc) the rows are copied at full PCIe rate and a batch
+ * group's copy overlaps the next group's computation.
+ */
+int shadowtopo_compute_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
+                            uint32_t* hops, uint8_t* kind, int32_t mem, void* stream);
+
+/* Page-locked host memory that compute_rows copies into directly (from any device of the
+ * process); free with shadowtopo_host_free.  NULL-safe free. */
+int shadowtopo_host_alloc(size_t bytes, void** out);
+void shadowtopo_host_free(void* p);
+
+/*
+ * Parity tooling: full single-source results for arbitrary source vertices (row-major
+ * [n_sources][n_vertices], host buffers, any may be NULL): distance (f64, +inf if
+ * unreached), predecessor vertex (-1 for the source / unreached), hop count, and a
+ * tie flag (1 if the vertex's shortest-path tree path crosses a heap-order tie).
+ */
+int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_sources, double* dist, int32_t* pred,
+                    uint32_t* hops, uint8_t* tie);
+
+int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out);
+void shadowtopo_reset_stats(shadowtopo_engine* eng);
+
+/* effective completeness (caller's F_COMPLETE, or the reference rule under F_AUTO_COMPLETE) */
+int shadowtopo_is_complete(const shadowtopo_engine* eng);
+
+/* igraph_get_eid(directed = graph's, error = FALSE) as _topology_getEdgeHelper uses it
+ * (topology.c:401-444): lowest edge id joining (from, to), or -1. */
+int64_t shadowtopo_get_eid(const shadowtopo_engine* eng, int32_t from, int32_t to);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SHADOWTOPO_H */
