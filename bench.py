@@ -417,6 +417,7 @@ def main():
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
                     "chunk c's all-gather overlaps chunk c+1's computation")
+    ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--csr-variant", type=int, default=1, help="sparse rounds: 1 = pull (default), 2 = push (u64 atomicMin)")
@@ -475,6 +476,8 @@ def main():
     eng.set_option(E.OPT_DENSE_VARIANT, args.dense_variant)
     if args.dense_tb:
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
+    if args.dense_w16 >= 0:
+        eng.set_option(E.OPT_DENSE_W16, args.dense_w16)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
     if not eng.complete and args.csr_variant != 1:

@@ -115,6 +115,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                             changed row): 2 (default) = when the previous round changed at most
                                             1/64 of the delta batches' pairs, 1 = always, 0 = never. Results are
                                             identical. */
+#define SHADOWTOPO_OPT_DENSE_W16 20       /* pruned dense sweep: 1 = the chunk loop filters with 16-bit weights (fp16,
+                                            rounded down; half the LDS slab and the table), 0 (default) = f32.
+                                            Results are identical. */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (55 % of free HBM, at least 24 GB) this
                                               engine may take (default 1000); engines sharing one device split it */
 

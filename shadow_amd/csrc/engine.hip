@@ -989,8 +989,13 @@ constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FT
 // Occupancy: LDS (24 KB per block) allows 6 blocks = 6 waves per SIMD, and 80 VGPRs fit 6
 // (the kernel wants 82, i.e. 5 waves); waves_per_eu(6) spills 3 dwords outside the chunk
 // loop and buys a sixth wave: 3.89 -> 3.68 ms on C2 together with the unrolls below.
-template <int TDT, int XR, int TB, bool PR, int PH = 0, int NW = 4>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1 ? (NW == 8 ? 8 : 6) : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
+// H16 (OPT_DENSE_W16, chunk loop only): the filter key is the 16-bit W16p table (latency rounded
+// toward -inf to fp16, saturating at 65504; NaN if no arc) instead of W32p: half the LDS slab
+// (8 blocks per CU instead of 6) and half the table (202 MB on C2, inside the Infinity Cache).
+// W16 <= W32 <= w keeps the filter conservative; a passing row tightens the
+// thresholds with an upper bound of w (one fp16 ulp up; +inf past the saturation).
+template <int TDT, int XR, int TB, bool PR, int PH = 0, int NW = 4, bool H16 = false>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1 ? (NW == 8 || H16 ? 8 : 6) : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
                                                        int32_t nb, int32_t ntb, int32_t parity, int32_t thresh,
@@ -1020,11 +1025,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     // 8 waves per SIMD -- measured 3.57 vs 3.42-3.43 ms on C2, r03s: a block-wide chunk skip
     // then needs all 8 waves dead, so more chunks are staged.)
     static_assert(NW == 4 || (NW == 8 && PH == 1), "8-wave blocks only for the chunk loop");
+    static_assert(!H16 || (PH == 1 && PR && TB == 1 && NW == 4 && TDT == 8), "W16: the pruned chunk loop alone");
     constexpr int NT = 64 * NW;  // threads per block
     constexpr int BW = NW * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
-    __shared__ __attribute__((aligned(16))) float sW[2][SRS * BW];
+    __shared__ __attribute__((aligned(16))) float sW[2][H16 ? SRS * BW / 2 : SRS * BW];
     int32_t grp, vt;
     if (!xcd_tile(blockIdx.x, (nb + TB - 1) / TB, ntb, grp, vt)) return;  // block-uniform exits only (barriers below)
     const int32_t b0 = grp * TB;  // this block's TB batches
@@ -1095,6 +1101,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     constexpr int WQT = (SRS * WQ + NT - 1) / NT;  // float4 of W32 per thread
     static_assert(DQ * NT * 4 == SRS * KL, "the D32 chunk is whole float4s per thread");
     f4 pd[TB][DQ], pw[WQT];
+    // W16: a chunk's W16 slab is SRS rows x BW halves = SRS * BW / 8 16-byte pieces
+    constexpr int WQ16 = BW / 8;
+    constexpr int WQT16 = (SRS * WQ16 + NT - 1) / NT;
     // PR: the chunk's skip bounds (md: min D32 per lane and batch, mw: min W32 of the
     // wave's tile columns)
     float mdn[TB], mdc[TB], mwn[TDT], mwc[TDT];
@@ -1144,6 +1153,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
 #pragma unroll
             for (int t = 0; t < TDT; ++t) mwn[t] = minW[(size_t)c * ncol + v0 + t];
         }
+        if constexpr (H16) {
+#pragma unroll
+            for (int i = 0; i < WQT16; ++i) {
+                const int e = threadIdx.x + i * NT;
+                if (e < SRS * WQ16) {
+                    const int r = e / WQ16, c = e % WQ16;
+                    typedef __attribute__((address_space(1))) const uint16_t gu16;
+                    pw[i] = *(gf4*)((gu16*)W32 + (size_t)(u0 + r) * Vp + vb + c * 8);
+                }
+            }
+        } else {
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
             const int e = threadIdx.x + i * NT;
@@ -1152,16 +1172,25 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                 pw[i] = *(gf4*)((const gfloat*)W32 + (size_t)(u0 + r) * Vp + vb + c * 4);
             }
         }
+        }
     };
     auto stash = [&](int buf) {
 #pragma unroll
         for (int k = 0; k < TB; ++k)
 #pragma unroll
             for (int i = 0; i < DQ; ++i) *(f4*)&sD[buf][k][(threadIdx.x + i * NT) * 4] = pd[k][i];
+        if constexpr (H16) {
+#pragma unroll
+            for (int i = 0; i < WQT16; ++i) {
+                const int e = threadIdx.x + i * NT;
+                if (e < SRS * WQ16) *(f4*)&sW[buf][e * 4] = pw[i];
+            }
+        } else {
 #pragma unroll
         for (int i = 0; i < WQT; ++i) {
             const int e = threadIdx.x + i * NT;
             if (e < SRS * WQ) *(f4*)&sW[buf][e * 4] = pw[i];
+        }
         }
     };
     auto advance = [&]() {
@@ -1305,13 +1334,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         for (int k = 0; k < TB; ++k) hits[k] = 0;
         // PH 1 (the chunk loop alone has VGPRs to spare): each row's LDS reads are issued one
         // row ahead, so they are in flight while the previous row is filtered and votes
-        constexpr bool RP = PH == 1 && NW == 4;
+        constexpr bool RP = PH == 1 && NW == 4 && !H16;
         f4 wn[TDT / 4];
         float dn[TB];
+        // W16: the row's 8 halves (one 16-byte LDS read), widened to f32
+        auto w16_row = [&](int r, f4* out) {
+            typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+            typedef float f8 __attribute__((ext_vector_type(8)));
+            const h8 h = *(const h8*)((const uint16_t*)&sW[cur][0] + r * BW + wave * TDT);
+            const f8 f = __builtin_convertvector(h, f8);
+            out[0] = f4{f[0], f[1], f[2], f[3]};
+            out[1] = f4{f[4], f[5], f[6], f[7]};
+        };
         auto lds_row = [&](int r) {
+            if constexpr (H16) {
+                w16_row(r, wn);
+            } else {
             const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
 #pragma unroll
             for (int j = 0; j < TDT / 4; ++j) wn[j] = wr[j];
+            }
 #pragma unroll
             for (int k = 0; k < TB; ++k) dn[k] = sD[cur][k][r * KL + lane];
         };
@@ -1326,6 +1368,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
 #pragma unroll
                 for (int k = 0; k < TB; ++k) dk[k] = dn[k];
                 if (r + 1 < SRS) lds_row(r + 1);
+            } else if constexpr (H16) {
+                w16_row(r, w4);
+#pragma unroll
+                for (int k = 0; k < TB; ++k) dk[k] = sD[cur][k][r * KL + lane];
             } else {
                 const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
 #pragma unroll
@@ -1365,7 +1411,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                         for (int i = 0; i < 4; ++i) {
                             // branch-free (v_cndmask): an infinite or NaN candidate, or a bound
                             // that would wrap past +inf into a NaN pattern, leaves thr as it is
-                            const float c32 = du + wj[i];
+                            float wu = wj[i];
+                            if constexpr (H16) {
+                                // an upper bound of w from its fp16 round-down: one fp16 ulp up
+                                // (2^13 f32 ulps), 2^-14 below the normal range, +inf at the
+                                // saturation value
+                                wu = wu < 6.103515625e-05f ? 6.103515625e-05f
+                                     : (wu >= 65504.0f ? __int_as_float(0x7f800000)
+                                                        : __int_as_float(__float_as_int(wu) + (1 << 13)));
+                                wu = wj[i] == wj[i] ? wu : wj[i];  // NaN (no arc) stays NaN
+                            }
+                            const float c32 = du + wu;
                             const float nb = __int_as_float(__float_as_int(c32) + 9);
                             float& th = thr[k][4 * j + i];
                             th = ((c32 < __int_as_float(0x7f800000)) & (nb < th)) ? nb : th;
@@ -1474,6 +1530,26 @@ __global__ __launch_bounds__(256) void k_permute_w(const T* __restrict__ W, cons
 
 // minW[c][w] = min of W32p over rows [c*SRS, c*SRS+SRS) x columns [w*tdt, w*tdt+tdt), NaN (no
 // arc) ignored, +inf when the tile has no arc (the pruned sweep uses tdt = 1: one per column)
+// W16p for the H16 chunk loop: W32p rounded toward -inf to fp16 (latencies are positive, so
+// toward zero), saturating at 65504 (never +inf: a finite weight must keep a finite key),
+// NaN (no arc) kept
+__global__ __launch_bounds__(256) void k_w16(const float* __restrict__ W32p, uint16_t* __restrict__ W16p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float f = W32p[i];
+        uint16_t hb;
+        if (f != f) {
+            hb = 0x7e00;
+        } else if (f >= 65504.0f) {
+            hb = 0x7bff;
+        } else {
+            const _Float16 h = (_Float16)f;
+            hb = __builtin_bit_cast(uint16_t, h);
+            if ((float)h > f) hb = (uint16_t)(hb - 1);  // f >= 0: the next fp16 below
+        }
+        W16p[i] = hb;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_min_w32(const float* __restrict__ W32p, int32_t Vp, int32_t nchunks,
                                                  int32_t nwt, int32_t tdt, float* __restrict__ minW) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -2602,6 +2678,8 @@ struct shadowtopo_engine {
     // pruned full sweep (OPT_DENSE_PRUNE): vertex locality order and its chunk bounds
     int32_t* d_perm = nullptr;  // [Vp] row/column order (padding maps to itself)
     float* d_W32p = nullptr;    // [Vp][Vp] W32 in that order
+    uint16_t* d_W16p = nullptr; // OPT_DENSE_W16: [Vp][Vp] W32p rounded down to fp16 (the chunk loop's key)
+    int32_t opt_dense_w16 = 0;
     double* d_Wp = nullptr;     // [Vp][Vp] W in that order
     int32_t* d_WIp = nullptr;   // [Vp][Vp] WI in that order
     double* d_WRp = nullptr;    // [Vp][Vp] WR in that order
@@ -2694,6 +2772,7 @@ struct shadowtopo_engine {
     int32_t opt_delta_permille = 125;  // dense: delta round when a batch changed <= this share of its pairs
     int32_t opt_hbm_share = 1000;      // per mille of the batch-slot HBM budget this engine may take
     bool floor_ok = false;             // default_nb: the 24 GB budget floor was found free once
+    bool floor_checked = false;        // an allocation at the floor failed once: never trust it again
     size_t pool_bytes = 0;             // device bytes the batch pools hold (ensure_batches)
     int32_t opt_worklist = 1;          // CSR rounds over compacted frontier worklists
     int32_t opt_csr_variant = SHADOWTOPO_CSR_FULL;  // CSR rounds: pull (FULL) or push (PUSH, undirected)
@@ -2891,7 +2970,7 @@ int32_t default_nb(shadowtopo_engine* eng, int32_t rows) {
     // grow the budget from one call to the next and reallocate the pools every step (r03: C5
     // paid 1.3 s per step for that after the change-record pool was dropped)
     const double held = (double)eng->pool_bytes;
-    if ((double)free_b + held >= floor_b) eng->floor_ok = true;
+    if ((double)free_b + held >= floor_b && !eng->floor_checked) eng->floor_ok = true;
     // engines sharing one device (SHADOWTOPO_DEVICES listing it twice) split the budget
     const double budget = std::max(eng->floor_ok ? floor_b : 0.0,
                                    0.55 * ((double)free_b + held) * eng->opt_hbm_share / 1000.0);
@@ -2949,6 +3028,23 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
         hipLaunchKernelGGL(k_min_d32, dim3((uint32_t)((nchunks + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
                            eng->d_perm, (int32_t)nchunks, eng->d_minD);
         if (TB == 1 && eng->opt_sweep_split) {  // the chunk loop, then the exact pass + epilogue
+            if (eng->opt_dense_w16 && !eng->d_W16p) {
+                const size_t n = (size_t)eng->Vp * eng->Vp;
+                hipError_t e = hipMalloc((void**)&eng->d_W16p, n * sizeof(uint16_t));
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(k_w16, dim3(4096), dim3(256), 0, s, eng->d_W32p, eng->d_W16p, n);
+            }
+            bool w16 = false;
+            if constexpr (TB == 1) {
+                w16 = eng->opt_dense_w16 != 0;
+                if (w16)
+                    hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1, 4, true>), dim3((uint32_t)nblocks), dim3(256),
+                                       0, s, (const float*)eng->d_W16p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
+                                       eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev, cnt_cur, eng->d_prof,
+                                       eng->d_hitlog, eng->d_perm, eng->d_minW, eng->d_minD, eng->d_pos, eng->d_WIp,
+                                       eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1);
+            }
+            if (!w16)
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
@@ -3836,7 +3932,16 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             row_bytes >= 0.5 * (double)eng->n_arcs)
             nb = std::max(1, (need + eng->opt_host_split - 1) / eng->opt_host_split);
     }
-    if ((rc = ensure_batches(eng, nb))) return rc;
+    if ((rc = ensure_batches(eng, nb)) == SHADOWTOPO_ENOMEM && eng->floor_ok) {
+        // the 24 GB floor was free once, but something else has taken HBM since (another
+        // engine or process on the device): size the pools from a fresh free-memory query
+        (void)hipGetLastError();  // the failed hipMalloc's error, not a launch's
+        eng->floor_ok = false;
+        eng->floor_checked = true;
+        nb = default_nb(eng, row_end - row_begin);
+        rc = ensure_batches(eng, nb);
+    }
+    if (rc) return rc;
     const int32_t group = nb * KL;
     if ((rc = ensure_vperm(eng, s))) return rc;
     // rows of a group go to batch lanes in locality order (CSR rounds, and the pruned dense
@@ -4490,6 +4595,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
     if (eng->d_perm) (void)hipFree(eng->d_perm);
     if (eng->d_W32p) (void)hipFree(eng->d_W32p);
+    if (eng->d_W16p) (void)hipFree(eng->d_W16p);
     if (eng->d_Wp) (void)hipFree(eng->d_Wp);
     if (eng->d_WIp) (void)hipFree(eng->d_WIp);
     if (eng->d_WRp) (void)hipFree(eng->d_WRp);
@@ -4618,6 +4724,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value < 8 || value % 8 || value > ((int64_t)1 << 23))
                 return fail(SHADOWTOPO_EINVAL, "grid x limit must be a multiple of 8 in [8, 2^23]");
             eng->opt_grid_x = value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DENSE_W16:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense W16 must be 0 or 1");
+            eng->opt_dense_w16 = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_LIVE:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "delta live must be 0, 1 or 2");

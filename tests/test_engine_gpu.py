@@ -488,3 +488,25 @@ def test_push_rounds_rejects_directed():
     with pytest.raises(E.ShadowTopoError):
         eng.set_option(E.OPT_CSR_VARIANT, E.CSR_PUSH)
     eng.close()
+
+
+@pytest.mark.parametrize("case", ["geometric", "geometric_odd", "geometric_huge", "ties", "vloss_prefer"])
+def test_dense_w16_filter_same_results(case):
+    """OPT_DENSE_W16: the pruned sweep's chunk loop filters with fp16 weights rounded down
+    (half the LDS slab and table); the matrices are bit for bit the f32 filter's and the
+    oracle's.  The geometric graph has latencies up to ~280 ms (fp16 ulp 0.25 ms there)."""
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=2000, A=300)
+    elif case == "geometric_odd":
+        g = synth.geometric_complete_ish(V=1337, A=257)
+    elif case == "geometric_huge":  # latencies past fp16's 65504: the saturated keys
+        g = synth.geometric_complete_ish(V=1500, A=200)
+        g.latency = g.latency * 1000.0
+    elif case == "ties":
+        g = synth.integer_grid(rows=11, cols=12, seed=6)
+    else:
+        rng = np.random.default_rng(5)
+        g = synth.random_sparse(V=170, avg_deg=8, seed=7, vloss=rng.uniform(0, 0.1, 170))
+        g.prefer_direct = True
+    st = compare(g, layout="dense", dense_w16=1)
+    assert st["dense"] == 1 and st["full_sweeps"] > 0
