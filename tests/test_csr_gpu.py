@@ -54,7 +54,8 @@ def test_csr_removed_variants_rejected():
     g = _case("sparse")
     eng = E.Engine.from_synth(g, layout="csr")
     eng.set_option(E.OPT_CSR_VARIANT, E.CSR_FULL)
-    for v in (0, 2, 3):
+    eng.set_option(E.OPT_CSR_VARIANT, E.CSR_PUSH)  # the push rounds (undirected graphs)
+    for v in (0, 3, 4):
         with pytest.raises(E.ShadowTopoError):
             eng.set_option(E.OPT_CSR_VARIANT, v)
     eng.close()
