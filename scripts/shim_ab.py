@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Warm / cold per-packet lookup rates of two builds of the drop-in on ONE box (verdict r03
 item 6): the current libshadowtopo_hip against the r02k build (commit 932dcde, built from
-that commit's own sources into tools/abshim/r02k/, with that commit's harness), C4 graph,
+that commit's own sources into tools/abshim/r02k/), one harness (tests/c/topo_harness.c,
+compiled against each build's own headers), C4 graph,
 10^4 hosts, 8 threads and 1 thread, runs interleaved.  One JSON object per run."""
 import json
 import os
@@ -31,7 +32,9 @@ def main():
         builds = {
             "current": build(os.path.join(ROOT, "tests", "c", "topo_harness.c"), os.path.dirname(E.LIB_PATH), inc,
                              os.path.join(tmp, "h_cur")),
-            "r02k": build(os.path.join(ROOT, "tools", "abshim", "r02k", "topo_harness.c"),
+            # the same (current) harness, against r02k's headers and library: its warm pass
+            # completes before the timed pass on every build
+            "r02k": build(os.path.join(ROOT, "tests", "c", "topo_harness.c"),
                           os.path.join(ROOT, "tools", "abshim", "r02k"),
                           os.path.join(ROOT, "tools", "abshim", "r02k", "include"), os.path.join(tmp, "h_r02k")),
         }
