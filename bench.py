@@ -420,6 +420,8 @@ def main():
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
+    ap.add_argument("--device-rounds", type=int, default=-1, help="CSR worklist rounds driven from the device: 0 never, "
+                    "1 when batches x vertices <= 4 Mi, 2 always; -1 = engine default")
     ap.add_argument("--csr-variant", type=int, default=1, help="sparse rounds: 1 = pull (default), 2 = push (u64 atomicMin)")
     ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists when under half the pairs are active (1, default), "
                          "always (2), or the full grid (0)")
@@ -480,6 +482,8 @@ def main():
         eng.set_option(E.OPT_DENSE_W16, args.dense_w16)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
+    if args.device_rounds >= 0:
+        eng.set_option(E.OPT_DEVICE_ROUNDS, args.device_rounds)
     if not eng.complete and args.csr_variant != 1:
         eng.set_option(E.OPT_CSR_VARIANT, args.csr_variant)
     log(f"[rank {rank}] engine (graph resident in HBM) in {time.perf_counter() - t:.1f}s, "
