@@ -546,18 +546,38 @@ __global__ __launch_bounds__(256) void k_scan_wl(uint32_t* __restrict__ wlcnt, i
 
 // k_relax_wl with a fixed grid (G blocks, G / 8 per XCD) that loops over the round's items:
 // XCD x (block % 8) takes the slice [x*S, (x+1)*S) of the batch-major list, S = ceil(T / 8),
-// its waves striding through it; an empty round's blocks exit at once
+// its waves striding through it; an empty round's blocks exit at once.  A heavy round (at
+// least half the pairs active, where the host-driven rounds launch the grid kernel) walks the
+// virtual grid of k_relax instead -- block vb = blockIdx.x + k * gridDim.x, the same XCD
+// (vb % 8) and xcd_tile mapping, one activity flag per (vertex, batch): a worklist entry load
+// in front of every visit made these rounds 22-25 % slower (r04l, C4 groups of 20 / 40 batches)
 __global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                    const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                    const int64_t* __restrict__ out_ptr,
                                                    const int32_t* __restrict__ out_dst, Pools pools, int32_t parity,
                                                    const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
                                                    int32_t nb, int32_t* __restrict__ cnt,
-                                                   unsigned long long* __restrict__ prof) {
+                                                   unsigned long long* __restrict__ prof, int32_t V) {
     const int64_t T = prefix[nb];
     if (T == 0) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    if (T * 2 >= (int64_t)nb * V) {
+        const int32_t nvb = (V + 3) / 4;
+        const int64_t nvblocks = 8 * (((int64_t)nb * nvb + 7) / 8);
+        for (int64_t vb = blockIdx.x; vb < nvblocks; vb += gridDim.x) {
+            int32_t b, vt;
+            if (!xcd_tile(vb, nb, nvb, b, vt)) continue;
+            const int32_t v = vt * 4 + wave;
+            if (v >= V) continue;
+            const BatchDev B = batch_view(pools, b);
+            gbyte* act_cur = B.act(parity);
+            if (act_cur[v] == 0) continue;
+            relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+            if (lane == 0) act_cur[v] = 0;  // cleared after the visit, as k_relax_wl does
+        }
+        return;
+    }
     const int64_t S = (T + 7) / 8;
     const int64_t x = blockIdx.x & 7;
     const int64_t waves_per_xcd = (int64_t)(gridDim.x >> 3) * 4;
@@ -3285,7 +3305,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0)], s));
                 hipLaunchKernelGGL(k_relax_wlp, dim3(G), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r, g.out_ptr,
                                    g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl, eng->d_wlpre, nbg, cnt_cur,
-                                   eng->d_prof);
+                                   eng->d_prof, V);
                 if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0) + 1], s));
                 hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
                                    (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);

@@ -191,3 +191,13 @@ def test_device_driven_rounds_same_results(case):
     st1 = compare(g, layout="csr", device_rounds=2, batches_in_flight=2)
     st0 = compare(g, layout="csr", device_rounds=0, batches_in_flight=2)
     assert st1["rounds"] == st0["rounds"] and st1["wl_launches"] == st1["relax_launches"]
+
+
+@pytest.mark.parametrize("case", ["sparse", "ties", "vloss_prefer", "multigraph"])
+def test_csr_device_rounds_heavy_grid_mode(case):
+    """Device-driven rounds (OPT_DEVICE_ROUNDS=2) over several batch groups: the persistent
+    kernel walks the virtual grid in rounds with at least half the pairs active and the
+    worklist otherwise; the same matrices as the oracle's, bit for bit"""
+    g = _case(case)
+    st = compare(g, layout="csr", device_rounds=2, batches_in_flight=2)
+    assert st["dense"] == 0 and st["host_syncs"] < st["rounds"]
