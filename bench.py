@@ -421,7 +421,7 @@ def main():
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--device-rounds", type=int, default=-1, help="CSR worklist rounds driven from the device: 0 never, "
-                    "1 when batches x vertices <= 4 Mi, 2 always; -1 = engine default")
+                    "1 when batches x vertices <= 1 Mi, 2 always; -1 = engine default")
     ap.add_argument("--csr-variant", type=int, default=1, help="sparse rounds: 1 = pull (default), 2 = push (u64 atomicMin)")
     ap.add_argument("--worklist", type=int, default=1, help="CSR rounds over compacted frontier worklists when under half the pairs are active (1, default), "
                          "always (2), or the full grid (0)")

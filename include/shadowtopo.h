@@ -107,7 +107,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               vertices with one neighbour; they lie on no attached-pair path);
                                               0 = every vertex. Results are identical. */
 #define SHADOWTOPO_OPT_DEVICE_ROUNDS 17   /* CSR FULL worklist rounds: 1 (default) = driven from the device (item
-                                              counts read back once per 8 rounds) when batches x vertices <= 4 Mi,
+                                              counts read back once per 8 rounds) when batches x vertices <= 1 Mi,
                                               2 = always, 0 = never (one host read-back per round). Results are
                                               identical. */
 /* (18: retired -- batched delta-stepping rounds, measured slower and removed in r04) */
