@@ -2773,7 +2773,6 @@ struct shadowtopo_engine {
     // rounds take milliseconds, so the host's read-back per round is noise, while the
     // persistent kernel runs at most 7 waves per SIMD; C3, 0.77 M pairs and 0.1 ms rounds, gains)
     int64_t dev_rounds_max = (int64_t)1 << 20;
-    uint32_t wlp_grid = 0;  // k_relax_wlp blocks: every one resident at once (occupancy query, once)
     // staging for host outputs
     void* stage = nullptr;
     size_t stage_bytes = 0;
@@ -3295,18 +3294,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             eng->ev_dev.resize(2 * DEV_K);
             for (auto& e : eng->ev_dev) HIP_TRY(hipEventCreate(&e));
         }
-        // fixed grid of resident blocks: the kernel strides over its items, so a block that
-        // is not resident from the start would run its share after the others (106 SGPRs
-        // hold it at 7 waves per SIMD, not the 8 a 2048-block grid assumed)
-        if (!eng->wlp_grid) {
-            int per_cu = 0, ncu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_relax_wlp, 256, 0) != hipSuccess || per_cu < 1)
-                per_cu = 1;
-            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device) != hipSuccess || ncu < 8)
-                ncu = 256;
-            eng->wlp_grid = (uint32_t)std::max(8, (per_cu * ncu) / 8 * 8);  // a multiple of 8: XCD slices
-        }
-        const uint32_t G = eng->wlp_grid;
+        // fixed grid: 2048 blocks (8192 waves).  Sized from the occupancy query instead (7
+        // blocks per CU: the kernel's 106 SGPRs) it ran C3 7.29 -> 7.78 ms (r04n): the strided
+        // item loop balances better over more, partly queued, blocks
+        const uint32_t G = 8 * 256;
         HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
         hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V, 0, eng->d_wl,
                            eng->d_wlcnt, g.in_ptr);
