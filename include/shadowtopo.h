@@ -57,6 +57,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 /* where compute_rows' output buffers live */
 #define SHADOWTOPO_MEM_HOST 0
 #define SHADOWTOPO_MEM_DEVICE 1
+/* host, latency and reliability interleaved: `lat` holds rows x count {lat, rel} pairs
+ * (16 bytes per pair, one cache line serves a packet's getLatency and getReliability),
+ * `rel` must be NULL */
+#define SHADOWTOPO_MEM_HOST_LR 2
 
 /* per-pair kind codes (optional output) */
 #define SHADOWTOPO_KIND_NONE 0     /* unroutable: lat = rel = -1 (topology.c:2073, 2085) */

@@ -1015,7 +1015,7 @@ constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FT
 // W16 <= W32 <= w keeps the filter conservative; a passing row tightens the
 // thresholds with an upper bound of w (one fp16 ulp up; +inf past the saturation).
 template <int TDT, int XR, int TB, bool PR, int PH = 0, int NW = 4, bool H16 = false>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1 ? (NW == 8 || H16 ? 8 : 6) : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1 ? (NW == 8 ? 8 : 6) : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
                                                        int32_t nb, int32_t ntb, int32_t parity, int32_t thresh,
@@ -2406,7 +2406,7 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
                                                  const uint32_t* __restrict__ self_hops,
                                                  const uint8_t* __restrict__ self_kind, double* out_lat,
                                                  double* out_rel, uint32_t* out_hops, uint8_t* out_kind,
-                                                 int32_t row_base) {
+                                                 int32_t row_base, int32_t ls) {
     __shared__ double sd[64 * 65];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const BatchDev B = batch_view(pools, blockIdx.y);
@@ -2460,7 +2460,7 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
     for (int k = threadIdx.x; k < nrow * 64; k += COMPOSE_T) {
         const int j = k >> 6, tl = k & 63;
         const int32_t r = B.row[j], ti = t0 + tl;
-        if (r >= 0 && ti < A) out_lat[(size_t)(r - row_base) * A + ti] = sd[j * 65 + tl];
+        if (r >= 0 && ti < A) out_lat[((size_t)(r - row_base) * A + ti) * ls] = sd[j * 65 + tl];
     }
     __syncthreads();
 #pragma unroll
@@ -2469,7 +2469,7 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
     for (int k = threadIdx.x; k < nrow * 64; k += COMPOSE_T) {
         const int j = k >> 6, tl = k & 63;
         const int32_t r = B.row[j], ti = t0 + tl;
-        if (r >= 0 && ti < A) out_rel[(size_t)(r - row_base) * A + ti] = sd[j * 65 + tl];
+        if (r >= 0 && ti < A) out_rel[((size_t)(r - row_base) * A + ti) * ls] = sd[j * 65 + tl];
     }
     __syncthreads();
     uint32_t* su = reinterpret_cast<uint32_t*>(sd);
@@ -2605,7 +2605,7 @@ __global__ void k_compose_replay(GraphDev g, ReplayDev rp, const int32_t* __rest
                                  const double* __restrict__ self_lat, const double* __restrict__ self_rel,
                                  const uint32_t* __restrict__ self_hops, const uint8_t* __restrict__ self_kind,
                                  double* out_lat, double* out_rel, uint32_t* out_hops, uint8_t* out_kind,
-                                 int32_t row_base) {
+                                 int32_t row_base, int32_t ls) {
     const int32_t slot = blockIdx.y;
     const int32_t ti = blockIdx.x * blockDim.x + threadIdx.x;
     if (ti >= A) return;
@@ -2651,8 +2651,8 @@ __global__ void k_compose_replay(GraphDev g, ReplayDev rp, const int32_t* __rest
         }
     }
     const size_t w = (size_t)(rp.row[slot] - row_base) * A + ti;
-    out_lat[w] = o.lat;
-    out_rel[w] = o.rel;
+    out_lat[w * ls] = o.lat;  // ls = 2: {lat, rel} interleaved (SHADOWTOPO_MEM_HOST_LR)
+    out_rel[w * ls] = o.rel;
     if (out_hops) out_hops[w] = o.hops;
     if (out_kind) out_kind[w] = o.kind;
 }
@@ -3930,6 +3930,11 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
 
 int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
                       uint32_t* hops, uint8_t* kind, int32_t mem, hipStream_t s) {
+    // MEM_HOST_LR: host rows of {lat, rel} pairs in `lat` (the shim's per-packet layout); the
+    // staging rows are composed interleaved (element stride 2) and leave in one copy
+    const bool lr = mem == SHADOWTOPO_MEM_HOST_LR;
+    if (lr) mem = SHADOWTOPO_MEM_HOST;
+    const int32_t ls = lr ? 2 : 1;
     const int32_t A = eng->A;
     const bool complete = (eng->flags & SHADOWTOPO_F_COMPLETE) != 0;
     int rc;
@@ -3940,7 +3945,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     // into pinned (page-locked) host memory -- shadowtopo_host_alloc, as the topology shim
     // allocates its matrix -- the copy of group g runs on the copy stream behind group
     // g + 1's relaxation (two staging slots), into pageable memory it is a synchronous copy
-    const bool pinned_out = mem == SHADOWTOPO_MEM_HOST && is_pinned(lat) && is_pinned(rel) &&
+    const bool pinned_out = mem == SHADOWTOPO_MEM_HOST && is_pinned(lat) && (lr || is_pinned(rel)) &&
                             (!hops || is_pinned(hops)) && (!kind || is_pinned(kind));
     int32_t nb = default_nb(eng, row_end - row_begin);
     {
@@ -4014,7 +4019,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             char* p = static_cast<char*>(eng->stage) + slot * slot_bytes;
             const size_t n = (size_t)group * A;
             dl = reinterpret_cast<double*>(p);
-            dr = reinterpret_cast<double*>(p + n * 8);
+            dr = lr ? dl + 1 : reinterpret_cast<double*>(p + n * 8);
             dh = hops ? reinterpret_cast<uint32_t*>(p + n * 16) : nullptr;
             dk = kind ? reinterpret_cast<uint8_t*>(p + n * (hops ? 20 : 16)) : nullptr;
             row_base = r0;
@@ -4044,7 +4049,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         if (A > 0) {
             hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(COMPOSE_T), 0, s, *eng->rg, eng->pools,
                                d_att_r, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
-                               eng->d_self_kind, dl, dr, dh, dk, row_base);
+                               eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
             HIP_TRY(hipGetLastError());
         }
         // collect tie-tainted sources
@@ -4076,7 +4081,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                 HIP_TRY(hipGetLastError());
                 hipLaunchKernelGGL(k_compose_replay, dim3((A + 255) / 256, nj), dim3(256), 0, s, eng->g, eng->rp,
                                    eng->d_attached, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
-                                   eng->d_self_kind, dl, dr, dh, dk, row_base);
+                                   eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
                 HIP_TRY(hipGetLastError());
             }
             HIP_TRY(hipStreamSynchronize(s));
@@ -4092,8 +4097,12 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                 HIP_TRY(hipEventRecord(eng->ev_comp[slot], s));
                 HIP_TRY(hipStreamWaitEvent(cs, eng->ev_comp[slot], 0));
             }
-            HIP_TRY(hipMemcpyAsync(lat + o, dl, n * 8, hipMemcpyDeviceToHost, cs));
-            HIP_TRY(hipMemcpyAsync(rel + o, dr, n * 8, hipMemcpyDeviceToHost, cs));
+            if (lr) {
+                HIP_TRY(hipMemcpyAsync(lat + 2 * o, dl, n * 16, hipMemcpyDeviceToHost, cs));
+            } else {
+                HIP_TRY(hipMemcpyAsync(lat + o, dl, n * 8, hipMemcpyDeviceToHost, cs));
+                HIP_TRY(hipMemcpyAsync(rel + o, dr, n * 8, hipMemcpyDeviceToHost, cs));
+            }
             if (hops) HIP_TRY(hipMemcpyAsync(hops + o, dh, n * 4, hipMemcpyDeviceToHost, cs));
             if (kind) HIP_TRY(hipMemcpyAsync(kind + o, dk, n, hipMemcpyDeviceToHost, cs));
             if (pinned_out)
@@ -4782,8 +4791,9 @@ int shadowtopo_compute_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t r
     if (!eng->d_attached) return fail(SHADOWTOPO_ESTATE, "shadowtopo_set_attached not called");
     if (row_begin < 0 || row_end > eng->A || row_begin > row_end) return fail(SHADOWTOPO_EINVAL, "bad row range");
     if (row_begin == row_end) return SHADOWTOPO_OK;
-    if (!lat || !rel) return fail(SHADOWTOPO_EINVAL, "NULL output");
-    if (mem != SHADOWTOPO_MEM_HOST && mem != SHADOWTOPO_MEM_DEVICE) return fail(SHADOWTOPO_EINVAL, "bad mem kind");
+    if (mem != SHADOWTOPO_MEM_HOST && mem != SHADOWTOPO_MEM_DEVICE && mem != SHADOWTOPO_MEM_HOST_LR)
+        return fail(SHADOWTOPO_EINVAL, "bad mem kind");
+    if (!lat || (!rel) != (mem == SHADOWTOPO_MEM_HOST_LR)) return fail(SHADOWTOPO_EINVAL, "NULL output");
     HIP_TRY(hipSetDevice(eng->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
     auto t0 = std::chrono::steady_clock::now();

@@ -162,8 +162,8 @@ static void ipt_del(_Atomic(iptab*)* live, uint32_t ip) {
 typedef struct matrix {
     int32_t A;
     int pinned;
-    double* lat;
-    double* rel;
+    double* lr;     /* {latency, reliability} per pair, interleaved (SHADOWTOPO_MEM_HOST_LR): a
+                     * packet's getLatency and getReliability read one cache line */
     uint8_t* kind;
     /* undirected late attach: rows [0, partial) hold the reverse-direction entries in
      * columns >= fill_col until an old source's own row is needed (fill_old_rows rewrites
@@ -694,8 +694,7 @@ static void mat_free(const matrix* m, void* p) {
 
 static void free_matrix(matrix* m) {
     if (!m) return;
-    mat_free(m, m->lat);
-    mat_free(m, m->rel);
+    mat_free(m, m->lr);
     mat_free(m, m->kind);
     free(m->srl_lat);
     free(m->srl_rel);
@@ -887,7 +886,7 @@ static char* path_string(const Topology* top, int32_t s, int32_t t, const matrix
     size_t o = (size_t)i * m->A + j;
     snprintf(buf, len,
              "SourceIndex=%ld DestinationIndex=%ld Latency=%f Reliability=%f PacketCount=%lu isDirect=%s", (long)s,
-             (long)t, srl ? m->srl_lat[i] : cell_d(&m->lat[o]), srl ? m->srl_rel[i] : cell_d(&m->rel[o]),
+             (long)t, srl ? m->srl_lat[i] : cell_d(&m->lr[2 * o]), srl ? m->srl_rel[i] : cell_d(&m->lr[2 * o + 1]),
              (unsigned long)count, (!srl && cell_k(&m->kind[o]) == SHADOWTOPO_KIND_DIRECT) ? "True" : "False");
     (void)top;
     return buf;
@@ -1414,8 +1413,7 @@ typedef struct {
     shadowtopo_engine* eng;
     const int32_t* attached;
     int32_t A, r0, r1;
-    double* lat;
-    double* rel;
+    double* lr;
     uint8_t* kind;
     int rc;
     char err[256];
@@ -1425,7 +1423,7 @@ static void* compute_block(void* arg) {
     row_block* w = arg;
     w->rc = shadowtopo_set_attached(w->eng, w->attached, w->A);
     if (w->rc == SHADOWTOPO_OK && w->r1 > w->r0)
-        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->lat, w->rel, NULL, w->kind, SHADOWTOPO_MEM_HOST,
+        w->rc = shadowtopo_compute_rows(w->eng, w->r0, w->r1, w->lr, NULL, NULL, w->kind, SHADOWTOPO_MEM_HOST_LR,
                                         NULL);
     if (w->rc != SHADOWTOPO_OK) snprintf(w->err, sizeof w->err, "%s", shadowtopo_last_error());
     return NULL;
@@ -1448,8 +1446,7 @@ static int compute_rows_sharded(Topology* top, const int32_t* attached, int32_t 
         b->r0 = r0 + (k * per < rows ? k * per : rows);
         b->r1 = r0 + ((k + 1) * per < rows ? (k + 1) * per : rows);
         const size_t o = (size_t)b->r0 * (size_t)A;
-        b->lat = m->lat + o;
-        b->rel = m->rel + o;
+        b->lr = m->lr + 2 * o;
         b->kind = m->kind + o;
         b->rc = 0;
         b->err[0] = 0;
@@ -1479,24 +1476,20 @@ static matrix* alloc_matrix(int32_t A) {
     size_t n = (size_t)A * (size_t)A;
     m->A = A;
     /* page-locked first; plain malloc when the driver refuses (the copy is then slower) */
-    void *pl = NULL, *pr = NULL, *pk = NULL;
-    if (shadowtopo_host_alloc(sizeof(double) * (n ? n : 1), &pl) == SHADOWTOPO_OK &&
-        shadowtopo_host_alloc(sizeof(double) * (n ? n : 1), &pr) == SHADOWTOPO_OK &&
+    void *pl = NULL, *pk = NULL;
+    if (shadowtopo_host_alloc(2 * sizeof(double) * (n ? n : 1), &pl) == SHADOWTOPO_OK &&
         shadowtopo_host_alloc(n ? n : 1, &pk) == SHADOWTOPO_OK) {
         m->pinned = 1;
-        m->lat = pl;
-        m->rel = pr;
+        m->lr = pl;
         m->kind = pk;
     } else {
         shadowtopo_host_free(pl);
-        shadowtopo_host_free(pr);
         shadowtopo_host_free(pk);
         m->pinned = 0;
-        m->lat = malloc(sizeof(double) * (n ? n : 1));
-        m->rel = malloc(sizeof(double) * (n ? n : 1));
+        m->lr = malloc(2 * sizeof(double) * (n ? n : 1));
         m->kind = malloc(n ? n : 1);
     }
-    if (!m->lat || !m->rel || !m->kind) {
+    if (!m->lr || !m->kind) {
         st_critical("out of host memory for the %d x %d attached-pair matrix", A, A);
         free_matrix(m);
         return NULL;
@@ -1535,13 +1528,12 @@ static matrix* compute_matrix(Topology* top, const int32_t* attached, int32_t A,
     }
     for (int32_t i = 0; i < A0; i++) {
         const size_t src = (size_t)i * (size_t)A0, dst = (size_t)i * (size_t)A;
-        memcpy(m->lat + dst, old->lat + src, sizeof(double) * (size_t)A0);
-        memcpy(m->rel + dst, old->rel + src, sizeof(double) * (size_t)A0);
+        memcpy(m->lr + 2 * dst, old->lr + 2 * src, 2 * sizeof(double) * (size_t)A0);
         memcpy(m->kind + dst, old->kind + src, (size_t)A0);
         for (int32_t j = A0; j < A; j++) {
             const size_t o = dst + (size_t)j, r = (size_t)j * (size_t)A + (size_t)i;
-            m->lat[o] = m->lat[r];
-            m->rel[o] = m->rel[r];
+            m->lr[2 * o] = m->lr[2 * r];
+            m->lr[2 * o + 1] = m->lr[2 * r + 1];
             m->kind[o] = m->kind[r];
         }
     }
@@ -1612,10 +1604,9 @@ static int fill_old_rows(Topology* top, matrix* m) {
         matrix tmp;
         memset(&tmp, 0, sizeof tmp);
         tmp.A = A;
-        tmp.lat = malloc(sizeof(double) * (size_t)P * (size_t)A);
-        tmp.rel = malloc(sizeof(double) * (size_t)P * (size_t)A);
+        tmp.lr = malloc(2 * sizeof(double) * (size_t)P * (size_t)A);
         tmp.kind = malloc((size_t)P * (size_t)A);
-        if (att && tmp.lat && tmp.rel && tmp.kind) {
+        if (att && tmp.lr && tmp.kind) {
             pthread_rwlock_rdlock(&top->ip_lock);
             memcpy(att, top->attached, sizeof(int32_t) * (size_t)A);  /* attach order: a stable prefix */
             pthread_rwlock_unlock(&top->ip_lock);
@@ -1627,8 +1618,8 @@ static int fill_old_rows(Topology* top, matrix* m) {
                 for (int32_t i = 0; i < P; i++)
                     for (int32_t t = m->fill_col; t < A; t++) {
                         const size_t o = (size_t)i * (size_t)A + (size_t)t;
-                        cell_d_store(&m->lat[o], tmp.lat[o]);
-                        cell_d_store(&m->rel[o], tmp.rel[o]);
+                        cell_d_store(&m->lr[2 * o], tmp.lr[2 * o]);
+                        cell_d_store(&m->lr[2 * o + 1], tmp.lr[2 * o + 1]);
                         __atomic_store_n(&m->kind[o], tmp.kind[o], __ATOMIC_RELAXED);
                     }
                 atomic_store_explicit(&m->partial, 0, memory_order_release);
@@ -1639,8 +1630,7 @@ static int fill_old_rows(Topology* top, matrix* m) {
             top->compute_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
         }
         free(att);
-        free(tmp.lat);
-        free(tmp.rel);
+        free(tmp.lr);
         free(tmp.kind);
     }
     pthread_mutex_unlock(&top->compute_lock);
@@ -1702,7 +1692,7 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
             if (k != SHADOWTOPO_KIND_DIRECT)
                 success = 0;
             else if (cache_claim(top, i, j)) {
-                mn = cell_d(&m->lat[(size_t)i * A + j]);
+                mn = cell_d(&m->lr[2 * ((size_t)i * A + j)]);
                 stored = 1;
             }
         } else if (i == j) {
@@ -1713,7 +1703,7 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
             if (ks == SHADOWTOPO_KIND_NONE)
                 success = 0; /* no incident edge: no self path */
             else if (cache_claim_bit(top, i, i, top->self_rule ? 2u : 1u)) {
-                mn = top->self_rule ? m->srl_lat[i] : cell_d(&m->lat[(size_t)i * A + i]);
+                mn = top->self_rule ? m->srl_lat[i] : cell_d(&m->lr[2 * ((size_t)i * A + i)]);
                 stored = 1;
             }
         } else {
@@ -1736,7 +1726,7 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
                 const uint8_t kt = cell_k(&kr[t]);
                 if (kt == SHADOWTOPO_KIND_NONE || kt == SHADOWTOPO_KIND_DIRECT) continue;
                 if (!cache_claim(top, i, t)) continue;
-                const double l = cell_d(&m->lat[(size_t)i * A + t]);
+                const double l = cell_d(&m->lr[2 * ((size_t)i * A + t)]);
                 if (!stored || l < mn) mn = l;
                 stored++;
             }
@@ -1811,7 +1801,7 @@ double topology_getLatency(Topology* top, Address* srcAddress, Address* dstAddre
     int32_t i;
     int srl = 0;
     matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, NULL, &srl);
-    return m ? (srl ? m->srl_lat[i] : cell_d(&m->lat[o])) : -1.0;
+    return m ? (srl ? m->srl_lat[i] : cell_d(&m->lr[2 * o])) : -1.0;
 }
 
 double topology_getReliability(Topology* top, Address* srcAddress, Address* dstAddress) {
@@ -1819,7 +1809,7 @@ double topology_getReliability(Topology* top, Address* srcAddress, Address* dstA
     int32_t i;
     int srl = 0;
     matrix* m = path_entry(top, srcAddress, dstAddress, &o, &i, NULL, &srl);
-    return m ? (srl ? m->srl_rel[i] : cell_d(&m->rel[o])) : -1.0;
+    return m ? (srl ? m->srl_rel[i] : cell_d(&m->lr[2 * o + 1])) : -1.0;
 }
 
 int topology_isRoutable(Topology* top, Address* srcAddress, Address* dstAddress) {

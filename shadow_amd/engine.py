@@ -26,6 +26,7 @@ F_FORCE_CSR = 0x40
 
 MEM_HOST = 0
 MEM_DEVICE = 1
+MEM_HOST_LR = 2  # host rows of interleaved {lat, rel} pairs (the shim's layout)
 
 KIND_NONE, KIND_DIRECT, KIND_SELF, KIND_DIJKSTRA = 0, 1, 2, 3
 
@@ -268,6 +269,19 @@ class Engine:
                 raise ValueError("output arrays must be C-contiguous [rows, A] of the right dtype")
         _check(lib().shadowtopo_compute_rows(self._h, int(row_begin), int(row_end), _ptr(lat), _ptr(rel), _ptr(hops),
                                              _ptr(kind), MEM_HOST, None))
+
+    def compute_rows_lr(self, row_begin=0, row_end=None, pinned=True):
+        """host rows of interleaved {lat, rel} pairs ([rows, A, 2] float64, MEM_HOST_LR: the
+        topology shim's matrix layout) and the pair kinds"""
+        if row_end is None:
+            row_end = self.A
+        R = row_end - row_begin
+        mk = pinned_empty if pinned else np.empty
+        lr = mk((R, self.A, 2), np.float64)
+        kind = mk((R, self.A), np.uint8)
+        _check(lib().shadowtopo_compute_rows(self._h, int(row_begin), int(row_end), _ptr(lr), None, None, _ptr(kind),
+                                             MEM_HOST_LR, None))
+        return lr, kind
 
     def compute_rows_device(self, row_begin, row_end, lat_ptr, rel_ptr, hops_ptr, kind_ptr=None, stream=None):
         """device outputs (raw pointers, e.g. torch tensors' data_ptr()) on `stream`"""

@@ -510,3 +510,26 @@ def test_dense_w16_filter_same_results(case):
         g.prefer_direct = True
     st = compare(g, layout="dense", dense_w16=1)
     assert st["dense"] == 1 and st["full_sweeps"] > 0
+
+
+@pytest.mark.parametrize("layout", ["csr", "dense"])
+def test_host_rows_interleaved_lat_rel(layout):
+    """SHADOWTOPO_MEM_HOST_LR (the shim's per-packet layout): {lat, rel} pairs interleaved in
+    one host array, page-locked (pipelined copy over several groups) and pageable, identical
+    to the separate arrays; a replayed (tie) source's rows too"""
+    g = synth.integer_grid(rows=12, cols=12, seed=3) if layout == "csr" else synth.geometric_complete_ish(V=600, A=150)
+    eng = E.Engine.from_synth(g, layout=layout)
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_BATCHES_IN_FLIGHT, 1)
+    lat, rel, _, kind = eng.compute_rows()
+    for pinned in (True, False):
+        lr, kl = eng.compute_rows_lr(pinned=pinned)
+        assert np.array_equal(lr[:, :, 0].view(np.uint64), lat.view(np.uint64))
+        assert np.array_equal(lr[:, :, 1].view(np.uint64), rel.view(np.uint64))
+        assert np.array_equal(kl, kind)
+        a, b = 5, len(g.attached) - 3
+        lr2, _ = eng.compute_rows_lr(a, b, pinned=pinned)
+        assert np.array_equal(lr2[:, :, 0].view(np.uint64), lat[a:b].view(np.uint64))
+    if layout == "csr":
+        assert eng.stats()["replayed_sources"] > 0
+    eng.close()
