@@ -28,6 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <strings.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "graphml.h"
@@ -220,6 +221,13 @@ typedef struct {
 
 #define CTILE 64 /* packet counters: 64 x 64 tiles, allocated on first touch */
 
+struct arena_slab;
+typedef struct {
+    pthread_mutex_t mu;
+    struct arena_slab* head;
+    size_t off;
+} tile_arena;
+
 struct _Topology {
     uint32_t magic;
     gml_graph* gml;
@@ -247,6 +255,7 @@ struct _Topology {
      * crow[i / 64] -> [ctd] tile pointers -> 64 x 64 u64 (count + 1 once touched) */
     int32_t ctd;
     _Atomic(_Atomic(uint64_t*)*)* crow;
+    tile_arena tiles; /* the counter and cache-cell tiles (arena_alloc) */
     shadowtopo_engine* eng;  /* engine on devices[0] */
     int32_t device;
     /* in-process multi-GPU: one engine per device, each computing a
@@ -734,9 +743,55 @@ static void free_index(attach_index* x) {
     free(x);
 }
 
+/* Zeroed tile memory for the counter and cache-cell tables, bumped out of 32 MiB anonymous
+ * maps backed by transparent huge pages: worker threads touch the tiles at random, one pair
+ * per packet, and over 4 KiB pages each touch is also a page walk (engine.hip:
+ * shadowtopo_host_alloc has the measurement).  A tile is allocated once, on first touch, so
+ * the arena takes a lock; a tile lost to a racing first touch stays unused until
+ * topology_free unmaps the slabs. */
+#define ARENA_SLAB ((size_t)32 << 20)
+typedef struct arena_slab {
+    struct arena_slab* next;
+    size_t len;
+} arena_slab;
+
+static void* arena_alloc(tile_arena* ar, size_t bytes) {
+    bytes = (bytes + 63) & ~(size_t)63;
+    pthread_mutex_lock(&ar->mu);
+    if (!ar->head || ar->off + bytes > ar->head->len) {
+        size_t len = bytes + 64 > ARENA_SLAB ? ((bytes + 64 + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1)) : ARENA_SLAB;
+        void* p = mmap(NULL, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) {
+            pthread_mutex_unlock(&ar->mu);
+            return NULL;
+        }
+        (void)madvise(p, len, MADV_HUGEPAGE);
+        arena_slab* sl = p;
+        sl->next = ar->head;
+        sl->len = len;
+        ar->head = sl;
+        ar->off = 64;
+    }
+    void* r = (char*)ar->head + ar->off;
+    ar->off += bytes;
+    pthread_mutex_unlock(&ar->mu);
+    return r;
+}
+
+static void arena_free(tile_arena* ar) {
+    for (arena_slab* sl = ar->head; sl;) {
+        arena_slab* n = sl->next;
+        munmap(sl, sl->len);
+        sl = n;
+    }
+    ar->head = NULL;
+    pthread_mutex_destroy(&ar->mu);
+}
+
 /* tile (ti, tj) of `words` u64 in a rows -> tiles table, allocated on first touch with a
  * compare-and-swap (no lock); NULL when out of range or out of memory */
-static uint64_t* tile_get(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd, int32_t ti, int32_t tj, size_t words) {
+static uint64_t* tile_get(tile_arena* ar, _Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd, int32_t ti, int32_t tj,
+                          size_t words) {
     if (!rows || ti >= ctd || tj >= ctd) return NULL;
     _Atomic(uint64_t*)* row = atomic_load_explicit(&rows[ti], memory_order_acquire);
     if (!row) {
@@ -753,16 +808,13 @@ static uint64_t* tile_get(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd, int32
     }
     uint64_t* tile = atomic_load_explicit(&row[tj], memory_order_acquire);
     if (!tile) {
-        uint64_t* fresh = calloc(words, sizeof(uint64_t));
+        uint64_t* fresh = arena_alloc(ar, words * sizeof(uint64_t));
         if (!fresh) return NULL;
         uint64_t* expect = NULL;
-        if (atomic_compare_exchange_strong_explicit(&row[tj], &expect, fresh, memory_order_acq_rel,
-                                                    memory_order_acquire))
-            tile = fresh;
-        else {
-            free(fresh);
-            tile = expect;
-        }
+        tile = atomic_compare_exchange_strong_explicit(&row[tj], &expect, fresh, memory_order_acq_rel,
+                                                       memory_order_acquire)
+                   ? fresh
+                   : expect;
     }
     return tile;
 }
@@ -779,7 +831,6 @@ static void tiles_free(_Atomic(_Atomic(uint64_t*)*)* rows, int32_t ctd) {
     for (int32_t ti = 0; ti < ctd; ti++) {
         _Atomic(uint64_t*)* row = atomic_load(&rows[ti]);
         if (!row) continue;
-        for (int32_t tj = 0; tj < ctd; tj++) free(atomic_load(&row[tj]));
         free((void*)row);
     }
     free((void*)rows);
@@ -794,7 +845,7 @@ static _Atomic uint64_t* counter_slot(Topology* top, int32_t i, int32_t j) {
         i = j;
         j = t;
     }
-    uint64_t* tile = tile_get(top->crow, top->ctd, i / CTILE, j / CTILE, CTILE * CTILE);
+    uint64_t* tile = tile_get(&top->tiles, top->crow, top->ctd, i / CTILE, j / CTILE, CTILE * CTILE);
     return tile ? (_Atomic uint64_t*)&tile[(i % CTILE) * CTILE + (j % CTILE)] : NULL;
 }
 
@@ -819,7 +870,8 @@ static uint64_t counter_peek(const Topology* top, int32_t i, int32_t j) {
 #define STILE_WORDS(top) (2 * CTILE)
 
 static _Atomic uint64_t* cell_word(const Topology* top, int32_t a, int32_t b, int alloc, int* shift) {
-    uint64_t* tile = alloc ? tile_get(top->srow, top->ctd, a / CTILE, b / CTILE, STILE_WORDS(top))
+    /* the arena is the topology's mutable allocator state, not part of the query's const view */
+    uint64_t* tile = alloc ? tile_get((tile_arena*)&top->tiles, top->srow, top->ctd, a / CTILE, b / CTILE, STILE_WORDS(top))
                            : tile_peek(top->srow, top->ctd, a / CTILE, b / CTILE);
     if (!tile) return NULL;
     *shift = 2 * (b % 32);
@@ -938,6 +990,7 @@ void topology_free(Topology* top) {
     }
     tiles_free(top->crow, top->ctd);
     tiles_free(top->srow, top->ctd);
+    arena_free(&top->tiles);
     free(atomic_load(&top->ips));
     for (iptab* r = top->ips_retired; r;) {
         iptab* n = r->next;
@@ -980,6 +1033,7 @@ Topology* topology_new(const char* graphPath) {
     pthread_mutex_init(&top->compute_lock, NULL);
     pthread_mutex_init(&top->idx_lock, NULL);
     pthread_mutex_init(&top->min_lock, NULL);
+    pthread_mutex_init(&top->tiles.mu, NULL);
     atomic_store(&top->ips, NULL);
     const char* dev = getenv("SHADOWTOPO_DEVICE");
     top->device = dev ? atoi(dev) : 0;
@@ -1783,6 +1837,18 @@ static matrix* path_entry(Topology* top, Address* src, Address* dst, size_t* off
     int32_t i = atomic_load_explicit(&top->att_index[vs], memory_order_acquire);
     int32_t j = atomic_load_explicit(&top->att_index[vd], memory_order_acquire);
     matrix* m = (i >= 0 && j >= 0) ? current_matrix(top, i > j ? i : j) : NULL;
+    if (m) {
+        /* a packet makes four calls on one pair (isRoutable, getLatency, getReliability,
+         * increment; worker.c:267-279): start the pair's value line (either direction, the
+         * cache decides which one holds it) and its counter on the first call, while the
+         * cache cell is read, instead of three dependent DRAM misses */
+        const size_t A = (size_t)m->A;
+        __builtin_prefetch(&m->lr[2 * ((size_t)i * A + (size_t)j)]);
+        __builtin_prefetch(&m->lr[2 * ((size_t)j * A + (size_t)i)]);
+        const int32_t a = (!top->directed && j < i) ? j : i, b = a == i ? j : i;
+        const uint64_t* ct = tile_peek(top->crow, top->ctd, a / CTILE, b / CTILE);
+        if (ct) __builtin_prefetch(&ct[(a % CTILE) * CTILE + (b % CTILE)], 1);
+    }
     int32_t si, sj;
     if (m && cache_resolve(top, &m, i, j, &si, &sj) == 0) {
         *off = (size_t)si * (size_t)m->A + (size_t)sj;
