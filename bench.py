@@ -418,6 +418,7 @@ def main():
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
+    ap.add_argument("--dense-spec", type=int, default=-1, help="dense: leading rounds with no host read-back (0..4); -1 = engine default")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--device-rounds", type=int, default=-1, help="CSR worklist rounds driven from the device: 0 never, "
@@ -480,6 +481,8 @@ def main():
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
     if args.dense_w16 >= 0:
         eng.set_option(E.OPT_DENSE_W16, args.dense_w16)
+    if args.dense_spec >= 0:
+        eng.set_option(E.OPT_DENSE_SPEC, args.dense_spec)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
     if args.device_rounds >= 0:

@@ -49,6 +49,7 @@
 namespace {
 
 constexpr int KL = 64;                    // sources per batch = wave width
+constexpr int SPEC_MAX = 4;               // dense: most leading rounds enqueued without a read-back
 constexpr uint32_t TAINT = 0x80000000u;   // H bit: tree path crosses a heap-order tie
 constexpr uint32_t LTIE = 0x40000000u;    // H bit: the tie is at this vertex (its own predecessor choice)
 constexpr uint32_t HMASK = 0x3fffffffu;
@@ -2816,6 +2817,9 @@ struct shadowtopo_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr, evm2 = nullptr;
     hipEvent_t ev_spin = nullptr;  // round_sync
     std::vector<hipEvent_t> ev_dev;  // device-driven rounds: one pair per round of a block
+    std::vector<hipEvent_t> ev_spec;  // dense: one pair per round enqueued without a read-back
+    int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
+    int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
     shadowtopo_stats st{};
 };
 
@@ -2865,6 +2869,8 @@ void free_batches(shadowtopo_engine* eng) {
     eng->d_cnt = nullptr;
     if (eng->h_cnt) (void)hipHostFree(eng->h_cnt);
     eng->h_cnt = nullptr;
+    if (eng->h_cnt_spec) (void)hipHostFree(eng->h_cnt_spec);
+    eng->h_cnt_spec = nullptr;
     if (eng->h_wlcnt) (void)hipHostFree(eng->h_wlcnt);
     if (eng->h_wlpre) (void)hipHostFree(eng->h_wlpre);
     eng->h_wlcnt = nullptr;
@@ -2929,6 +2935,7 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     eng->h_row.assign((size_t)KL * nb, -1);
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
     HIP_TRY(hipHostMalloc((void**)&eng->h_cnt, sizeof(int32_t) * nb, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&eng->h_cnt_spec, sizeof(int32_t) * nb * SPEC_MAX, hipHostMallocDefault));
     if (!eng->dense) {
         if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wl, sizeof(int4) * VK / KL * nb)) ||
             (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlcnt, sizeof(uint32_t) * nb)) ||
@@ -3357,9 +3364,29 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         HIP_TRY(round_sync(eng, s));
         eng->st.host_syncs++;
     }
+    // dense: the first spec_rounds rounds are enqueued back to back, with no host read-back
+    // between them (the full sweep, then delta rounds; C2's step is a full sweep and two delta
+    // rounds, and each read-back left the GPU idle ~30 us).  A round whose decisions would
+    // come from an unread count runs the delta kernel over every batch that changed at all
+    // (threshold raised): exact for any set of changed pairs (the change masks hold them all),
+    // a batch that would have taken another full sweep just takes a slower delta round.  Its
+    // counts reach the host, for the statistics, with the next read-back.
+    const int32_t spec_rounds = eng->dense && !eng->opt_profile ? std::min(eng->opt_dense_spec, SPEC_MAX) : 0;
+    if (spec_rounds && eng->opt_timing && eng->ev_spec.empty()) {
+        eng->ev_spec.resize(2 * (SPEC_MAX + 1));
+        for (auto& e : eng->ev_spec) HIP_TRY(hipEventCreate(&e));
+    }
+    std::vector<uint8_t> spec_fb[SPEC_MAX];  // those rounds' full-sweep batches
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
+        const bool spec = round < spec_rounds;                   // no read-back after this round
+        const bool blind = round >= 1 && round <= spec_rounds;  // decided without the last counts
+        hipEvent_t e0 = eng->ev0, e1 = eng->ev1;
+        if (round <= spec_rounds && !eng->ev_spec.empty()) {
+            e0 = eng->ev_spec[2 * round];
+            e1 = eng->ev_spec[2 * round + 1];
+        }
         int64_t wl_total = 0;
         if (use_wl) {
             eng->h_wlpre[0] = 0;
@@ -3374,7 +3401,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
         int32_t* cnt_prev = eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
         HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
-        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev0, s));
+        if (eng->opt_timing) HIP_TRY(hipEventRecord(e0, s));
         bool round_full = false, round_delta = false;
         if (eng->dense) {
             // per batch: full sweep when its previous round changed more than `thresh` pairs,
@@ -3383,11 +3410,24 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             bool& any_delta = round_delta;
             any_full = any_delta = false;
             full_b.assign((size_t)nbg, 0);
-            for (int32_t b = 0; b < nbg; ++b) {
-                full_b[b] = eng->h_cnt[b] > thresh;
-                any_full |= full_b[b] != 0;
-                any_delta |= eng->h_cnt[b] > 0 && eng->h_cnt[b] <= thresh;
+            int32_t thr = thresh;  // delta rounds: batches that changed 1 .. thr pairs
+            if (blind && thresh == 0) {  // full sweeps only (OPT_DELTA_PERMILLE 0): every batch that changed
+                any_full = true;
+                full_b.assign((size_t)nbg, 1);
+            } else if (blind) {
+                any_delta = true;
+                thr = 0x7f7f7f7e;
+            } else {
+                for (int32_t b = 0; b < nbg; ++b) {
+                    full_b[b] = eng->h_cnt[b] > thresh;
+                    any_full |= full_b[b] != 0;
+                    any_delta |= eng->h_cnt[b] > 0 && eng->h_cnt[b] <= thresh;
+                }
             }
+            // live-chunk (sparse) delta rounds after a round that changed few pairs; blind: the
+            // round right after the full sweep is pruned, later ones sparse (C2's pattern)
+            const bool dsparse = !blind ? delta_is_sparse(eng, nbg, thr)
+                                        : (eng->opt_delta_live != 2 ? eng->opt_delta_live == 1 : round >= 2);
             const int32_t par = (int32_t)(round & 1);
             if (any_full && any_delta && eng->opt_timing) HIP_TRY(hipEventRecord(eng->evm, s));
             if (any_full) {
@@ -3405,9 +3445,8 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 if (eng->opt_dense_variant == SHADOWTOPO_DENSE_F64)
                     hipLaunchKernelGGL(k_relax_dense_delta, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
                                        eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par,
-                                       thresh, cnt_prev, cnt_cur);
-                else if (eng->vperm_ready && eng->opt_dense_prune && nvc <= PR_CHUNKS &&
-                         !delta_is_sparse(eng, nbg, thresh)) {
+                                       thr, cnt_prev, cnt_cur);
+                else if (eng->vperm_ready && eng->opt_dense_prune && nvc <= PR_CHUNKS && !dsparse) {
                     // pruned: rows and tiles in the locality order, each block walking only the
                     // chunks whose changed pairs can pass (k_min_d32c bounds, minW64); a round
                     // after one that changed few pairs takes the live-chunk lists below instead
@@ -3430,17 +3469,17 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                         eng->cmask_n = need_cm;
                     }
                     hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, nbg), dim3(256), 0, s, eng->pools,
-                                       eng->d_perm, V, nvc, par, cnt_prev, thresh, eng->d_minDc);
+                                       eng->d_perm, V, nvc, par, cnt_prev, thr, eng->d_minDc);
                     hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
-                                       nbg, nvc, par, thresh, cnt_prev, cnt_cur, nullptr, nullptr, eng->d_perm,
+                                       nbg, nvc, par, thr, cnt_prev, cnt_cur, nullptr, nullptr, eng->d_perm,
                                        eng->d_minW64, eng->d_minDc, eng->opt_delta_colbound ? eng->d_minW : nullptr,
                                        eng->opt_delta_colbound >= 2 ? eng->d_cmask : nullptr);
                     eng->st.pruned_deltas++;
                 } else {
                     // a round after one that changed few pairs walks only the chunks holding
                     // a changed row (k_live_chunks); after a full sweep nearly every chunk does
-                    const bool sparse = delta_is_sparse(eng, nbg, thresh);
+                    const bool sparse = dsparse;
                     const int32_t* live = nullptr;
                     const int32_t* nlive = nullptr;
                     if (sparse) {
@@ -3459,7 +3498,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     }
                     hipLaunchKernelGGL(k_relax_dense_delta_s<false>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
                                        s, eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
-                                       nbg, nvc, par, thresh, cnt_prev, cnt_cur, live, nlive, nullptr, nullptr,
+                                       nbg, nvc, par, thr, cnt_prev, cnt_cur, live, nlive, nullptr, nullptr,
                                        nullptr, nullptr, nullptr);
                 }
                 eng->st.delta_sweeps++;
@@ -3478,7 +3517,16 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                                eng->d_prof);
         }
         HIP_TRY(hipGetLastError());
-        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev1, s));
+        if (eng->opt_timing) HIP_TRY(hipEventRecord(e1, s));
+        if (spec) {
+            // no read-back: this round's counts follow the next read-back into h_cnt_spec
+            HIP_TRY(hipMemcpyAsync(eng->h_cnt_spec + (size_t)round * eng->nb_cap, cnt_cur, sizeof(int32_t) * nbg,
+                                   hipMemcpyDeviceToHost, s));
+            spec_fb[round] = full_b;
+            eng->st.relax_launches++;
+            eng->st.rounds++;
+            continue;
+        }
         if (use_wl) {  // the next round's worklists, from the flags this round set
             HIP_TRY(hipMemsetAsync(eng->d_wlcnt, 0, sizeof(uint32_t) * nbg, s));
             hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
@@ -3491,9 +3539,30 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         eng->st.host_syncs++;
         eng->st.relax_launches++;
         eng->st.rounds++;
+        if (round == spec_rounds) {
+            // the rounds enqueued without a read-back: their counts and times
+            for (int32_t r = 0; r < spec_rounds; ++r) {
+                const int32_t* hc = eng->h_cnt_spec + (size_t)r * eng->nb_cap;
+                const bool full = std::find(spec_fb[r].begin(), spec_fb[r].end(), 1) != spec_fb[r].end();
+                int64_t ch = 0;
+                for (int32_t b = 0; b < nbg; ++b) {
+                    ch += hc[b];
+                    if (!spec_fb[r].empty() && spec_fb[r][b]) eng->st.full_changes += hc[b];
+                }
+                float ms = 0;
+                if (eng->opt_timing) {
+                    HIP_TRY(hipEventElapsedTime(&ms, eng->ev_spec[2 * r], eng->ev_spec[2 * r + 1]));
+                    eng->st.relax_ms += ms;
+                    (full ? eng->st.full_ms : eng->st.delta_ms) += ms;
+                }
+                if (eng->trace_rounds)
+                    fprintf(stderr, "[shadowtopo] round %d batches %d items %lld %s (no read-back) changed %lld %.3f ms\n",
+                            r, nbg, (long long)nbg * V, full ? "full" : "delta", (long long)ch, ms);
+            }
+        }
         if (eng->opt_timing) {
             float ms = 0;
-            HIP_TRY(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
+            HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
             eng->st.relax_ms += ms;
             if (round_wl) eng->st.wl_ms += ms;
             if (eng->dense) {
@@ -4618,6 +4687,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_tlog) (void)hipFree(eng->d_tlog);
     if (eng->h_tlog) (void)hipHostFree(eng->h_tlog);
     for (auto e : eng->ev_dev) (void)hipEventDestroy(e);
+    for (auto e : eng->ev_spec) (void)hipEventDestroy(e);
     free_batches(eng);
     for (void* p : eng->graph_allocs) (void)hipFree(p);
     for (void* p : eng->prune_allocs) (void)hipFree(p);
@@ -4764,6 +4834,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_W16:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense W16 must be 0 or 1");
             eng->opt_dense_w16 = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DENSE_SPEC:
+            if (value < 0 || value > SPEC_MAX) return fail(SHADOWTOPO_EINVAL, "dense spec rounds must be in [0, 4]");
+            eng->opt_dense_spec = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_LIVE:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "delta live must be 0, 1 or 2");

@@ -533,3 +533,29 @@ def test_host_rows_interleaved_lat_rel(layout):
     if layout == "csr":
         assert eng.stats()["replayed_sources"] > 0
     eng.close()
+
+
+@pytest.mark.parametrize("spec", [0, 1, 2, 4])
+@pytest.mark.parametrize("case", ["geometric", "ties", "directed", "over_thresh"])
+def test_dense_rounds_without_read_back(case, spec):
+    """OPT_DENSE_SPEC: the first rounds enqueued back to back with no host read-back of their
+    change counts (a round decided blind runs the delta kernel over every batch that changed,
+    or a full sweep when delta rounds are off) give the oracle's matrices, bit for bit, and
+    fewer host synchronisations; over_thresh: a 1-per-mille delta threshold, so the batches
+    that the host would full-sweep again after round 0 take a blind delta round instead"""
+    permille = 125
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=900, A=200)
+    elif case == "ties":
+        g = synth.integer_grid(rows=11, cols=12, seed=6)
+    elif case == "directed":
+        g = synth.random_sparse(V=260, avg_deg=5, seed=9, directed=True)
+    else:
+        g = synth.geometric_complete_ish(V=700, A=150, drop=0.3)
+        permille = 1
+    st = compare(g, layout="dense", dense_spec=spec, delta_permille=permille)
+    assert st["dense"] == 1
+    if spec:
+        assert st["host_syncs"] < st["rounds"] + st["groups"], st
+    st0 = compare(g, layout="dense", dense_spec=spec, delta_permille=0)  # full sweeps only
+    assert st0["delta_sweeps"] == 0
