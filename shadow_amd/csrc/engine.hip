@@ -50,6 +50,7 @@ namespace {
 
 constexpr int KL = 64;                    // sources per batch = wave width
 constexpr int SPEC_MAX = 4;               // dense: most leading rounds enqueued without a read-back
+constexpr int CNT_ROWS = SPEC_MAX + 4;    // change-count rows per batch slot (run_rounds: cnt_row)
 constexpr uint32_t TAINT = 0x80000000u;   // H bit: tree path crosses a heap-order tie
 constexpr uint32_t LTIE = 0x40000000u;    // H bit: the tie is at this vertex (its own predecessor choice)
 constexpr uint32_t HMASK = 0x3fffffffu;
@@ -1640,10 +1641,15 @@ constexpr int SEED_T = 16;             // destinations per block: 22 KB of LDS, 
 constexpr int SEED_ST = SEED_T + 1;    // LDS row stride: the transposed reads spread over the banks
 __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__ W, const int32_t* __restrict__ WI,
                                                       int32_t Vp, const double* __restrict__ WR,
-                                                      const double* __restrict__ vfac, Pools pools, int32_t V) {
+                                                      const double* __restrict__ vfac, Pools pools, int32_t V,
+                                                      int32_t* __restrict__ cnt, int32_t cnt_rows, int32_t cnt_stride) {
     __shared__ double sw[KL * SEED_ST];
     __shared__ double sr[KL * SEED_ST];
     __shared__ int32_t si[KL * SEED_ST];
+    // the rounds' change-count rows of this batch (run_rounds: cnt_row): row 0, the virtual
+    // round -1, "everything changed"; the rows of the rounds enqueued without a read-back zero
+    if (blockIdx.x == 0 && (int)threadIdx.x < cnt_rows)
+        cnt[(size_t)threadIdx.x * cnt_stride + blockIdx.y] = threadIdx.x == 0 ? 0x7f7f7f7f : 0;
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -2744,6 +2750,7 @@ struct shadowtopo_engine {
     int32_t A = 0;
     std::vector<int32_t> h_attached;
     std::vector<uint64_t> h_key;  // locality key per attached index (OPT_SOURCE_ORDER)
+    std::vector<int32_t> h_key_order;  // attached indices sorted by h_key (stable)
     bool key_ready = false;
     int32_t opt_source_order = 1;
     int32_t opt_dense_seed = 1;
@@ -2933,9 +2940,9 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     if (state_d32(eng) && (rc = dev_alloc(eng->batch_allocs, (void**)&P.D32, VK * nb * sizeof(float)))) return rc;
     eng->h_srcv.assign((size_t)KL * nb, -1);
     eng->h_row.assign((size_t)KL * nb, -1);
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * 2 * nb))) return rc;
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_cnt, sizeof(int32_t) * CNT_ROWS * nb))) return rc;
     HIP_TRY(hipHostMalloc((void**)&eng->h_cnt, sizeof(int32_t) * nb, hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void**)&eng->h_cnt_spec, sizeof(int32_t) * nb * SPEC_MAX, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&eng->h_cnt_spec, sizeof(int32_t) * nb * (SPEC_MAX + 1), hipHostMallocDefault));
     if (!eng->dense) {
         if ((rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wl, sizeof(int4) * VK / KL * nb)) ||
             (rc = dev_alloc(eng->batch_allocs, (void**)&eng->d_wlcnt, sizeof(uint32_t) * nb)) ||
@@ -3239,9 +3246,23 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const int32_t V = g.V;
     if (!eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_PUSH && eng->d_wl) return run_push_rounds(eng, nbg, s);
     const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->d_WR && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
+    // dense: the first spec_rounds rounds are enqueued back to back, with no host read-back
+    // between them (the full sweep, then delta rounds; C2's step is a full sweep and two delta
+    // rounds, and each read-back left the GPU idle ~30 us).  A round whose decisions would
+    // come from an unread count runs the delta kernel over every batch that changed at all
+    // (threshold raised): exact for any set of changed pairs (the change masks hold them all),
+    // a batch that would have taken another full sweep just takes a slower delta round.
+    const int32_t spec_rounds = eng->dense && !eng->opt_profile ? std::min(eng->opt_dense_spec, SPEC_MAX) : 0;
+    // dense change-count rows: row 0 = the virtual round -1 ("everything changed"), rows
+    // 1 .. spec_rounds + 1 = rounds 0 .. spec_rounds (reset once, at the seed; read back in one
+    // copy with the first read-back), then two rows alternating for the host-driven rounds
+    const auto cnt_row = [&](int64_t r) {
+        const int64_t i = r < 0 ? 0 : (r <= spec_rounds ? 1 + r : spec_rounds + 2 + (r & 1));
+        return eng->d_cnt + i * eng->nb_cap;
+    };
     if (fused_seed) {
         hipLaunchKernelGGL(k_seed_dense_t, dim3(eng->Vp / SEED_T, nbg), dim3(256), 0, s, eng->d_W, eng->d_WI, eng->Vp,
-                           eng->d_WR, g.vfac, eng->pools, V);
+                           eng->d_WR, g.vfac, eng->pools, V, eng->d_cnt, spec_rounds + 2, eng->nb_cap);
         HIP_TRY(hipGetLastError());
     } else {
         const size_t total = (size_t)eng->pools.Vp * KL;
@@ -3266,8 +3287,11 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             HIP_TRY(hipGetLastError());
         }
         // round 0 consumes the change counts of a virtual round -1: every batch changed
-        // everything (full sweep)
-        HIP_TRY(hipMemsetAsync(eng->d_cnt + eng->nb_cap, 0x7f, sizeof(int32_t) * nbg, s));
+        // everything (full sweep); k_seed_dense_t resets the rows itself
+        if (!fused_seed) {
+            HIP_TRY(hipMemsetAsync(cnt_row(-1), 0x7f, sizeof(int32_t) * nbg, s));
+            HIP_TRY(hipMemsetAsync(cnt_row(0), 0, sizeof(int32_t) * eng->nb_cap * (spec_rounds + 1), s));
+        }
         for (int32_t b = 0; b < nbg; ++b) eng->h_cnt[b] = 0x7f7f7f7f;
     }
     const int32_t nvc = eng->Vp / KL;
@@ -3364,14 +3388,6 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         HIP_TRY(round_sync(eng, s));
         eng->st.host_syncs++;
     }
-    // dense: the first spec_rounds rounds are enqueued back to back, with no host read-back
-    // between them (the full sweep, then delta rounds; C2's step is a full sweep and two delta
-    // rounds, and each read-back left the GPU idle ~30 us).  A round whose decisions would
-    // come from an unread count runs the delta kernel over every batch that changed at all
-    // (threshold raised): exact for any set of changed pairs (the change masks hold them all),
-    // a batch that would have taken another full sweep just takes a slower delta round.  Its
-    // counts reach the host, for the statistics, with the next read-back.
-    const int32_t spec_rounds = eng->dense && !eng->opt_profile ? std::min(eng->opt_dense_spec, SPEC_MAX) : 0;
     if (spec_rounds && eng->opt_timing && eng->ev_spec.empty()) {
         eng->ev_spec.resize(2 * (SPEC_MAX + 1));
         for (auto& e : eng->ev_spec) HIP_TRY(hipEventCreate(&e));
@@ -3398,9 +3414,9 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         const bool round_wl = use_wl && (eng->opt_worklist == 2 || wl_total * 2 < (int64_t)nbg * V);
         if (round_wl)
             HIP_TRY(hipMemcpyAsync(eng->d_wlpre, eng->h_wlpre, sizeof(int64_t) * (nbg + 1), hipMemcpyHostToDevice, s));
-        int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;
-        int32_t* cnt_prev = eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
-        HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
+        int32_t* cnt_cur = eng->dense ? cnt_row(round) : eng->d_cnt + (round & 1) * eng->nb_cap;
+        int32_t* cnt_prev = eng->dense ? cnt_row(round - 1) : eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
+        if (!eng->dense || round > spec_rounds) HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
         if (eng->opt_timing) HIP_TRY(hipEventRecord(e0, s));
         bool round_full = false, round_delta = false;
         if (eng->dense) {
@@ -3519,9 +3535,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         HIP_TRY(hipGetLastError());
         if (eng->opt_timing) HIP_TRY(hipEventRecord(e1, s));
         if (spec) {
-            // no read-back: this round's counts follow the next read-back into h_cnt_spec
-            HIP_TRY(hipMemcpyAsync(eng->h_cnt_spec + (size_t)round * eng->nb_cap, cnt_cur, sizeof(int32_t) * nbg,
-                                   hipMemcpyDeviceToHost, s));
+            // no read-back: this round's counts come back with the next one (h_cnt_spec)
             spec_fb[round] = full_b;
             eng->st.relax_launches++;
             eng->st.rounds++;
@@ -3534,9 +3548,18 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
         }
-        HIP_TRY(hipMemcpyAsync(eng->h_cnt, cnt_cur, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
+        if (eng->dense && round == spec_rounds && spec_rounds > 0) {
+            // the counts of every round since the seed, rows 1 .. spec_rounds + 1, in one copy
+            HIP_TRY(hipMemcpyAsync(eng->h_cnt_spec, cnt_row(0), sizeof(int32_t) * eng->nb_cap * (spec_rounds + 1),
+                                   hipMemcpyDeviceToHost, s));
+        } else {
+            HIP_TRY(hipMemcpyAsync(eng->h_cnt, cnt_cur, sizeof(int32_t) * nbg, hipMemcpyDeviceToHost, s));
+        }
         HIP_TRY(round_sync(eng, s));
         eng->st.host_syncs++;
+        if (eng->dense && round == spec_rounds && spec_rounds > 0)
+            std::copy(eng->h_cnt_spec + (size_t)spec_rounds * eng->nb_cap,
+                      eng->h_cnt_spec + (size_t)spec_rounds * eng->nb_cap + nbg, eng->h_cnt);
         eng->st.relax_launches++;
         eng->st.rounds++;
         if (round == spec_rounds) {
@@ -3768,22 +3791,33 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
     return SHADOWTOPO_OK;
 }
 
+// the attached rows in key order (ties by row), once per attached set: a group's lanes are
+// then its rows picked out of it in one pass, instead of a sort per group and call (C2's
+// 1000-row group: tens of microseconds of host time between the steps)
+static void key_order(shadowtopo_engine* eng) {
+    eng->h_key_order.resize((size_t)eng->A);
+    for (int32_t i = 0; i < eng->A; ++i) eng->h_key_order[i] = i;
+    std::stable_sort(eng->h_key_order.begin(), eng->h_key_order.end(),
+                     [&](int32_t x, int32_t y) { return eng->h_key[x] < eng->h_key[y]; });
+    eng->key_ready = true;
+}
+
 int ensure_locality(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->key_ready) return SHADOWTOPO_OK;
     if (eng->A <= KL) {
         eng->h_key.assign((size_t)eng->A, 0);
-        eng->key_ready = true;
+        key_order(eng);
         return SHADOWTOPO_OK;
     }
     if (eng->vperm_ready && !eng->h_vkey.empty()) {  // the pruned sweep's vertex keys
         eng->h_key.resize((size_t)eng->A);
         for (int32_t i = 0; i < eng->A; ++i) eng->h_key[i] = eng->h_vkey[eng->h_attached[i]];
-        eng->key_ready = true;
+        key_order(eng);
         return SHADOWTOPO_OK;
     }
     int rc = locality_keys(eng, s, eng->h_attached, eng->h_key, 8, true);
     if (rc) return rc;
-    eng->key_ready = true;
+    key_order(eng);
     return SHADOWTOPO_OK;
 }
 
@@ -4096,11 +4130,14 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             // the slot's previous rows (group g - 2) must have left before compose rewrites it
             if (pinned_out && gidx >= nslots) HIP_TRY(hipStreamWaitEvent(s, eng->ev_copy[slot], 0));
         }
-        lane_row.resize((size_t)nbg * KL);
-        for (size_t i = 0; i < lane_row.size(); ++i) lane_row[i] = r0 + (int32_t)i < r1 ? r0 + (int32_t)i : -1;
-        if (order)
-            std::stable_sort(lane_row.begin(), lane_row.begin() + (r1 - r0),
-                             [&](int32_t x, int32_t y) { return eng->h_key[x] < eng->h_key[y]; });
+        lane_row.assign((size_t)nbg * KL, -1);
+        if (order) {  // the group's rows in key order (key_order)
+            size_t n = 0;
+            for (const int32_t row : eng->h_key_order)
+                if (row >= r0 && row < r1) lane_row[n++] = row;
+        } else {
+            for (int32_t i = 0; i < r1 - r0; ++i) lane_row[i] = r0 + i;
+        }
         for (size_t i = 0; i < lane_row.size(); ++i) {
             const int32_t row = lane_row[i];
             const int32_t v = row >= 0 ? eng->h_attached[row] : -1;
