@@ -13,6 +13,7 @@
 #include <netinet/in.h>
 #include <stdarg.h>
 #include <stdint.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -33,7 +34,9 @@ struct _Random {
     unsigned int initialSeed;
 };
 
-static double g_last_min_jump = -1.0;
+/* the last upcall's value; worker threads upcall concurrently (Shadow's master takes a lock,
+ * master.c:148-159), so the stand-in keeps it in one atomic word */
+static _Atomic double g_last_min_jump = -1.0;
 static int g_log_level = -1;
 
 __attribute__((weak)) uint32_t address_toNetworkIP(Address* address) { return address->ip; }
@@ -54,7 +57,9 @@ __attribute__((weak)) double random_nextDouble(Random* random) {
     return (double)(((double)v) / ((double)RAND_MAX));
 }
 
-__attribute__((weak)) void worker_updateMinTimeJump(double minPathLatency) { g_last_min_jump = minPathLatency; }
+__attribute__((weak)) void worker_updateMinTimeJump(double minPathLatency) {
+    atomic_store_explicit(&g_last_min_jump, minPathLatency, memory_order_relaxed);
+}
 
 Address* shadowtopo_address_new(const char* ipString, const char* name) {
     Address* a = (Address*)calloc(1, sizeof(Address));
@@ -83,7 +88,7 @@ Random* shadowtopo_random_new(uint32_t seed) {
 
 void shadowtopo_random_free(Random* r) { free(r); }
 
-double shadowtopo_last_min_time_jump(void) { return g_last_min_jump; }
+double shadowtopo_last_min_time_jump(void) { return atomic_load_explicit(&g_last_min_jump, memory_order_relaxed); }
 
 void shadowtopo_set_log_level(int level) { g_log_level = level; }
 

@@ -403,13 +403,18 @@ def test_self_pairs_follow_query_order_under_the_s_path_rule(tmp_path):
     top.free()
 
 
-def test_lock_free_cache_under_racing_workers(tmp_path):
+@pytest.mark.parametrize("tsan", [False, True])
+def test_lock_free_cache_under_racing_workers(tmp_path, tsan):
     """the path cache is lock-free (a CAS claim per Path, a CAS per source store
     loop, in-place fills of old rows after a late attach).  8 C worker threads
     (tests/c/topo_race.c) query and count packets over overlapping pairs of 32 hosts, then of
     48 after a late attach that the workers themselves resolve.  Every returned value must be
     the oracle's entry of the direction the pair is cached in, no unordered pair may be cached
-    in both directions, cached_paths must equal the cached cells, and no increment is lost."""
+    in both directions, cached_paths must equal the cached cells, and no increment is lost.
+    tsan: the shim's C sources compiled into the harness with ThreadSanitizer (host code
+    only; the engine library stays uninstrumented and its shim copy is interposed), which
+    must report no data race."""
+    import platform
     import subprocess
     from test_topology_shim import INCLUDE
     from shadow_amd import engine as E
@@ -421,11 +426,26 @@ def test_lock_free_cache_under_racing_workers(tmp_path):
     src = os.path.join(os.path.dirname(__file__), "c", "topo_race.c")
     lib_dir = os.path.dirname(E.LIB_PATH)
     exe = str(tmp_path / "topo_race")
-    subprocess.run(["gcc", "-O2", "-std=gnu11", "-pthread", "-I", INCLUDE, src, "-o", exe, "-L", lib_dir,
-                    "-lshadowtopo_hip", f"-Wl,-rpath,{lib_dir}"], check=True)
+    cmd = ["gcc", "-O2", "-std=gnu11", "-pthread", "-I", INCLUDE, src]
+    env = dict(os.environ)
+    if tsan:
+        csrc = os.path.join(os.path.dirname(os.path.dirname(__file__)), "shadow_amd", "csrc")
+        # (non-PIE: a PIE image loaded high by the box's kernel ASLR is outside TSan's expected layout)
+        cmd = ["gcc", "-O1", "-g", "-fsanitize=thread", "-fno-pie", "-no-pie", "-std=gnu11", "-pthread", "-ffp-contract=off", "-I", INCLUDE,
+               "-I", csrc, src] + [os.path.join(csrc, f) for f in ("topology_hip.c", "graphml.c", "shadow_hooks.c")]
+        # the ROCm runtime and the engine are not instrumented: TSan cannot see their own
+        # synchronisation, so what they allocate and free on their threads is not checked
+        supp = write(tmp_path, "tsan.supp", "".join(f"called_from_lib:{lib}\nrace:{lib}\n" for lib in
+                                                    ("libhsa-runtime64.so", "libamdhip64.so", "libshadowtopo_hip.so")))
+        env["TSAN_OPTIONS"] = f"halt_on_error=1 exitcode=66 suppressions={supp}"
+    subprocess.run(cmd + ["-o", exe, "-L", lib_dir, "-lshadowtopo_hip", f"-Wl,-rpath,{lib_dir}", "-lm"], check=True)
     out = str(tmp_path / "recs.bin")
-    res = subprocess.run([exe, path, hints, "32", "16", "8", "3000", out], check=True, capture_output=True,
-                         text=True, timeout=300)
+    # (TSan: without address-space randomisation -- the box's kernel places mappings where this
+    # TSan does not expect them)
+    pre = ["setarch", platform.machine(), "-R"] if tsan else []
+    res = subprocess.run(pre + [exe, path, hints, "32", "16", "8", "1000" if tsan else "3000", out],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0 and "ThreadSanitizer" not in res.stderr, res.stderr[-4000:]
     lines = res.stdout.strip().splitlines()
     head = json.loads(lines[0])
     assert head["compute_failed"] == 0
@@ -442,7 +462,7 @@ def test_lock_free_cache_under_racing_workers(tmp_path):
     assert total == head["increments"]
     rec = np.fromfile(out, dtype=[("phase", "<i4"), ("i", "<i4"), ("j", "<i4"), ("pad", "<i4"),
                                   ("lat", "<f8"), ("rel", "<f8")])
-    assert len(rec) == 2 * 8 * 3000
+    assert len(rec) == 2 * 8 * (1000 if tsan else 3000)
     lat_o, rel_o, _, kind_o, _ = oracle_matrix(g)
     for r in rec:
         i, j = int(r["i"]), int(r["j"])
