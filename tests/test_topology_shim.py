@@ -451,3 +451,48 @@ def test_prepare_rejects_a_bad_device():
         E.prepare(-1)
     with pytest.raises(E.ShadowTopoError):
         E.prepare(E.device_count())
+
+
+def test_host_paths_under_address_sanitizer(tmp_path):
+    """The shim's host code -- GraphML reader, validation (accepted and rejected graphs,
+    truncated and garbage files), the three attach hint paths, detach / re-attach churn of
+    the lock-free IP table, teardown -- compiled with AddressSanitizer and UBSan
+    (tests/c/shim_asan.c; host code only, the engine library uninstrumented): no memory
+    error, no undefined behaviour, and the same accept / reject decisions as the library."""
+    import subprocess
+    csrc = os.path.join(os.path.dirname(os.path.dirname(__file__)), "shadow_amd", "csrc")
+    lib_dir = os.path.dirname(E.LIB_PATH)
+    exe = str(tmp_path / "shim_asan")
+    subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", "-std=gnu11", "-pthread", "-ffp-contract=off", "-I", INCLUDE, "-I", csrc,
+                    os.path.join(os.path.dirname(__file__), "c", "shim_asan.c")] +
+                   [os.path.join(csrc, f) for f in ("topology_hip.c", "graphml.c", "shadow_hooks.c")] +
+                   ["-o", exe, "-L", lib_dir, "-lshadowtopo_hip", f"-Wl,-rpath,{lib_dir}", "-lm"], check=True)
+    files, want = [], []
+    shipped = lzma.open(os.path.join(GOLD, "c1_topology.graphml.xml.xz"), "rt").read()
+    files.append(write(tmp_path, "c1.xml", shipped))
+    want.append(True)
+    for i, (kw, ok) in enumerate([({}, True), ({"lat": "0"}, False), ({"loss": "1.5"}, False), ({"lt": "string"}, False),
+                                  ({"ed": "directed"}, False)]):
+        files.append(write(tmp_path, f"v{i}.xml", mk(**kw)))
+        want.append(ok)
+    for seed, dup in ((13, False), (14, True)):
+        _, text, _ = attach_graph(n=300, seed=seed, dup_ips=dup)
+        files.append(write(tmp_path, f"a{seed}.xml", text))
+        want.append(True)
+        files.append(write(tmp_path, f"t{seed}.xml", text[: len(text) // 2]))  # truncated mid-file
+        want.append(False)
+    files.append(write(tmp_path, "garbage.xml", "<graphml><graph><node id=\"a\"><data key=\"zz\">\x01\x02</data>"))
+    want.append(False)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=66",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=67")
+    res = subprocess.run([exe, "400"] + files, capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0 and "Sanitizer" not in res.stderr and "runtime error" not in res.stderr, \
+        res.stderr[-4000:]
+    lines = res.stdout.strip().splitlines()
+    assert len(lines) == len(files)
+    for ln, f, ok in zip(lines, files, want):
+        parts = ln.split()
+        assert parts[0] == f and (parts[1] == "ok") == ok, ln
+        if ok:
+            assert int(parts[3]) > 0
