@@ -1007,7 +1007,8 @@ __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ 
 //    exactly in f64 (D and W from global memory) in row order -- the same lexicographic
 //    minimum and tie flag as a sequential scan.
 constexpr int SRS = 32;  // rows per LDS chunk
-constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FTDT; 4 was slower: 4.63 vs 3.8 ms on C2)
+constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FTDT; 4 was slower: 4.63 vs 3.8 ms on C2;
+                         // 16: 122 VGPRs and 4 waves per SIMD in the chunk loop, spills in the exact pass)
 
 // Occupancy: LDS (24 KB per block) allows 6 blocks = 6 waves per SIMD, and 80 VGPRs fit 6
 // (the kernel wants 82, i.e. 5 waves); waves_per_eu(6) spills 3 dwords outside the chunk
@@ -3073,7 +3074,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                 hipLaunchKernelGGL(k_w16, dim3(4096), dim3(256), 0, s, eng->d_W32p, eng->d_W16p, n);
             }
             bool w16 = false;
-            if constexpr (TB == 1) {
+            if constexpr (TB == 1 && TDT == 8) {
                 w16 = eng->opt_dense_w16 != 0;
                 if (w16)
                     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1, 4, true>), dim3((uint32_t)nblocks), dim3(256),
