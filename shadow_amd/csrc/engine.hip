@@ -1116,7 +1116,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     const int32_t nchunks = nrows / SRS;
     // this wave's hit log [TB][nchunks] of row masks, indexed by (batch group, wave tile) so the
     // exact-pass kernel finds it whatever block shape wrote it
-    const int64_t gw = (int64_t)grp * (Vp / TDT) + v0 / TDT;
+    // per batch and wave tile: the log rows of batch b0 + k (the same place whatever TB the
+    // chunk loop ran with, so the exact pass may run one batch per wave)
+    const auto hl_at = [&](int k) { return ((size_t)(b0 + k) * (size_t)(Vp / TDT) + (size_t)(v0 / TDT)) * nchunks; };
     if constexpr (PH != 2) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const f4 gf4;
@@ -1293,7 +1295,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         if (lane < nw && !((lv >> lane) & 1ull)) {
             const int32_t c = chunk_of(base + lane);
 #pragma unroll
-            for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + c] = 0u;
+            for (int k = 0; k < TB; ++k) hitlog[hl_at(k) + c] = 0u;
         }
         return lv;
     };
@@ -1456,7 +1458,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         }
         if (lane == 0) {
 #pragma unroll
-            for (int k = 0; k < TB; ++k) hitlog[((size_t)gw * TB + k) * nchunks + (u0 / SRS)] = hits[k];
+            for (int k = 0; k < TB; ++k) hitlog[hl_at(k) + (u0 / SRS)] = hits[k];
         }
         if (more) {
             stash(cur ^ 1);
@@ -1476,7 +1478,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
 #pragma unroll
     for (int k = 0; k < TB; ++k) {
         if (!live[k]) continue;
-        const uint32_t* hl = hitlog + ((size_t)gw * TB + k) * nchunks;
+        const uint32_t* hl = hitlog + hl_at(k);
         const gdouble* Dl = B[k].D + lane;
         const int32_t vl = v0 + (lane & (TDT - 1));  // PR: a position (W is permuted), else the vertex
         for (int32_t c0 = 0; c0 < nchunks; c0 += 64) {
@@ -3066,7 +3068,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
         }
         hipLaunchKernelGGL(k_min_d32, dim3((uint32_t)((nchunks + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
                            eng->d_perm, (int32_t)nchunks, eng->d_minD);
-        if (TB == 1 && eng->opt_sweep_split) {  // the chunk loop, then the exact pass + epilogue
+        if (TB <= 2 && eng->opt_sweep_split) {  // the chunk loop, then the exact pass + epilogue
             if (eng->opt_dense_w16 && !eng->d_W16p) {
                 const size_t n = (size_t)eng->Vp * eng->Vp;
                 hipError_t e = hipMalloc((void**)&eng->d_W16p, n * sizeof(uint16_t));
@@ -3089,8 +3091,10 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
                                eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
                                eng->opt_sweep_win1);
-            // (4 logged rows in flight per wave instead of 2 measured the same, r03u)
-            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 2>), dim3((uint32_t)nblocks), dim3(256), 0, s,
+            // (4 logged rows in flight per wave instead of 2 measured the same, r03u); one batch
+            // per wave whatever TB the chunk loop ran with (the f64 state of two would spill)
+            const int64_t nblocks1 = 8 * (((int64_t)nbg * ntb + 7) / 8);
+            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 2>), dim3((uint32_t)nblocks1), dim3(256), 0, s,
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
                                eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,

@@ -559,3 +559,19 @@ def test_dense_rounds_without_read_back(case, spec):
         assert st["host_syncs"] < st["rounds"] + st["groups"], st
     st0 = compare(g, layout="dense", dense_spec=spec, delta_permille=0)  # full sweeps only
     assert st0["delta_sweeps"] == 0
+
+
+@pytest.mark.parametrize("tb", [1, 2, 4])
+@pytest.mark.parametrize("case", ["geometric", "geometric_odd", "ties"])
+def test_dense_batches_per_wave(case, tb):
+    """OPT_DENSE_BATCHES_PER_WAVE: the chunk loop filtering 1, 2 or 4 batches per wave against
+    one staged W32 slab (the exact pass then one batch per wave, from the per-batch hit log),
+    with an odd batch count, bit for bit the oracle's matrices"""
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=900, A=256)
+    elif case == "geometric_odd":
+        g = synth.geometric_complete_ish(V=611, A=150)  # 3 batches: a half-empty wave group
+    else:
+        g = synth.integer_grid(rows=11, cols=12, seed=6)
+    st = compare(g, layout="dense", dense_batches_per_wave=tb)
+    assert st["dense"] == 1 and st["full_sweeps"] >= 1
