@@ -107,11 +107,36 @@ typedef __attribute__((address_space(1))) uint32_t guint;
 typedef __attribute__((address_space(1))) int32_t gint;
 typedef __attribute__((address_space(1))) uint8_t gbyte;
 
+// The tree record of a (vertex, source) pair: reliability fold, hops | TAINT | LTIE and the
+// predecessor in-arc, interleaved in 16 bytes, so the predecessor gather of a changed pair
+// (finish_vertex: one lane, one scattered record) touches one cache line instead of two,
+// and a visit reads / writes its own record with one 16-byte access per lane.
+struct __attribute__((aligned(16))) Rec {
+    double r;
+    uint32_t h;
+    int32_t p;
+};
+typedef __attribute__((address_space(1))) Rec gRec;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+
+__device__ __forceinline__ Rec rec_load(const gRec* q) {
+    const u32x4 v = *(const gu32x4*)q;
+    Rec x;
+    x.r = __longlong_as_double((long long)(((unsigned long long)v.y << 32) | v.x));
+    x.h = v.z;
+    x.p = (int32_t)v.w;
+    return x;
+}
+
+__device__ __forceinline__ void rec_store(gRec* q, double r, uint32_t h, int32_t p) {
+    const unsigned long long rb = (unsigned long long)__double_as_longlong(r);
+    *(gu32x4*)q = u32x4{(uint32_t)rb, (uint32_t)(rb >> 32), h, (uint32_t)p};
+}
+
 struct Pools {
     double* D;          // [slot][Vp][64] distance
-    uint32_t* H;        // [slot][Vp][64] hops | TAINT
-    double* R;          // [slot][Vp][64] reliability fold along the tree path
-    int32_t* P;         // [slot][Vp][64] predecessor in-arc
+    Rec* Q;             // [slot][Vp][64] tree record {reliability fold, hops | TAINT, predecessor in-arc}
     uint8_t* act;       // [slot][2][Vp] frontier flags, alternating rounds
     int32_t* srcv;      // [slot][64] source vertex per lane (-1 = unused lane)
     int32_t* row;       // [slot][64] attached row per lane (-1 = none)
@@ -126,9 +151,7 @@ struct Pools {
 
 struct BatchDev {
     gdouble* D;
-    guint* H;
-    gdouble* R;
-    gint* P;
+    gRec* Q;
     gbyte* act0;
     gbyte* act1;
     const int32_t* srcv;
@@ -146,9 +169,7 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     BatchDev B;
     const size_t o = (size_t)b * (size_t)p.vk;
     B.D = (gdouble*)(p.D + o);
-    B.H = (guint*)(p.H + o);
-    B.R = (gdouble*)(p.R + o);
-    B.P = (gint*)(p.P + o);
+    B.Q = (gRec*)(p.Q + o);
     B.act0 = (gbyte*)(p.act + (size_t)b * 2 * p.Vp);
     B.act1 = B.act0 + p.Vp;
     B.srcv = p.srcv + (size_t)b * KL;
@@ -256,9 +277,7 @@ __global__ void k_init(Pools pools, int32_t V, int32_t tree) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         B.D[i] = inf;
         if (tree) {
-            B.H[i] = 0;
-            B.R[i] = 0.0;
-            B.P[i] = -1;
+            rec_store(B.Q + i, 0.0, 0u, -1);
         }
     }
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
@@ -287,9 +306,7 @@ __global__ void k_seed(GraphDev g, Pools pools) {
     if (threadIdx.x == 0) {
         const size_t idx = (size_t)s * KL + j;
         B.D[idx] = 0.0;
-        B.H[idx] = 0;
-        B.R[idx] = g.vfac[s];
-        B.P[idx] = -1;
+        rec_store(B.Q + idx, g.vfac[s], 0u, -1);
         // dense mode: f32 filter key NaN (the source's own row never passes a dense filter:
         // its seed candidate starts every lexicographic state, k_relax_dense_f), and the
         // first delta round reads the change masks of a virtual round -1
@@ -307,8 +324,9 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
                                               uint32_t curH, double curR, int32_t curP) {
     const size_t idx = (size_t)v * KL + lane;
     const size_t uidx = (size_t)u * KL + lane;
-    const uint32_t hu = B.H[uidx];
-    const double ru = B.R[uidx];
+    const Rec qu = rec_load(B.Q + uidx);  // the predecessor's record: one line per lane
+    const uint32_t hu = qu.h;
+    const double ru = qu.r;
     // local tie: two candidates share (fl(d(u)+w), d(u)), or the degenerate d(u) == d(v)
     const uint32_t taint = (hu & TAINT) | ((tie || bdu == bc) ? (TAINT | LTIE) : 0u);
     const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | taint;
@@ -316,9 +334,7 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
     if (bc != curD || h != curH || r != curR || arc != curP) {
         B.D[idx] = bc;
         if (B.D32) B.D32[idx] = f32_key(bc);
-        B.H[idx] = h;
-        B.R[idx] = r;
-        B.P[idx] = arc;
+        rec_store(B.Q + idx, r, h, arc);
         return true;
     }
     return false;
@@ -357,9 +373,10 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
     const int32_t sv = B.srcv[lane];
     const size_t idx = (size_t)v * KL + lane;
     const double curD = B.D[idx];
-    const uint32_t curH = B.H[idx];
-    const double curR = B.R[idx];
-    const int32_t curP = B.P[idx];
+    const Rec cur = rec_load(B.Q + idx);
+    const uint32_t curH = cur.h;
+    const double curR = cur.r;
+    const int32_t curP = cur.p;
     const gdouble* Dl = B.D + lane;
     // (unlike the dense kernel, the running best is not seeded with curD here: rows are
     // short, and seeding would put curD's load latency in front of the first row loads)
@@ -708,9 +725,7 @@ __global__ void k_seed_push(GraphDev g, Pools pools) {
     if (s < 0) return;
     const size_t idx = (size_t)s * KL + j;
     B.D[idx] = 0.0;
-    B.H[idx] = 0;
-    B.R[idx] = g.vfac[s];
-    B.P[idx] = -1;
+    rec_store(B.Q + idx, g.vfac[s], 0u, -1);
     atomicOr(&B.chm0[s], 1ull << j);
     B.act0[s] = 1;
 }
@@ -734,7 +749,7 @@ __global__ __launch_bounds__(256) void k_pred_pass(const int64_t* __restrict__ i
     if (__ballot(src)) {  // a source vertex of some lane: fold round 1 starts at its out-neighbours
         for (int64_t x = in_ptr[v] + lane; x < in_ptr[v + 1]; x += 64) B.act1[in_src[x]] = 1;
     }
-    if (!(dv < dinf()) && !src) B.H[idx] = 0u;  // unreached: never folded (k_fold tests H alone)
+    if (!(dv < dinf()) && !src) B.Q[idx].h = 0u;  // unreached: never folded (k_fold tests H alone)
     if (!__ballot(dv < dinf() && !src)) return;
     const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
     const gdouble* Dl = B.D + lane;
@@ -759,8 +774,8 @@ __global__ __launch_bounds__(256) void k_pred_pass(const int64_t* __restrict__ i
     }
     if (dv < dinf() && !src && sv >= 0) {
         // bc == dv: the distances are the fixed point of exactly this minimum
-        B.P[idx] = be;
-        B.H[idx] = HNOT | ((tie || bdu == bc) ? LTIE : 0u);
+        B.Q[idx].p = be;
+        B.Q[idx].h = HNOT | ((tie || bdu == bc) ? LTIE : 0u);
     }
 }
 
@@ -772,17 +787,17 @@ __device__ __forceinline__ void fold_visit(const int32_t* __restrict__ in_src, c
                                            const BatchDev& B, int32_t b, int32_t v, int lane, int32_t parity,
                                            uint32_t k, int32_t* __restrict__ cnt) {
     const size_t idx = (size_t)v * KL + lane;
-    const uint32_t hv = B.H[idx];
+    const Rec qv = rec_load(B.Q + idx);
+    const uint32_t hv = qv.h;
     bool fin = false;
     if ((hv & HMASK) == HNOT) {
-        const int32_t arc = B.P[idx];
+        const int32_t arc = qv.p;
         const int32_t u = in_src[arc];
-        const size_t uidx = (size_t)u * KL + lane;
-        const uint32_t hu = B.H[uidx];
+        const Rec qu = rec_load(B.Q + (size_t)u * KL + lane);
+        const uint32_t hu = qu.h;
         if ((hu & HMASK) < k) {
             const uint32_t taint = (hu & TAINT) | ((hv & LTIE) ? (TAINT | LTIE) : 0u);
-            B.H[idx] = (((hu & HMASK) + 1u) & HMASK) | taint;
-            B.R[idx] = B.R[uidx] * in_r[arc];
+            rec_store(B.Q + idx, qu.r * in_r[arc], (((hu & HMASK) + 1u) & HMASK) | taint, arc);
             fin = true;
         }
     }
@@ -904,18 +919,18 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
                 const int32_t arc = sr.WIp[sr.srow + v0 + t];
                 const double r = sr.rs * sr.WRp[sr.srow + v0 + t];
                 const uint32_t h = 1u | ((((tie >> t) & 1u) || bdu[t] == bc[t]) ? (TAINT | LTIE) : 0u);
-                if (bc[t] != B.D[idx] || h != B.H[idx] || r != B.R[idx] || arc != B.P[idx]) {
+                const Rec cur = rec_load(B.Q + idx);
+                if (bc[t] != B.D[idx] || h != cur.h || r != cur.r || arc != cur.p) {
                     B.D[idx] = bc[t];
                     if (B.D32) B.D32[idx] = f32_key(bc[t]);
-                    B.H[idx] = h;
-                    B.R[idx] = r;
-                    B.P[idx] = arc;
+                    rec_store(B.Q + idx, r, h, arc);
                     ch = true;
                 }
             } else {
                 const int32_t arc = WI[(size_t)bu[t] * Vp + v];
+                const Rec cur = rec_load(B.Q + idx);
                 ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx],
-                                   B.H[idx], B.R[idx], B.P[idx]);
+                                   cur.h, cur.r, cur.p);
             }
             B.BDU[idx] = bdu[t];
         }
@@ -1611,8 +1626,9 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
     const int32_t sv = B.srcv[lane];
     if (sv < 0) return;
     const int32_t v0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * DT;
-    const uint32_t hs = B.H[(size_t)sv * KL + lane];
-    const double rs = B.R[(size_t)sv * KL + lane];
+    const Rec qs = rec_load(B.Q + (size_t)sv * KL + lane);
+    const uint32_t hs = qs.h;
+    const double rs = qs.r;
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
         const int32_t v = v0 + t;
@@ -1623,9 +1639,7 @@ __global__ __launch_bounds__(256) void k_seed_dense(const double* __restrict__ W
         const int32_t arc = WI[(size_t)sv * Vp + v];
         B.D[idx] = 0.0 + w;
         B.D32[idx] = f32_key(0.0 + w);
-        B.H[idx] = ((hs & HMASK) + 1u) | (hs & TAINT);
-        B.R[idx] = rs * in_r[arc];
-        B.P[idx] = arc;
+        rec_store(B.Q + idx, rs * in_r[arc], ((hs & HMASK) + 1u) | (hs & TAINT), arc);
         B.BDU[idx] = 0.0;
     }
 }
@@ -1700,9 +1714,7 @@ __global__ __launch_bounds__(256) void k_seed_dense_t(const double* __restrict__
         const size_t idx = (size_t)v * KL + lane;
         B.D[idx] = d;
         B.D32[idx] = d32;
-        B.H[idx] = h;
-        B.R[idx] = r;
-        B.P[idx] = p;
+        rec_store(B.Q + idx, r, h, p);
         B.BDU[idx] = bdu;
         const unsigned long long reach = __ballot(seeded);
         const unsigned long long srcm = __ballot(own);
@@ -1724,10 +1736,11 @@ __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, in
                                                 const int32_t* __restrict__ in_src, const double* __restrict__ in_r,
                                                 double* sdcell, float* tcell = nullptr) {
     const size_t idx = (size_t)v * KL + s;
-    const uint32_t hv = B.H[idx];
+    const Rec qv = rec_load(B.Q + idx);
+    const uint32_t hv = qv.h;
     uint32_t lt = 0;
     if (!(c < cur)) {  // c == d(v): the recorded predecessor refreshed, or a same-distance rival
-        const int32_t pa = B.P[idx];
+        const int32_t pa = qv.p;
         const int32_t pu = pa >= 0 ? in_src[pa] : -1;
         const double bdu = B.BDU[idx];
         if (pu == u) {
@@ -1738,7 +1751,7 @@ __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, in
         } else if (du == bdu) {
             const uint32_t nh = hv | LTIE | TAINT;
             if (nh == hv) return false;
-            B.H[idx] = nh;
+            B.Q[idx].h = nh;
             return (hv & TAINT) == 0;
         } else if (du > bdu) {
             return false;
@@ -1747,19 +1760,16 @@ __device__ __forceinline__ bool delta_candidate(const BatchDev& B, int32_t v, in
     if (du == c) lt = LTIE;  // degenerate d(u) == d(v): the reference order is heap-dependent
     const int32_t arc = WI[(size_t)u * Vp + v];
     const size_t uidx = (size_t)u * KL + s;
-    const uint32_t hu = B.H[uidx];
-    const double ru = B.R[uidx];
-    const uint32_t h = (((hu & HMASK) + 1u) & HMASK) | (hu & TAINT) | (lt ? (TAINT | LTIE) : 0u);
-    const double r = ru * in_r[arc];
+    const Rec qu = rec_load(B.Q + uidx);
+    const uint32_t h = (((qu.h & HMASK) + 1u) & HMASK) | (qu.h & TAINT) | (lt ? (TAINT | LTIE) : 0u);
+    const double r = qu.r * in_r[arc];
     B.BDU[idx] = du;
     if (sdcell) *sdcell = c;
     if (tcell) *tcell = f32_thr(c);
-    if (c != cur || h != hv || r != B.R[idx] || arc != B.P[idx]) {
+    if (c != cur || h != hv || r != qv.r || arc != qv.p) {
         B.D[idx] = c;
         B.D32[idx] = f32_key(c);
-        B.H[idx] = h;
-        B.R[idx] = r;
-        B.P[idx] = arc;
+        rec_store(B.Q + idx, r, h, arc);
         return true;
     }
     return false;
@@ -2398,8 +2408,8 @@ __device__ void walk_tree(const GraphDev& g, const BatchDev& B, int lane, int32_
     double lat = 0.0, rel = g.vfac[s] * g.vfac[t];
     for (uint32_t i = 0; i < h; ++i) {
         int32_t x = t;
-        for (uint32_t k = 0; k + 1 + i < h; ++k) x = g.in_src[B.P[(size_t)x * KL + lane]];
-        const int32_t arc = B.P[(size_t)x * KL + lane];
+        for (uint32_t k = 0; k + 1 + i < h; ++k) x = g.in_src[B.Q[(size_t)x * KL + lane].p];
+        const int32_t arc = B.Q[(size_t)x * KL + lane].p;
         lat += g.elat[g.in_eid[arc]];
         rel *= g.in_r[arc];
     }
@@ -2443,7 +2453,8 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
                 const size_t idx = (size_t)t * KL + lane;
                 const double d = B.D[idx];
                 if (d < dinf()) {
-                    const uint32_t h = B.H[idx];
+                    const Rec q = rec_load(B.Q + idx);
+                    const uint32_t h = q.h;
                     o.taint = (h & TAINT) != 0;
                     o.hops = h & HMASK;
                     o.lat = (d == 0) ? 1.0 : d;  // topology.c:1848-1852
@@ -2451,7 +2462,7 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
                     if (g.multigraph || g.vfac[t] != 1.0)
                         walk_tree(g, B, lane, s, t, o.hops, o);
                     else
-                        o.rel = B.R[idx];
+                        o.rel = q.r;
                 }
             }
         }
@@ -2681,11 +2692,11 @@ __global__ void k_extract(GraphDev g, Pools pools, int32_t nsrc, double* dist, i
     const bool reached = d < dinf();  // an unreached state's H / R / P were never written
     if (dist) dist[o] = d;
     if (pred) {
-        const int32_t p = reached ? B.P[idx] : -1;
+        const int32_t p = reached ? B.Q[idx].p : -1;
         pred[o] = p >= 0 ? g.in_src[p] : -1;
     }
-    if (hops) hops[o] = reached ? B.H[idx] & HMASK : 0u;
-    if (tie) tie[o] = (reached && (B.H[idx] & TAINT)) ? 1 : 0;
+    if (hops) hops[o] = reached ? B.Q[idx].h & HMASK : 0u;
+    if (tie) tie[o] = (reached && (B.Q[idx].h & TAINT)) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- host side
@@ -2928,9 +2939,7 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     P.Vp = pvp;
     int rc;
     if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.D, VK * nb * sizeof(double))) ||
-        (rc = dev_alloc(eng->batch_allocs, (void**)&P.H, VK * nb * sizeof(uint32_t))) ||
-        (rc = dev_alloc(eng->batch_allocs, (void**)&P.R, VK * nb * sizeof(double))) ||
-        (rc = dev_alloc(eng->batch_allocs, (void**)&P.P, VK * nb * sizeof(int32_t))) ||
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.Q, VK * nb * sizeof(Rec))) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.act, (size_t)pvp * 2 * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.srcv, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
