@@ -205,7 +205,7 @@ def host_build_ms(eng, r0, r1, A, steps, timed):
 
 
 def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, on_timed_start=None,
-                on_timed_end=None, on_first_step=None):
+                on_timed_end=None, on_first_step=None, codec=None):
     """One sharded attached-pair matrix build per step: this rank's contiguous
     row block computed by `compute(a, z, lat, rel, hops)` into packed row chunks, each chunk
     all-gathered (shard.RowExchange).  `warmup` untimed steps, then exactly `steps` bracketed
@@ -238,7 +238,7 @@ def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, 
             el = float(tt.item())
         return el
 
-    ex = shard.RowExchange(dist, A, world, rank, device, chunks)
+    ex = shard.RowExchange(dist, A, world, rank, device, chunks, codec=codec)
     for i in range(max(1, warmup)):
         ex.step(compute)
         if i == 0 and on_first_step:
@@ -246,18 +246,26 @@ def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, 
             on_first_step()
     if on_timed_start:
         on_timed_start()
+    sent0 = ex.exchanged_bytes
     elapsed = timed(lambda: ex.step(compute), steps)
     if on_timed_end:
         on_timed_end()
     out = {"exchange": ex, "elapsed_s": elapsed, "timed": timed}
     if world > 1:
-        def gather_only():
-            works = [dist.all_gather_into_tensor(ex.gathered[c], ex.packs[c], async_op=True)
-                     for c in range(len(ex.bounds))]
-            for w in works:
-                w.wait()
+        if ex.codec is not None:
+            # the packed exchange alone: pack, size agreement, payload all-gather, unpack
+            def gather_only():
+                for c, (c0, n) in enumerate(ex.bounds):
+                    ex._exchange_packed(c, c0, n, ex.r0 + c0, min(ex.r1, ex.r0 + c0 + n))
+            out["allgather_bytes"] = (ex.exchanged_bytes - sent0) // max(1, steps) * world
+        else:
+            def gather_only():
+                works = [dist.all_gather_into_tensor(ex.gathered[c], ex.packs[c], async_op=True)
+                         for c in range(len(ex.bounds))]
+                for w in works:
+                    w.wait()
+            out["allgather_bytes"] = sum(p.numel() for p in ex.packs) * world
         out["allgather_s"] = timed(gather_only, steps)
-        out["allgather_bytes"] = sum(p.numel() for p in ex.packs) * world
     return out
 
 
@@ -419,6 +427,8 @@ def main():
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-spec", type=int, default=-1, help="dense: leading rounds with no host read-back (0..4); -1 = engine default")
+    ap.add_argument("--exchange", choices=["packed", "raw"], default="packed",
+                    help="N > 1, dense graphs: exchange rows packed (EngineRowCodec, default) or raw")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--device-rounds", type=int, default=-1, help="CSR worklist rounds driven from the device: 0 never, "
@@ -500,7 +510,13 @@ def main():
     # runs in tests/test_shard_gloo.py with world size 2 on gloo).
     # (measured at N=1: 2 chunks cost +0.9 ms of per-chunk overhead, so overlap pays only
     # where the exchange is long: 8 ranks move ~1.1 GB into every GPU per step)
-    chunks = args.chunks or (2 if world >= 8 else 1)
+    # dense graphs exchange packed rows (shard.EngineRowCodec: a bit per pair every rank
+    # rebuilds from its own graph replica, the rest in full; C2 at 8 ranks ~11 MB per rank
+    # instead of 160 MB), which is small enough that one chunk suffices
+    dense = bool(eng.stats()["dense"])
+    codec = (shard.EngineRowCodec(eng, stream_of=lambda: torch.cuda.current_stream(dev).cuda_stream)
+             if world > 1 and dense and args.exchange == "packed" else None)
+    chunks = args.chunks or (2 if world >= 8 and codec is None else 1)
 
     def compute(a, z, lat, rel, hops):
         stream = torch.cuda.current_stream(dev).cuda_stream
@@ -511,7 +527,7 @@ def main():
     run = run_sharded(dist, world, rank, dev, A, compute, args.steps, args.warmup, chunks,
                       on_timed_start=eng.reset_stats, on_timed_end=lambda: st.update(eng.stats()),
                       # engine creation -> first finished matrix rows on the device
-                      on_first_step=lambda: cold.update(ms=(time.perf_counter() - t_cold) * 1e3))
+                      on_first_step=lambda: cold.update(ms=(time.perf_counter() - t_cold) * 1e3), codec=codec)
     cold_start_ms = cold["ms"]
     elapsed = run["elapsed_s"]
     total_sources = A if world > 1 else rows  # every rank's rows per step
@@ -580,6 +596,22 @@ def main():
         except Exception as e:  # report, never fake
             cpu = {"value": None, "error": str(e)}
 
+    # the row exchange: at N > 1 what the timed steps moved; at N = 1 (dense) a probe packing
+    # this rank's rows once, after the timing, for the packed-to-raw ratio the N-rank runs see
+    exchange = {"mode": "packed" if codec is not None else ("raw" if world > 1 else None)}
+    if world > 1:
+        exchange.update(gathered_bytes_per_step=run["allgather_bytes"],
+                        raw_bytes_per_step=sum(p.numel() for p in run["exchange"].packs) * world,
+                        exchange_ms=run["allgather_s"] / args.steps * 1e3)
+    elif dense and rows > 0 and args.exchange == "packed":
+        ex = run["exchange"]
+        lat_v, rel_v, hops_v = ex.views[0]
+        n0 = min(rows, ex.bounds[0][1])
+        probe = shard.EngineRowCodec(eng, stream_of=lambda: torch.cuda.current_stream(dev).cuda_stream)
+        buf = torch.empty(probe.capacity(n0, A), dtype=torch.uint8, device=dev)
+        nbytes = probe.pack(r0, r0 + n0, lat_v[:n0], rel_v[:n0], hops_v[:n0], buf)
+        exchange.update(probe_rows=n0, probe_raw_bytes=n0 * A * 20, probe_packed_bytes=nbytes,
+                        probe_ratio=n0 * A * 20 / max(1, nbytes))
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -600,7 +632,10 @@ def main():
                        "matrix_build_note": "matrix_build_ms: rows left in HBM (the timed steps above); "
                                             "matrix_build_host_ms: the same builds delivered into page-locked "
                                             "host memory (lat, rel, hops, kind; PCIe included), timed the same way",
-                       "parallelism": f"sources sharded x{world}" + (f" + RCCL all-gather ({chunks} chunks, overlapped)" if world > 1 else "")},
+                       "parallelism": f"sources sharded x{world}" + (
+                           "" if world == 1 else (" + packed-row RCCL all-gather (EngineRowCodec)" if codec is not None
+                                                  else f" + RCCL all-gather ({chunks} chunks, overlapped)"))},
+            "exchange": exchange,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "north_star": north,

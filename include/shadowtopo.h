@@ -199,6 +199,8 @@ typedef struct shadowtopo_stats {
     double fold_ms;
     int64_t push_rounds;
     int64_t fold_rounds;
+    int64_t packed_pairs;    /* row exchange codec: pairs packed, and of them sent explicitly */
+    int64_t packed_explicit;
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */
@@ -273,6 +275,22 @@ int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_so
  * F_SELF_DIJKSTRA_LOOP flag: under that flag the shim needs both values, because the
  * reference caches a self pair from whichever of the two rules runs first. */
 int shadowtopo_self_rule_paths(shadowtopo_engine* eng, double* lat, double* rel, uint8_t* kind);
+
+/* Row exchange codec (multi-GPU, shard.RowExchange; dense engines): the device rows
+   [row_begin, row_end) x A of lat (f64), rel (f64) and hops (u32), row-major, are packed
+   into `out` (device memory, at least shadowtopo_packed_capacity bytes): a bit per pair
+   that equals the value every engine rebuilds from its own graph replica (the single arc
+   from the source: latency 0 + w, one hop, reliability vfac(s) * the arc's factor, compared
+   bit for bit), the other pairs in full. *out_bytes = the payload's size (the call waits
+   for the stream).  shadowtopo_unpack_rows rebuilds the rows, bit-identical, on any engine
+   created from the same graph and attached set.  Not part of the reference's interface:
+   the exchange step SURVEY.md 8(e) adds, with 1/15 of C2's bytes at 8 ranks. */
+size_t shadowtopo_packed_capacity(int32_t rows, int32_t A);
+int shadowtopo_pack_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, const double* lat,
+                         const double* rel, const uint32_t* hops, void* out, size_t cap, size_t* out_bytes,
+                         void* stream);
+int shadowtopo_unpack_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, const void* in, double* lat,
+                           double* rel, uint32_t* hops, void* stream);
 
 int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out);
 void shadowtopo_reset_stats(shadowtopo_engine* eng);

@@ -2839,6 +2839,8 @@ struct shadowtopo_engine {
     hipEvent_t ev_spin = nullptr;  // round_sync
     std::vector<hipEvent_t> ev_dev;  // device-driven rounds: one pair per round of a block
     std::vector<hipEvent_t> ev_spec;  // dense: one pair per round enqueued without a read-back
+    void* d_pk_scratch = nullptr;     // row exchange codec: word counts + block sums
+    size_t pk_scratch_n = 0;
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
     shadowtopo_stats st{};
@@ -4739,6 +4741,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->h_tlog) (void)hipHostFree(eng->h_tlog);
     for (auto e : eng->ev_dev) (void)hipEventDestroy(e);
     for (auto e : eng->ev_spec) (void)hipEventDestroy(e);
+    if (eng->d_pk_scratch) (void)hipFree(eng->d_pk_scratch);
     free_batches(eng);
     for (void* p : eng->graph_allocs) (void)hipFree(p);
     for (void* p : eng->prune_allocs) (void)hipFree(p);
@@ -5043,6 +5046,264 @@ void shadowtopo_host_free(void* p) {
     } else {
         (void)hipHostFree(p);
     }
+}
+
+// ---------------------------------------------------------------- row exchange codec
+// Multi-GPU (shard.RowExchange): every rank needs every rank's rows, and on a
+// dense graph most pairs are a single arc from the source -- a value every rank can rebuild
+// from its own replica of the graph.  A row block is packed as
+//   header {u64 explicit pairs, u64 words} | mask[words] u64 | prefix[words] u32 (8-B padded)
+//   | explicit entries {f64 lat, f64 rel, u32 hops, u32 0} in pair order
+// where bit i of the mask says pair i equals pair_recon (the arc's value, below) bit for
+// bit -- the packer compares, so the rebuilt value is the computed one whatever the rule
+// that produced it -- and prefix[w] counts the explicit pairs before word w.  Pairs are the
+// block's [rows][A] row-major order.  C2 at 8 ranks: 160 MB of rows per rank -> ~11 MB.
+namespace {
+constexpr int PK_WPB = 1024;  // words per scan block
+
+struct PackHdr {
+    unsigned long long n_explicit;
+    unsigned long long n_words;
+};
+
+size_t pk_words(int64_t pairs) { return (size_t)((pairs + 63) / 64); }
+size_t pk_mask_off() { return sizeof(PackHdr); }
+size_t pk_prefix_off(size_t w) { return pk_mask_off() + w * 8; }
+size_t pk_entry_off(size_t w) { return (pk_prefix_off(w) + w * 4 + 15) & ~(size_t)15; }
+
+// the value of pair (s, t) if its path is the single arc s -> t (the dense sweep's seed
+// winner): latency 0 + w, one hop, reliability vfac(s) * that arc's factor (compose's R(t)
+// where the target has no vertex loss); false where there is no arc or s == t
+__device__ __forceinline__ bool pair_recon(const double* __restrict__ W, const double* __restrict__ WR,
+                                           const double* __restrict__ vfac, int32_t Vp, int32_t s, int32_t t,
+                                           double& lat, double& rel) {
+    if (s == t) return false;
+    const double w = W[(size_t)s * Vp + t];
+    if (!(w < dinf())) return false;
+    lat = 0.0 + w;
+    rel = vfac[s] * WR[(size_t)s * Vp + t];
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_pack_mask(const double* __restrict__ W, const double* __restrict__ WR,
+                                                   const double* __restrict__ vfac, int32_t Vp,
+                                                   const int32_t* __restrict__ attached, int32_t row0, int32_t A,
+                                                   int64_t pairs, const double* __restrict__ lat,
+                                                   const double* __restrict__ rel, const uint32_t* __restrict__ hops,
+                                                   unsigned long long* __restrict__ mask, uint32_t* __restrict__ cnt,
+                                                   int64_t nwords) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nwords) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = w * 64 + lane;
+    bool same = false;
+    const bool valid = i < pairs;
+    if (valid) {
+        const int32_t row = (int32_t)(i / A), col = (int32_t)(i % A);
+        double l, r;
+        if (pair_recon(W, WR, vfac, Vp, attached[row0 + row], attached[col], l, r))
+            same = hops[i] == 1u && __double_as_longlong(lat[i]) == __double_as_longlong(l) &&
+                   __double_as_longlong(rel[i]) == __double_as_longlong(r);
+    }
+    const unsigned long long m = __ballot(same);
+    const unsigned long long x = __ballot(valid && !same);
+    if (lane == 0) {
+        mask[w] = m;
+        cnt[w] = (uint32_t)__popcll(x);
+    }
+}
+
+// exclusive prefix of cnt over each block of PK_WPB words (pre), and the block totals
+__global__ __launch_bounds__(256) void k_pack_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ pre,
+                                                   unsigned long long* __restrict__ bsum, int64_t nwords) {
+    __shared__ uint32_t ws[256];
+    const int64_t b0 = (int64_t)blockIdx.x * PK_WPB;
+    uint32_t v[4], t = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int64_t w = b0 + threadIdx.x * 4 + k;
+        v[k] = w < nwords ? cnt[w] : 0u;
+        t += v[k];
+    }
+    ws[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the per-thread totals
+        const uint32_t y = threadIdx.x >= (unsigned)o ? ws[threadIdx.x - o] : 0u;
+        __syncthreads();
+        ws[threadIdx.x] += y;
+        __syncthreads();
+    }
+    uint32_t run = ws[threadIdx.x] - t;
+    for (int k = 0; k < 4; ++k) {
+        const int64_t w = b0 + threadIdx.x * 4 + k;
+        if (w < nwords) pre[w] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 255) bsum[blockIdx.x] = ws[255];
+}
+
+// block totals -> exclusive block offsets (one block, any count), the total into the header
+__global__ __launch_bounds__(256) void k_pack_blocks(unsigned long long* __restrict__ bsum, int64_t nblk,
+                                                     PackHdr* __restrict__ hdr, int64_t nwords) {
+    __shared__ unsigned long long ws[256];
+    unsigned long long carry = 0;
+    for (int64_t c0 = 0; c0 < nblk; c0 += 256) {
+        const int64_t j = c0 + threadIdx.x;
+        const unsigned long long v = j < nblk ? bsum[j] : 0ull;
+        ws[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const unsigned long long y = threadIdx.x >= (unsigned)o ? ws[threadIdx.x - o] : 0ull;
+            __syncthreads();
+            ws[threadIdx.x] += y;
+            __syncthreads();
+        }
+        if (j < nblk) bsum[j] = carry + ws[threadIdx.x] - v;
+        const unsigned long long tot = ws[255];
+        __syncthreads();
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        hdr->n_explicit = carry;
+        hdr->n_words = (unsigned long long)nwords;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pack_scatter(int64_t pairs, const double* __restrict__ lat,
+                                                      const double* __restrict__ rel,
+                                                      const uint32_t* __restrict__ hops,
+                                                      const unsigned long long* __restrict__ mask,
+                                                      uint32_t* __restrict__ pre,
+                                                      const unsigned long long* __restrict__ boff,
+                                                      char* __restrict__ entries, int64_t nwords) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nwords) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = w * 64 + lane;
+    const unsigned long long base = boff[w / PK_WPB] + pre[w];
+    const unsigned long long m = mask[w];
+    const bool expl = i < pairs && !((m >> lane) & 1ull);
+    // lanes past the end are above every valid lane: ~m below a valid lane counts explicit pairs only
+    const unsigned long long below = (lane ? (~0ull >> (64 - lane)) : 0ull);
+    if (expl) {
+        const unsigned long long k = base + (unsigned long long)__popcll(~m & below);
+        char* e = entries + k * 24;
+        *(double*)e = lat[i];
+        *(double*)(e + 8) = rel[i];
+        *(uint32_t*)(e + 16) = hops[i];
+        *(uint32_t*)(e + 20) = 0u;
+    }
+    if (lane == 0) pre[w] = (uint32_t)base;  // the final prefix (wrapped past 2^32 pairs: guarded on the host)
+}
+
+__global__ __launch_bounds__(256) void k_unpack(const double* __restrict__ W, const double* __restrict__ WR,
+                                                const double* __restrict__ vfac, int32_t Vp,
+                                                const int32_t* __restrict__ attached, int32_t row0, int32_t A,
+                                                int64_t pairs, const unsigned long long* __restrict__ mask,
+                                                const uint32_t* __restrict__ pre, const char* __restrict__ entries,
+                                                double* __restrict__ lat, double* __restrict__ rel,
+                                                uint32_t* __restrict__ hops, int64_t nwords) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nwords) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = w * 64 + lane;
+    if (i >= pairs) return;
+    const unsigned long long m = mask[w];
+    if ((m >> lane) & 1ull) {
+        const int32_t row = (int32_t)(i / A), col = (int32_t)(i % A);
+        double l = 0.0, r = 0.0;
+        (void)pair_recon(W, WR, vfac, Vp, attached[row0 + row], attached[col], l, r);
+        lat[i] = l;
+        rel[i] = r;
+        hops[i] = 1u;
+    } else {
+        const unsigned long long below = (lane ? (~0ull >> (64 - lane)) : 0ull);
+        const unsigned long long k = (unsigned long long)pre[w] + (unsigned long long)__popcll(~m & below);
+        const char* e = entries + k * 24;
+        lat[i] = *(const double*)e;
+        rel[i] = *(const double*)(e + 8);
+        hops[i] = *(const uint32_t*)(e + 16);
+    }
+}
+}  // namespace
+
+size_t shadowtopo_packed_capacity(int32_t rows, int32_t A) {
+    if (rows <= 0 || A <= 0) return 256;
+    const int64_t pairs = (int64_t)rows * A;
+    const size_t w = pk_words(pairs);
+    return (pk_entry_off(w) + (size_t)pairs * 24 + 255) & ~(size_t)255;
+}
+
+int shadowtopo_pack_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, const double* lat,
+                         const double* rel, const uint32_t* hops, void* out, size_t cap, size_t* out_bytes,
+                         void* stream) {
+    if (!eng || !out || !out_bytes || row_begin < 0 || row_end > eng->A || row_begin > row_end)
+        return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    if (!eng->dense || !eng->d_W || !eng->d_WR) return fail(SHADOWTOPO_ESTATE, "row packing needs a dense engine");
+    const int32_t A = eng->A;
+    const int64_t pairs = (int64_t)(row_end - row_begin) * A;
+    if (pairs >= ((int64_t)1 << 32)) return fail(SHADOWTOPO_EINVAL, "row block over 2^32 pairs");
+    if (cap < shadowtopo_packed_capacity(row_end - row_begin, A)) return fail(SHADOWTOPO_EINVAL, "payload buffer too small");
+    if (pairs && (!lat || !rel || !hops)) return fail(SHADOWTOPO_EINVAL, "NULL rows");
+    HIP_TRY(hipSetDevice(eng->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
+    const int64_t nw = (int64_t)pk_words(pairs);
+    const int64_t nblk = (nw + PK_WPB - 1) / PK_WPB;
+    char* o = static_cast<char*>(out);
+    PackHdr* hdr = reinterpret_cast<PackHdr*>(o);
+    auto* mask = reinterpret_cast<unsigned long long*>(o + pk_mask_off());
+    auto* pre = reinterpret_cast<uint32_t*>(o + pk_prefix_off(nw));
+    char* entries = o + pk_entry_off(nw);
+    // scratch: the word counts and the block sums
+    const size_t need = (size_t)nw * 4 + (size_t)(nblk + 1) * 8;
+    if (eng->pk_scratch_n < need) {
+        if (eng->d_pk_scratch) (void)hipFree(eng->d_pk_scratch);
+        eng->d_pk_scratch = nullptr;
+        eng->pk_scratch_n = 0;
+        HIP_TRY(hipMalloc(&eng->d_pk_scratch, need));
+        eng->pk_scratch_n = need;
+    }
+    auto* bsum = reinterpret_cast<unsigned long long*>(eng->d_pk_scratch);
+    auto* cnt = reinterpret_cast<uint32_t*>(bsum + nblk + 1);
+    if (nw > 0) {
+        const uint32_t gw = (uint32_t)((nw + 3) / 4);
+        hipLaunchKernelGGL(k_pack_mask, dim3(gw), dim3(256), 0, s, eng->d_W, eng->d_WR, eng->g.vfac, eng->Vp,
+                           eng->d_attached, row_begin, A, pairs, lat, rel, hops, mask, cnt, nw);
+        hipLaunchKernelGGL(k_pack_scan, dim3((uint32_t)nblk), dim3(256), 0, s, cnt, pre, bsum, nw);
+    }
+    hipLaunchKernelGGL(k_pack_blocks, dim3(1), dim3(256), 0, s, bsum, nblk, hdr, nw);
+    if (nw > 0)
+        hipLaunchKernelGGL(k_pack_scatter, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, s, pairs, lat, rel, hops,
+                           mask, pre, bsum, entries, nw);
+    HIP_TRY(hipGetLastError());
+    PackHdr h{};
+    HIP_TRY(hipMemcpyAsync(&h, hdr, sizeof h, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *out_bytes = (pk_entry_off(nw) + (size_t)h.n_explicit * 24 + 255) & ~(size_t)255;
+    eng->st.packed_pairs += pairs;
+    eng->st.packed_explicit += (int64_t)h.n_explicit;
+    return SHADOWTOPO_OK;
+}
+
+int shadowtopo_unpack_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, const void* in, double* lat,
+                           double* rel, uint32_t* hops, void* stream) {
+    if (!eng || !in || row_begin < 0 || row_end > eng->A || row_begin > row_end)
+        return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    if (!eng->dense || !eng->d_W || !eng->d_WR) return fail(SHADOWTOPO_ESTATE, "row unpacking needs a dense engine");
+    const int32_t A = eng->A;
+    const int64_t pairs = (int64_t)(row_end - row_begin) * A;
+    if (pairs == 0) return SHADOWTOPO_OK;
+    if (!lat || !rel || !hops) return fail(SHADOWTOPO_EINVAL, "NULL rows");
+    HIP_TRY(hipSetDevice(eng->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
+    const int64_t nw = (int64_t)pk_words(pairs);
+    const char* o = static_cast<const char*>(in);
+    hipLaunchKernelGGL(k_unpack, dim3((uint32_t)((nw + 3) / 4)), dim3(256), 0, s, eng->d_W, eng->d_WR, eng->g.vfac,
+                       eng->Vp, eng->d_attached, row_begin, A, pairs,
+                       reinterpret_cast<const unsigned long long*>(o + pk_mask_off()),
+                       reinterpret_cast<const uint32_t*>(o + pk_prefix_off(nw)), o + pk_entry_off(nw), lat, rel, hops,
+                       nw);
+    HIP_TRY(hipGetLastError());
+    return SHADOWTOPO_OK;
 }
 
 int shadowtopo_self_rule_paths(shadowtopo_engine* eng, double* lat, double* rel, uint8_t* kind) {

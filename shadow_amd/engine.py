@@ -90,6 +90,7 @@ class Stats(ctypes.Structure):
         ("group_batches", ctypes.c_int64), ("host_syncs", ctypes.c_int64),
         ("push_ms", ctypes.c_double), ("pred_ms", ctypes.c_double), ("fold_ms", ctypes.c_double),
         ("push_rounds", ctypes.c_int64), ("fold_rounds", ctypes.c_int64),
+        ("packed_pairs", ctypes.c_int64), ("packed_explicit", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -124,6 +125,11 @@ def lib():
         L.shadowtopo_sssp.argtypes = [vp, vp, ctypes.c_int32, vp, vp, vp, vp]
         L.shadowtopo_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.shadowtopo_self_rule_paths.argtypes = [vp, vp, vp, vp]
+        L.shadowtopo_packed_capacity.restype = ctypes.c_size_t
+        L.shadowtopo_packed_capacity.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        L.shadowtopo_pack_rows.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t), vp]
+        L.shadowtopo_unpack_rows.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]
         L.shadowtopo_reset_stats.argtypes = [vp]
         L.shadowtopo_is_complete.argtypes = [vp]
         L.shadowtopo_get_eid.restype = ctypes.c_int64
@@ -290,6 +296,25 @@ class Engine:
         _check(lib().shadowtopo_compute_rows(self._h, int(row_begin), int(row_end), vp(lat_ptr), vp(rel_ptr),
                                              vp(hops_ptr), vp(kind_ptr) if kind_ptr else None, MEM_DEVICE,
                                              vp(stream) if stream else None))
+
+    @staticmethod
+    def packed_capacity(rows, A):
+        """bytes a packed row block of `rows` x A pairs may need (shadowtopo_pack_rows)"""
+        return int(lib().shadowtopo_packed_capacity(int(rows), int(A)))
+
+    def pack_rows(self, row_begin, row_end, lat_ptr, rel_ptr, hops_ptr, out_ptr, cap, stream=None):
+        """pack device rows [row_begin, row_end) into the device buffer out_ptr; returns the
+        payload's bytes (waits for the stream)"""
+        vp = ctypes.c_void_p
+        n = ctypes.c_size_t(0)
+        _check(lib().shadowtopo_pack_rows(self._h, int(row_begin), int(row_end), vp(lat_ptr), vp(rel_ptr), vp(hops_ptr),
+                                          vp(out_ptr), int(cap), ctypes.byref(n), vp(stream) if stream else None))
+        return int(n.value)
+
+    def unpack_rows(self, row_begin, row_end, in_ptr, lat_ptr, rel_ptr, hops_ptr, stream=None):
+        vp = ctypes.c_void_p
+        _check(lib().shadowtopo_unpack_rows(self._h, int(row_begin), int(row_end), vp(in_ptr), vp(lat_ptr),
+                                            vp(rel_ptr), vp(hops_ptr), vp(stream) if stream else None))
 
     def sssp(self, sources):
         s = np.ascontiguousarray(sources, np.int32)

@@ -80,6 +80,28 @@ def assemble(dist, compute_block, A, world, rank, device, dtypes):
     return [gather_rows(dist, b, per, world)[:A] for b in bufs]
 
 
+class EngineRowCodec:
+    """The row exchange codec of a dense engine (shadowtopo_pack_rows / unpack_rows): a
+    rank's rows leave as a payload of one bit per pair that every rank rebuilds from its own
+    graph replica (the single arc from the source) plus the other pairs in full; C2 at 8
+    ranks moves ~11 MB per rank instead of 160 MB.  Rows are the packed_views of a chunk."""
+
+    def __init__(self, eng, stream_of=None):
+        self.eng = eng
+        self.stream_of = stream_of or (lambda: None)
+
+    def capacity(self, rows: int, A: int) -> int:
+        return self.eng.packed_capacity(rows, A)
+
+    def pack(self, a, z, lat, rel, hops, out) -> int:
+        return self.eng.pack_rows(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), out.data_ptr(), out.numel(),
+                                  stream=self.stream_of())
+
+    def unpack(self, a, z, payload, lat, rel, hops):
+        self.eng.unpack_rows(a, z, payload.data_ptr(), lat.data_ptr(), rel.data_ptr(), hops.data_ptr(),
+                             stream=self.stream_of())
+
+
 class RowExchange:
     """The multi-GPU step of bench.py: this rank's source rows, computed in
     row chunks of whole 64-source batches into packed [lat | rel | hops] buffers (one
@@ -89,7 +111,7 @@ class RowExchange:
     attached-pair matrix into the [z - a, A] views (the engine on a GPU; tests pass a CPU
     stand-in and the gloo backend)."""
 
-    def __init__(self, dist, A: int, world: int, rank: int, device, chunks: int = 1):
+    def __init__(self, dist, A: int, world: int, rank: int, device, chunks: int = 1, codec=None):
         import torch
         self.dist, self.A, self.world, self.rank = dist, A, world, rank
         self.r0, self.r1, self.per = shard_rows(A, world, rank)
@@ -98,6 +120,16 @@ class RowExchange:
         self.views = [pack_views(b, n, A) for b, (_, n) in zip(self.packs, self.bounds)]
         self.gathered = ([torch.empty(world * p.numel(), dtype=torch.uint8, device=device) for p in self.packs]
                          if world > 1 else None)
+        # with a codec (world > 1): each chunk leaves as a payload; its size is agreed first
+        # (all ranks gather the largest), then the payloads are all-gathered and every rank
+        # unpacks every rank's rows into `gathered`, so full() reads the same buffers
+        self.codec = codec if world > 1 else None
+        self.exchanged_bytes = 0  # payload bytes one rank contributed over the steps (codec)
+        if self.codec is not None:
+            self.payloads = [torch.empty(codec.capacity(n, A), dtype=torch.uint8, device=device) for _, n in self.bounds]
+            self.gpay = [torch.empty(world * p.numel(), dtype=torch.uint8, device=device) for p in self.payloads]
+            self.size_t = torch.zeros(1, dtype=torch.int64, device=device)
+            self.sizes = torch.zeros(world, dtype=torch.int64, device=device)
 
     @property
     def rows(self) -> int:
@@ -110,10 +142,28 @@ class RowExchange:
             if z > a:
                 lat, rel, hops = self.views[c]
                 compute(a, z, lat, rel, hops)
-            if self.world > 1:  # returns once the chunk is computed; the gather runs behind the next chunk
+            if self.codec is not None:
+                self._exchange_packed(c, c0, n, a, z)
+            elif self.world > 1:  # returns once the chunk is computed; the gather runs behind the next chunk
                 works.append(self.dist.all_gather_into_tensor(self.gathered[c], self.packs[c], async_op=True))
         for w in works:
             w.wait()
+
+    def _exchange_packed(self, c, c0, n, a, z):
+        lat, rel, hops = self.views[c]
+        nbytes = self.codec.pack(a, z, lat[:z - a], rel[:z - a], hops[:z - a], self.payloads[c]) if z > a else 0
+        self.size_t.fill_(nbytes)
+        self.dist.all_gather_into_tensor(self.sizes, self.size_t)
+        m = max(256, int(self.sizes.max().item()))  # every rank's slot in the gathered payloads
+        self.exchanged_bytes += m
+        self.dist.all_gather_into_tensor(self.gpay[c][:self.world * m], self.payloads[c][:m])
+        parts = unpack_gathered(self.gathered[c], self.world, n, self.A)
+        for rr in range(self.world):
+            s0, s1, _ = shard_rows(self.A, self.world, rr)
+            ra, rz = s0 + c0, min(s1, s0 + c0 + n)
+            if rz > ra:
+                pl, pr, ph = parts[rr]
+                self.codec.unpack(ra, rz, self.gpay[c][rr * m:(rr + 1) * m], pl[:rz - ra], pr[:rz - ra], ph[:rz - ra])
 
     def full(self):
         """the assembled [A, A] lat, rel, hops (torch, on the buffers' device) after step()"""

@@ -575,3 +575,61 @@ def test_dense_batches_per_wave(case, tb):
         g = synth.integer_grid(rows=11, cols=12, seed=6)
     st = compare(g, layout="dense", dense_batches_per_wave=tb)
     assert st["dense"] == 1 and st["full_sweeps"] >= 1
+
+
+@pytest.mark.parametrize("case", ["geometric", "vloss_prefer", "ties_dense", "odd_block"])
+def test_row_codec_round_trip(case):
+    """the row exchange codec (shadowtopo_pack_rows / unpack_rows): device rows packed by one
+    engine and unpacked by ANOTHER engine built from the same graph (another rank's replica)
+    come back bit for bit, equal to the oracle's; the single-arc pairs of a geometric graph
+    are rebuilt, not sent (payload < 1/4 of the raw rows)"""
+    import torch
+    rng = np.random.default_rng(9)
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=700, A=200)
+    elif case == "vloss_prefer":
+        g = synth.geometric_complete_ish(V=400, A=150)
+        g.vertex_packetloss = np.where(rng.random(400) < 0.3, 0.01, np.nan)
+        g.prefer_direct = True
+    elif case == "ties_dense":
+        g = synth.integer_grid(rows=11, cols=12, seed=6)
+    else:
+        g = synth.geometric_complete_ish(V=333, A=77, drop=0.3)
+    lat_o, rel_o, hops_o, _, _ = oracle_matrix(g)
+    dev = torch.device("cuda:0")
+    engs = [E.Engine.from_synth(g, layout="dense") for _ in range(2)]
+    for e in engs:
+        e.set_attached(g.attached)
+    A = len(g.attached)
+    a, z = (3, A - 5) if case == "odd_block" else (0, A)
+    n = z - a
+    lat = torch.empty((n, A), dtype=torch.float64, device=dev)
+    rel = torch.empty_like(lat)
+    hops = torch.empty((n, A), dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    engs[0].compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), stream=s)
+    cap = E.Engine.packed_capacity(n, A)
+    buf = torch.empty(cap, dtype=torch.uint8, device=dev)
+    nbytes = engs[0].pack_rows(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(), buf.data_ptr(), cap, stream=s)
+    assert 0 < nbytes <= cap
+    out = [torch.full_like(lat, -7.0), torch.full_like(rel, -7.0), torch.full_like(hops, -7)]
+    engs[1].unpack_rows(a, z, buf.data_ptr(), out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), stream=s)
+    torch.cuda.synchronize(dev)
+    assert_bitexact("latency", out[0].cpu().numpy(), lat_o[a:z])
+    assert_bitexact("reliability", out[1].cpu().numpy(), rel_o[a:z])
+    assert_bitexact("hops", out[2].cpu().numpy().astype(np.uint32), hops_o[a:z])
+    st = engs[0].stats()
+    assert st["packed_pairs"] == n * A
+    if case == "geometric":
+        assert nbytes * 4 < n * A * 20, (nbytes, n * A * 20)
+    for e in engs:
+        e.close()
+
+
+def test_row_codec_needs_a_dense_engine():
+    g = synth.random_sparse(V=200, avg_deg=4, seed=3, A=50)
+    eng = E.Engine.from_synth(g, layout="csr")
+    eng.set_attached(g.attached)
+    with pytest.raises(E.ShadowTopoError):
+        eng.pack_rows(0, 1, 0, 0, 0, 0, E.Engine.packed_capacity(1, 50))
+    eng.close()

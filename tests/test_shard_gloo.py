@@ -196,7 +196,7 @@ def test_two_rank_row_exchange_step(A_sel, chunks):
     assert res == [(0, True), (1, True)]
 
 
-def _worker_bench_sharded(rank, world, port, A_sel, chunks, q):
+def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False):
     """bench.py's run_sharded -- the timed step of both the headline line and the north-star
     C4 record at every GPU count (barriers, max-over-ranks timing, all-gather-only leg) --
     with the oracle as the compute stand-in on gloo"""
@@ -223,9 +223,14 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q):
         rel[:z - a] = torch.from_numpy(r)
         hops[:z - a] = torch.from_numpy(h.astype(np.int32))
 
+    codec = None
+    if packed:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from rowcodec_ref import RefRowCodec
+        codec = RefRowCodec(g)
     run = bench.run_sharded(dist, world, rank, torch.device("cpu"), A, compute, steps=3, warmup=2, chunks=chunks,
                             on_timed_start=lambda: hooks.append("start"), on_timed_end=lambda: hooks.append("end"),
-                            on_first_step=lambda: hooks.append("first"))
+                            on_first_step=lambda: hooks.append("first"), codec=codec)
     lat, rel, hops = run["exchange"].full()
     full = og.pair_rows(flags, g.attached)
     ok = np.array_equal(lat.numpy().view(np.uint64), full[0].view(np.uint64))
@@ -233,7 +238,10 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q):
     ok &= np.array_equal(hops.numpy(), full[2].astype(np.int32))
     ok &= hooks == ["first", "start", "end"]
     ok &= run["elapsed_s"] > 0 and run["allgather_s"] > 0
-    ok &= run["allgather_bytes"] == sum(p.numel() for p in run["exchange"].packs) * world
+    if packed:
+        ok &= 0 < run["allgather_bytes"] <= sum(p.numel() for p in run["exchange"].packs) * world * 2
+    else:
+        ok &= run["allgather_bytes"] == sum(p.numel() for p in run["exchange"].packs) * world
     # the reported time is the max over ranks: every rank holds the same number
     t = torch.tensor([run["elapsed_s"]], dtype=torch.float64)
     tl = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
@@ -244,12 +252,12 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("A_sel,chunks", [(170, 1), (149, 2)])
-def test_two_rank_bench_run_sharded(A_sel, chunks):
+@pytest.mark.parametrize("A_sel,chunks,packed", [(170, 1, False), (149, 2, False), (150, 1, True)])
+def test_two_rank_bench_run_sharded(A_sel, chunks, packed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_bench_sharded, args=(r, 2, port, A_sel, chunks, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_bench_sharded, args=(r, 2, port, A_sel, chunks, q, packed)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -257,3 +265,61 @@ def test_two_rank_bench_run_sharded(A_sel, chunks):
         assert p.exitcode == 0
     res = sorted(q.get(timeout=10) for _ in range(2))
     assert res == [(0, True), (1, True)]
+
+
+def _worker_exchange_packed(rank, world, port, A_sel, chunks, q):
+    """RowExchange with a row codec (the engine's payload format, CPU reference codec):
+    sizes agreed, payloads all-gathered, every rank's rows unpacked -- the same matrices as
+    the oracle's, with fewer bytes than the raw rows"""
+    import sys
+
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from shadow_amd import synth
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from rowcodec_ref import RefRowCodec
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = synth.geometric_complete_ish(V=220, A=A_sel, drop=0.1)
+    og = O.OracleGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss)
+    flags = og.flags()
+    A = len(g.attached)
+    ex = shard.RowExchange(dist, A, world, rank, "cpu", chunks, codec=RefRowCodec(g))
+
+    def compute(a, z, lat, rel, hops):
+        l, r, h, _, _ = og.pair_rows(flags, g.attached, a, z)
+        lat[:z - a] = torch.from_numpy(l)
+        rel[:z - a] = torch.from_numpy(r)
+        hops[:z - a] = torch.from_numpy(h.astype(np.int32))
+
+    full = og.pair_rows(flags, g.attached)
+    ok = True
+    for _ in range(2):
+        ex.step(compute)
+        lat, rel, hops = ex.full()
+        ok &= np.array_equal(lat.numpy().view(np.uint64), full[0].view(np.uint64))
+        ok &= np.array_equal(rel.numpy().view(np.uint64), full[1].view(np.uint64))
+        ok &= np.array_equal(hops.numpy(), full[2].astype(np.int32))
+    raw = 2 * sum(p.numel() for p in ex.packs)
+    q.put((rank, bool(ok), ex.exchanged_bytes, raw))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("A_sel,chunks", [(120, 1), (131, 2), (65, 1)])
+def test_two_rank_packed_row_exchange(A_sel, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_exchange_packed, args=(r, 2, port, A_sel, chunks, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert [(r, ok) for r, ok, _, _ in res] == [(0, True), (1, True)]
+    for _, _, sent, raw in res:
+        assert sent * 4 < raw, (sent, raw)  # most pairs are the single arc: rebuilt, not sent
