@@ -564,6 +564,22 @@ def main():
         host_pageable_ms = (time.perf_counter() - h0) * 1e3
         del outs
 
+    # the row exchange: at N > 1 what the timed steps moved; at N = 1 (dense) a probe packing
+    # this rank's rows once, after the timing, for the packed-to-raw ratio the N-rank runs see
+    exchange = {"mode": "packed" if codec is not None else ("raw" if world > 1 else None)}
+    if world > 1:
+        exchange.update(gathered_bytes_per_step=run["allgather_bytes"],
+                        raw_bytes_per_step=sum(p.numel() for p in run["exchange"].packs) * world,
+                        exchange_ms=run["allgather_s"] / args.steps * 1e3)
+    elif dense and rows > 0 and args.exchange == "packed":
+        ex = run["exchange"]
+        lat_v, rel_v, hops_v = ex.views[0]
+        n0 = min(rows, ex.bounds[0][1])
+        probe = shard.EngineRowCodec(eng, stream_of=lambda: torch.cuda.current_stream(dev).cuda_stream)
+        buf = torch.empty(probe.capacity(n0, A), dtype=torch.uint8, device=dev)
+        nbytes = probe.pack(r0, r0 + n0, lat_v[:n0], rel_v[:n0], hops_v[:n0], buf)
+        exchange.update(probe_rows=n0, probe_raw_bytes=n0 * A * 20, probe_packed_bytes=nbytes,
+                        probe_ratio=n0 * A * 20 / max(1, nbytes))
     # the north-star record (C4 sharded over every rank + all-gather) at every GPU count: all
     # ranks take part (barriers, all-gather), rank 0 reports
     north = None
@@ -596,22 +612,6 @@ def main():
         except Exception as e:  # report, never fake
             cpu = {"value": None, "error": str(e)}
 
-    # the row exchange: at N > 1 what the timed steps moved; at N = 1 (dense) a probe packing
-    # this rank's rows once, after the timing, for the packed-to-raw ratio the N-rank runs see
-    exchange = {"mode": "packed" if codec is not None else ("raw" if world > 1 else None)}
-    if world > 1:
-        exchange.update(gathered_bytes_per_step=run["allgather_bytes"],
-                        raw_bytes_per_step=sum(p.numel() for p in run["exchange"].packs) * world,
-                        exchange_ms=run["allgather_s"] / args.steps * 1e3)
-    elif dense and rows > 0 and args.exchange == "packed":
-        ex = run["exchange"]
-        lat_v, rel_v, hops_v = ex.views[0]
-        n0 = min(rows, ex.bounds[0][1])
-        probe = shard.EngineRowCodec(eng, stream_of=lambda: torch.cuda.current_stream(dev).cuda_stream)
-        buf = torch.empty(probe.capacity(n0, A), dtype=torch.uint8, device=dev)
-        nbytes = probe.pack(r0, r0 + n0, lat_v[:n0], rel_v[:n0], hops_v[:n0], buf)
-        exchange.update(probe_rows=n0, probe_raw_bytes=n0 * A * 20, probe_packed_bytes=nbytes,
-                        probe_ratio=n0 * A * 20 / max(1, nbytes))
     if rank == 0:
         out = {
             "metric": METRIC,
