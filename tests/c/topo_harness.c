@@ -49,17 +49,23 @@ static void* worker(void* arg) {
         }
         return NULL;
     }
+    /* the tallies stay in locals: the workers' structs share cache lines, and a store to
+       them per query made the threads' lookups pay for false sharing */
+    double sum = 0.0;
+    long routable = 0;
     double t0 = now();
     for (long q = 0; q < w->queries; q++) {
         Address* a = w->hosts[rand_r(&s) % w->nh];
         Address* b = w->hosts[rand_r(&s) % w->nh];
         /* the per-packet sequence of worker.c:267-279 */
         if (topology_isRoutable(w->top, a, b)) {
-            w->routable++;
-            w->sum += topology_getLatency(w->top, a, b) + topology_getReliability(w->top, a, b);
+            routable++;
+            sum += topology_getLatency(w->top, a, b) + topology_getReliability(w->top, a, b);
             topology_incrementPathPacketCounter(w->top, a, b);
         }
     }
+    w->sum = sum;
+    w->routable = routable;
     w->secs = now() - t0;
     return NULL;
 }
