@@ -1,0 +1,55 @@
+"""Seeded random parity sweep: graphs and engine options drawn together from one generator,
+each engine matrix compared with the oracle bit for bit (latency, reliability, hops, kind).
+The named tests pin one feature at a time; this sweep crosses them (directed x multigraph
+x integer ties x vertex loss x prefer-direct x layout x worklist / device rounds / batch
+groups / read-back-free dense rounds / push rounds / pendant pruning), so a combination no
+named test covers still meets the oracle.  Fixed seeds: a failure names its case."""
+import numpy as np
+import pytest
+
+from paritylib import compare
+from shadow_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    V = int(rng.integers(30, 420))
+    directed = bool(rng.random() < 0.3)
+    int_lat = bool(rng.random() < 0.35)
+    vloss = np.where(rng.random(V) < 0.3, rng.uniform(0, 0.08, V), np.nan) if rng.random() < 0.35 else None
+    g = synth.random_sparse(V=V, avg_deg=float(rng.uniform(1.6, 9.0)), seed=int(rng.integers(1 << 30)),
+                            A=int(rng.integers(1, V + 1)), directed=directed, loops=bool(rng.random() < 0.7),
+                            vloss=vloss, int_lat=int_lat)
+    if rng.random() < 0.25:  # parallel edges
+        k = int(min(len(g.src) // 4, 30))
+        pick = rng.choice(np.nonzero(g.src != g.dst)[0], k, replace=False)
+        g.src = np.concatenate([g.src, g.dst[pick] if not directed else g.src[pick]])
+        g.dst = np.concatenate([g.dst, g.src[pick] if not directed else g.dst[pick]])
+        lat = g.latency[pick] * rng.uniform(0.5, 1.5, k)
+        g.latency = np.concatenate([g.latency, np.round(lat) + 1 if int_lat else lat])
+        g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, k)])
+    g.prefer_direct = bool(rng.random() < 0.2)
+    layout = str(rng.choice(["auto", "csr", "dense"]))
+    opts = {}
+    if layout != "dense":
+        opts["worklist"] = int(rng.integers(0, 3))
+        opts["device_rounds"] = int(rng.choice([0, 2]))
+        opts["prune_pendant"] = int(rng.integers(0, 2))
+        if not directed and rng.random() < 0.2:
+            opts["csr_variant"] = 2  # push rounds
+    if layout != "csr":
+        opts["dense_spec"] = int(rng.choice([0, 2, 4]))
+        opts["dense_prune"] = int(rng.integers(0, 2))
+    if rng.random() < 0.4:
+        opts["batches_in_flight"] = int(rng.integers(1, 3))
+    return g, layout, opts
+
+
+@pytest.mark.parametrize("seed", range(96))
+def test_random_graph_and_options_vs_oracle(seed):
+    g, layout, opts = _case(seed)
+    if layout == "csr" and opts.get("worklist") == 0:
+        opts.pop("device_rounds", None)  # device-driven rounds run on worklists only
+    compare(g, layout=layout, **opts)
