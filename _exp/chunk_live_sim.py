@@ -28,7 +28,7 @@ perm = np.argsort(morton(q[:, 0], q[:, 1]), kind='stable')
 rng = np.random.default_rng(5)
 SRS, BW = 32, 32
 nch = V // SRS
-res = {"all": [], "arc_only": []}
+res = {"all": [], "arc_only": [], "sub2": [], "sub4": [], "sub8": [], "exact": []}
 for trial in range(6):
     c = pts[rng.integers(V)]
     S = np.argsort(((pts - c) ** 2).sum(1))[:64]            # a locality batch
@@ -48,5 +48,22 @@ for trial in range(6):
                 ok = (md[:, None] + mw[None, :] <= T) & mask
                 live += bool(ok.any())
             res[name].append(live / nch)
+        live = 0
+        for ch in range(nch):
+            rows = perm[ch * SRS:(ch + 1) * SRS]
+            c = D0[:, rows][:, :, None] + W[np.ix_(rows, tv)][None, :, :]   # [64, 32 rows, 32 dests]
+            live += bool((c <= T[:, None, :]).any())
+        res["exact"].append(live / nch)
+        for ns in (2, 4, 8):
+            live = 0
+            for ch in range(nch):
+                rows = perm[ch * SRS:(ch + 1) * SRS]
+                ok = np.zeros_like(arc)
+                for sg in np.split(rows, ns):
+                    md = np.min(D0[:, sg], axis=1)
+                    mw = np.min(W[np.ix_(sg, tv)], axis=0)
+                    ok |= md[:, None] + mw[None, :] <= T
+                live += bool(ok.any())
+            res[f"sub{ns}"].append(live / nch)
 for k, v in res.items():
     print(k, 'live chunk fraction mean %.3f (min %.3f, max %.3f)' % (np.mean(v), np.min(v), np.max(v)))
