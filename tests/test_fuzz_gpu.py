@@ -53,3 +53,30 @@ def test_random_graph_and_options_vs_oracle(seed):
     if layout == "csr" and opts.get("worklist") == 0:
         opts.pop("device_rounds", None)  # device-driven rounds run on worklists only
     compare(g, layout=layout, **opts)
+
+
+def _big_case(seed):
+    """larger graphs: several 64-source batches and batch groups, dense and sparse"""
+    rng = np.random.default_rng(5000 + seed)
+    kind = str(rng.choice(["sparse", "geometric", "knn", "ties"]))
+    if kind == "sparse":
+        V = int(rng.integers(800, 2500))
+        g = synth.random_sparse(V=V, avg_deg=float(rng.uniform(2.0, 6.0)), seed=int(rng.integers(1 << 30)),
+                                A=int(rng.integers(65, 800)), directed=bool(rng.random() < 0.3))
+    elif kind == "geometric":
+        g = synth.geometric_complete_ish(V=int(rng.integers(300, 1200)), A=int(rng.integers(65, 300)),
+                                         drop=float(rng.uniform(0.02, 0.3)), seeds=tuple(int(x) for x in rng.integers(1, 1 << 20, 3)))
+    elif kind == "knn":
+        g = synth.knn_geographic(V=int(rng.integers(500, 2000)), k=int(rng.integers(4, 12)), seed=int(rng.integers(1 << 20)))
+        if rng.random() < 0.5:
+            g.attached = np.sort(rng.choice(g.n, size=min(g.n, int(rng.integers(65, 600))), replace=False)).astype(np.int32)
+    else:
+        g = synth.integer_grid(rows=int(rng.integers(10, 30)), cols=int(rng.integers(10, 30)), seed=int(rng.integers(1 << 20)))
+    opts = {"batches_in_flight": int(rng.integers(1, 4))} if rng.random() < 0.5 else {}
+    return g, opts
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_larger_graphs_vs_oracle(seed):
+    g, opts = _big_case(seed)
+    compare(g, **opts)
