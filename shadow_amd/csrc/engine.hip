@@ -2829,6 +2829,9 @@ struct shadowtopo_engine {
     int32_t opt_sweep_spiral = 1;      // pruned sweep: chunks outward from the tile on both sides (1) or upward, wrapping (0)
     int32_t opt_sweep_win1 = 8;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
+    int32_t opt_sweep_halves = 0;      // experiments: the split sweep's two kernels per half of the batches, on two streams
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_h0 = nullptr, ev_h1 = nullptr;
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
@@ -3095,6 +3098,54 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                        eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev, cnt_cur, eng->d_prof,
                                        eng->d_hitlog, eng->d_perm, eng->d_minW, eng->d_minD, eng->d_pos, eng->d_WIp,
                                        eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1);
+            }
+            if constexpr (TB == 1) {
+                if (!w16 && eng->opt_sweep_halves && nbg >= 2 && !eng->d_prof) {
+                    // the two halves of the batches on two streams: one half's exact pass can
+                    // run beside the other half's chunk-loop tail (results are per batch)
+                    if (!eng->aux_stream) {
+                        hipError_t e = hipStreamCreateWithFlags(&eng->aux_stream, hipStreamNonBlocking);
+                        if (e == hipSuccess) e = hipEventCreateWithFlags(&eng->ev_h0, hipEventDisableTiming);
+                        if (e == hipSuccess) e = hipEventCreateWithFlags(&eng->ev_h1, hipEventDisableTiming);
+                        if (e != hipSuccess) return e;
+                    }
+                    const int32_t h = nbg / 2;
+                    hipError_t e = hipEventRecord(eng->ev_h0, s);
+                    if (e == hipSuccess) e = hipStreamWaitEvent(eng->aux_stream, eng->ev_h0, 0);
+                    if (e != hipSuccess) return e;
+                    auto half = [&](hipStream_t st, int32_t b0, int32_t n) {
+                        Pools P = eng->pools;
+                        const size_t o = (size_t)b0 * (size_t)P.vk;
+                        P.D += o;
+                        P.Q += o;
+                        P.act += (size_t)b0 * 2 * P.Vp;
+                        P.srcv += (size_t)b0 * KL;
+                        P.row += (size_t)b0 * KL;
+                        P.mask += b0;
+                        if (P.BDU) P.BDU += o;
+                        if (P.chm) P.chm += (size_t)b0 * 2 * P.Vp;
+                        if (P.D32) P.D32 += o;
+                        uint32_t* hl = eng->d_hitlog + (size_t)b0 * (size_t)(eng->Vp / TDT) * nchunks;
+                        const float* mD = eng->d_minD + (size_t)b0 * nchunks * KL;
+                        const int64_t nbl = 8 * (((int64_t)n * ntb + 7) / 8);
+                        hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1>), dim3((uint32_t)nbl), dim3(256), 0, st,
+                                           eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
+                                           par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
+                                           eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
+                                           eng->opt_sweep_spiral, eng->opt_sweep_win1);
+                        hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 2>), dim3((uint32_t)nbl), dim3(256), 0, st,
+                                           eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
+                                           par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
+                                           eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
+                                           eng->opt_sweep_spiral, eng->opt_sweep_win1);
+                    };
+                    half(s, 0, h);
+                    half(eng->aux_stream, h, nbg - h);
+                    e = hipEventRecord(eng->ev_h1, eng->aux_stream);
+                    if (e == hipSuccess) e = hipStreamWaitEvent(s, eng->ev_h1, 0);
+                    if (e != hipSuccess) return e;
+                    return hipGetLastError();
+                }
             }
             if (!w16)
             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true, 1>), dim3((uint32_t)nblocks), dim3(256), 0, s,
@@ -4717,6 +4768,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (w1 && atoi(w1) >= 0 && atoi(w1) < 64) eng->opt_sweep_win1 = atoi(w1);
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
+        const char* sh = getenv("SHADOWTOPO_SWEEP_HALVES");  // A/B knob: 0 (default) or 1
+        if (sh && (sh[0] == '0' || sh[0] == '1')) eng->opt_sweep_halves = sh[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
 #endif
@@ -4776,6 +4829,9 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
         if (eng->ev_copy[k]) (void)hipEventDestroy(eng->ev_copy[k]);
     }
     if (eng->copy_stream) (void)hipStreamDestroy(eng->copy_stream);
+    if (eng->aux_stream) (void)hipStreamDestroy(eng->aux_stream);
+    if (eng->ev_h0) (void)hipEventDestroy(eng->ev_h0);
+    if (eng->ev_h1) (void)hipEventDestroy(eng->ev_h1);
     if (eng->own_stream) (void)hipStreamDestroy(eng->own_stream);
     delete eng;
 }
