@@ -427,6 +427,7 @@ def main():
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-spec", type=int, default=-1, help="dense: leading rounds with no host read-back (0..4); -1 = engine default")
+    ap.add_argument("--sweep-parts", type=int, default=0, help="pruned dense sweep: batches in 1, 2 or 4 parts on their own streams (0 = engine default)")
     ap.add_argument("--exchange", choices=["packed", "raw"], default="packed",
                     help="N > 1, dense graphs: exchange rows packed (EngineRowCodec, default) or raw")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
@@ -493,6 +494,8 @@ def main():
         eng.set_option(E.OPT_DENSE_W16, args.dense_w16)
     if args.dense_spec >= 0:
         eng.set_option(E.OPT_DENSE_SPEC, args.dense_spec)
+    if args.sweep_parts:
+        eng.set_option(E.OPT_SWEEP_PARTS, args.sweep_parts)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
     if args.device_rounds >= 0:

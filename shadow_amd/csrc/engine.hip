@@ -2829,9 +2829,9 @@ struct shadowtopo_engine {
     int32_t opt_sweep_spiral = 1;      // pruned sweep: chunks outward from the tile on both sides (1) or upward, wrapping (0)
     int32_t opt_sweep_win1 = 8;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
-    int32_t opt_sweep_halves = 0;      // experiments: the split sweep's two kernels per half of the batches, on two streams
-    hipStream_t aux_stream = nullptr;
-    hipEvent_t ev_h0 = nullptr, ev_h1 = nullptr;
+    int32_t opt_sweep_parts = 2;       // the split sweep's two kernels per part of the batches, one stream per part
+    hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_h0 = nullptr, ev_hp[3] = {nullptr, nullptr, nullptr};
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
@@ -3100,20 +3100,21 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                        eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1);
             }
             if constexpr (TB == 1) {
-                if (!w16 && eng->opt_sweep_halves && nbg >= 2 && !eng->d_prof) {
-                    // the two halves of the batches on two streams: one half's exact pass can
-                    // run beside the other half's chunk-loop tail (results are per batch)
-                    if (!eng->aux_stream) {
-                        hipError_t e = hipStreamCreateWithFlags(&eng->aux_stream, hipStreamNonBlocking);
-                        if (e == hipSuccess) e = hipEventCreateWithFlags(&eng->ev_h0, hipEventDisableTiming);
-                        if (e == hipSuccess) e = hipEventCreateWithFlags(&eng->ev_h1, hipEventDisableTiming);
-                        if (e != hipSuccess) return e;
+                const int32_t parts = std::min(eng->opt_sweep_parts, nbg);
+                if (!w16 && parts >= 2 && !eng->d_prof) {
+                    // the batches in `parts` contiguous parts, one stream each: a part's exact
+                    // pass runs beside another part's chunk-loop tail (results are per batch;
+                    // C2, two parts: sweep 2.92 -> 2.70 ms, r04zm)
+                    hipError_t e = hipSuccess;
+                    if (!eng->ev_h0) e = hipEventCreateWithFlags(&eng->ev_h0, hipEventDisableTiming);
+                    for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) {
+                        if (!eng->aux_stream[k]) e = hipStreamCreateWithFlags(&eng->aux_stream[k], hipStreamNonBlocking);
+                        if (e == hipSuccess && !eng->ev_hp[k]) e = hipEventCreateWithFlags(&eng->ev_hp[k], hipEventDisableTiming);
                     }
-                    const int32_t h = nbg / 2;
-                    hipError_t e = hipEventRecord(eng->ev_h0, s);
-                    if (e == hipSuccess) e = hipStreamWaitEvent(eng->aux_stream, eng->ev_h0, 0);
+                    if (e == hipSuccess) e = hipEventRecord(eng->ev_h0, s);
+                    for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) e = hipStreamWaitEvent(eng->aux_stream[k], eng->ev_h0, 0);
                     if (e != hipSuccess) return e;
-                    auto half = [&](hipStream_t st, int32_t b0, int32_t n) {
+                    auto part = [&](hipStream_t st, int32_t b0, int32_t n) {
                         Pools P = eng->pools;
                         const size_t o = (size_t)b0 * (size_t)P.vk;
                         P.D += o;
@@ -3139,10 +3140,14 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
                                            eng->opt_sweep_spiral, eng->opt_sweep_win1);
                     };
-                    half(s, 0, h);
-                    half(eng->aux_stream, h, nbg - h);
-                    e = hipEventRecord(eng->ev_h1, eng->aux_stream);
-                    if (e == hipSuccess) e = hipStreamWaitEvent(s, eng->ev_h1, 0);
+                    for (int k = 0; k < parts; ++k) {
+                        const int32_t b0 = (int32_t)((int64_t)nbg * k / parts), b1 = (int32_t)((int64_t)nbg * (k + 1) / parts);
+                        part(k == 0 ? s : eng->aux_stream[k - 1], b0, b1 - b0);
+                    }
+                    for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) {
+                        e = hipEventRecord(eng->ev_hp[k], eng->aux_stream[k]);
+                        if (e == hipSuccess) e = hipStreamWaitEvent(s, eng->ev_hp[k], 0);
+                    }
                     if (e != hipSuccess) return e;
                     return hipGetLastError();
                 }
@@ -4768,8 +4773,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (w1 && atoi(w1) >= 0 && atoi(w1) < 64) eng->opt_sweep_win1 = atoi(w1);
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
-        const char* sh = getenv("SHADOWTOPO_SWEEP_HALVES");  // A/B knob: 0 (default) or 1
-        if (sh && (sh[0] == '0' || sh[0] == '1')) eng->opt_sweep_halves = sh[0] - '0';
+        const char* sh = getenv("SHADOWTOPO_SWEEP_PARTS");  // A/B knob: 1, 2 (default) or 4
+        if (sh && (sh[0] == '1' || sh[0] == '2' || sh[0] == '4')) eng->opt_sweep_parts = sh[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
 #endif
@@ -4829,9 +4834,11 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
         if (eng->ev_copy[k]) (void)hipEventDestroy(eng->ev_copy[k]);
     }
     if (eng->copy_stream) (void)hipStreamDestroy(eng->copy_stream);
-    if (eng->aux_stream) (void)hipStreamDestroy(eng->aux_stream);
+    for (int k = 0; k < 3; ++k) {
+        if (eng->aux_stream[k]) (void)hipStreamDestroy(eng->aux_stream[k]);
+        if (eng->ev_hp[k]) (void)hipEventDestroy(eng->ev_hp[k]);
+    }
     if (eng->ev_h0) (void)hipEventDestroy(eng->ev_h0);
-    if (eng->ev_h1) (void)hipEventDestroy(eng->ev_h1);
     if (eng->own_stream) (void)hipStreamDestroy(eng->own_stream);
     delete eng;
 }
@@ -4944,6 +4951,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_W16:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense W16 must be 0 or 1");
             eng->opt_dense_w16 = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SWEEP_PARTS:
+            if (value != 1 && value != 2 && value != 4) return fail(SHADOWTOPO_EINVAL, "sweep parts must be 1, 2 or 4");
+            eng->opt_sweep_parts = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DENSE_SPEC:
             if (value < 0 || value > SPEC_MAX) return fail(SHADOWTOPO_EINVAL, "dense spec rounds must be in [0, 4]");

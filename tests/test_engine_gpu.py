@@ -633,3 +633,23 @@ def test_row_codec_needs_a_dense_engine():
     with pytest.raises(E.ShadowTopoError):
         eng.pack_rows(0, 1, 0, 0, 0, 0, E.Engine.packed_capacity(1, 50))
     eng.close()
+
+
+@pytest.mark.parametrize("parts", [1, 2, 4])
+@pytest.mark.parametrize("case", ["geometric", "geometric_odd", "ties", "vloss_prefer"])
+def test_dense_sweep_parts(case, parts):
+    """OPT_SWEEP_PARTS: the pruned sweep's batches in 1 / 2 / 4 parts, each on its own stream
+    (chunk loop and exact pass per part, the parts overlapping): the oracle's matrices bit for
+    bit, with fewer batches than parts too"""
+    rng = np.random.default_rng(3)
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=900, A=330)       # 6 batches
+    elif case == "geometric_odd":
+        g = synth.geometric_complete_ish(V=611, A=100)       # 2 batches: 4 parts clamp to 2
+    elif case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=6)
+    else:
+        g = synth.geometric_complete_ish(V=500, A=200)
+        g.vertex_packetloss = np.where(rng.random(500) < 0.3, 0.01, np.nan)
+        g.prefer_direct = True
+    compare(g, layout="dense", sweep_parts=parts)
