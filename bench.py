@@ -428,6 +428,7 @@ def main():
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-spec", type=int, default=-1, help="dense: leading rounds with no host read-back (0..4); -1 = engine default")
     ap.add_argument("--sweep-parts", type=int, default=0, help="pruned dense sweep: batches in 1, 2 or 4 parts on their own streams (0 = engine default)")
+    ap.add_argument("--chain-parts", type=int, default=-1, help="read-back-free delta rounds on each sweep part's stream (1) or after the join (0); -1 = engine default")
     ap.add_argument("--exchange", choices=["packed", "raw"], default="packed",
                     help="N > 1, dense graphs: exchange rows packed (EngineRowCodec, default) or raw")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
@@ -496,6 +497,8 @@ def main():
         eng.set_option(E.OPT_DENSE_SPEC, args.dense_spec)
     if args.sweep_parts:
         eng.set_option(E.OPT_SWEEP_PARTS, args.sweep_parts)
+    if args.chain_parts >= 0:
+        eng.set_option(E.OPT_CHAIN_PARTS, args.chain_parts)
     eng.set_option(E.OPT_SOURCE_ORDER, args.source_order)
     eng.set_option(E.OPT_WORKLIST, args.worklist)
     if args.device_rounds >= 0:

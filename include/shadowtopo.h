@@ -125,6 +125,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_SWEEP_PARTS 22     /* pruned dense sweep: the batches in 1, 2 (default) or 4 parts, each part's chunk
                                             loop and exact pass on a stream of its own, so one part's exact pass overlaps
                                             another's chunk-loop tail. Results are identical. */
+#define SHADOWTOPO_OPT_CHAIN_PARTS 23     /* with a sweep in parts and read-back-free rounds (OPT_DENSE_SPEC > 0): 1
+                                            (default) enqueues those delta rounds on each part's stream behind its share of the
+                                            sweep, the parts joining once before the read-back; 0 joins after the sweep.
+                                            Results are identical. */
 #define SHADOWTOPO_OPT_DENSE_SPEC 21      /* dense rounds: how many leading rounds (0..4, default 2) are enqueued with no
                                             host read-back of their change counts; a round decided without them runs
                                             the delta kernel over every batch that changed. Results are identical. */

@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <mutex>
 #include <string>
@@ -2832,6 +2833,8 @@ struct shadowtopo_engine {
     int32_t opt_sweep_parts = 2;       // the split sweep's two kernels per part of the batches, one stream per part
     hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_h0 = nullptr, ev_hp[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_sw[4] = {nullptr, nullptr, nullptr, nullptr};  // timing: each part's sweep end (chained rounds)
+    int32_t opt_chain_parts = 1;       // the read-back-free delta rounds per sweep part, on the part's stream
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
@@ -3051,10 +3054,38 @@ int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
     return SHADOWTOPO_OK;
 }
 
+// the pools of batches b0, b0 + 1, ... as a pool set of their own (one part of the batches)
+Pools pools_from(const Pools& in, int32_t b0) {
+    Pools P = in;
+    const size_t o = (size_t)b0 * (size_t)P.vk;
+    P.D += o;
+    P.Q += o;
+    P.act += (size_t)b0 * 2 * P.Vp;
+    P.srcv += (size_t)b0 * KL;
+    P.row += (size_t)b0 * KL;
+    P.mask += b0;
+    if (P.BDU) P.BDU += o;
+    if (P.chm) P.chm += (size_t)b0 * 2 * P.Vp;
+    if (P.D32) P.D32 += o;
+    return P;
+}
+
+// the number of parts (one stream each) the f32 sweep of nbg batches runs in; 1: one launch
+int32_t sweep_parts(const shadowtopo_engine* eng, int32_t nbg) {
+    if (eng->opt_dense_variant == SHADOWTOPO_DENSE_F64 || eng->opt_dense_tb != 1 || !eng->vperm_ready ||
+        !eng->opt_dense_prune || !eng->opt_sweep_split || eng->opt_dense_w16 || eng->opt_profile)
+        return 1;
+    return std::max<int32_t>(1, std::min(eng->opt_sweep_parts, nbg));
+}
+
+// work a part's stream takes on after its share of the sweep, before the join (run_rounds'
+// chained delta rounds): (stream, first batch, batches, part)
+using PartTail = std::function<hipError_t(hipStream_t, int32_t, int32_t, int)>;
+
 // the f32-filtered full sweep: 8 destinations per wave, exact rows settled 2 at a time
 template <int TB>
 hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
-                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
+                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail) {
     constexpr int TDT = FTDT, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
@@ -3100,7 +3131,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                        eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1);
             }
             if constexpr (TB == 1) {
-                const int32_t parts = std::min(eng->opt_sweep_parts, nbg);
+                const int32_t parts = sweep_parts(eng, nbg);
                 if (!w16 && parts >= 2 && !eng->d_prof) {
                     // the batches in `parts` contiguous parts, one stream each: a part's exact
                     // pass runs beside another part's chunk-loop tail (results are per batch;
@@ -3114,18 +3145,8 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                     if (e == hipSuccess) e = hipEventRecord(eng->ev_h0, s);
                     for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) e = hipStreamWaitEvent(eng->aux_stream[k], eng->ev_h0, 0);
                     if (e != hipSuccess) return e;
-                    auto part = [&](hipStream_t st, int32_t b0, int32_t n) {
-                        Pools P = eng->pools;
-                        const size_t o = (size_t)b0 * (size_t)P.vk;
-                        P.D += o;
-                        P.Q += o;
-                        P.act += (size_t)b0 * 2 * P.Vp;
-                        P.srcv += (size_t)b0 * KL;
-                        P.row += (size_t)b0 * KL;
-                        P.mask += b0;
-                        if (P.BDU) P.BDU += o;
-                        if (P.chm) P.chm += (size_t)b0 * 2 * P.Vp;
-                        if (P.D32) P.D32 += o;
+                    auto part = [&](hipStream_t st, int32_t b0, int32_t n, int k) {
+                        const Pools P = pools_from(eng->pools, b0);
                         uint32_t* hl = eng->d_hitlog + (size_t)b0 * (size_t)(eng->Vp / TDT) * nchunks;
                         const float* mD = eng->d_minD + (size_t)b0 * nchunks * KL;
                         const int64_t nbl = 8 * (((int64_t)n * ntb + 7) / 8);
@@ -3139,10 +3160,11 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
                                            eng->opt_sweep_spiral, eng->opt_sweep_win1);
+                        if (tail && e == hipSuccess) e = (*tail)(st, b0, n, k);
                     };
                     for (int k = 0; k < parts; ++k) {
                         const int32_t b0 = (int32_t)((int64_t)nbg * k / parts), b1 = (int32_t)((int64_t)nbg * (k + 1) / parts);
-                        part(k == 0 ? s : eng->aux_stream[k - 1], b0, b1 - b0);
+                        part(k == 0 ? s : eng->aux_stream[k - 1], b0, b1 - b0, k);
                     }
                     for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) {
                         e = hipEventRecord(eng->ev_hp[k], eng->aux_stream[k]);
@@ -3182,11 +3204,11 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
 }
 
 hipError_t launch_dense_f(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
-                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s) {
+                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail = nullptr) {
     switch (eng->opt_dense_tb) {
-        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
-        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
-        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s);
+        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail);
+        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail);
+        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail);
     }
 }
 
@@ -3465,11 +3487,108 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         for (auto& e : eng->ev_spec) HIP_TRY(hipEventCreate(&e));
     }
     std::vector<uint8_t> spec_fb[SPEC_MAX];  // those rounds' full-sweep batches
+    // f32 dense delta rounds: pruned (chunk bounds, locality order), sparse (live-chunk lists)
+    // or plain; `delta_bufs` allocates the kind's scratch for all nbg batches, `enq_delta`
+    // enqueues one round over batches [b0, b0 + n) on stream st (pools, cnt rows, minDc,
+    // cmask and live lists offset to the part)
+    enum { DK_PLAIN, DK_PRUNED, DK_SPARSE };
+    const auto delta_kind = [&](bool dsparse) {
+        if (eng->vperm_ready && eng->opt_dense_prune && nvc <= PR_CHUNKS && !dsparse) return (int)DK_PRUNED;
+        return dsparse ? (int)DK_SPARSE : (int)DK_PLAIN;
+    };
+    const auto delta_bufs = [&](int kind) -> int {
+        if (kind == DK_PRUNED) {
+            const size_t need = (size_t)eng->nb_cap * nvc * KL;
+            if (eng->minDc_n < need) {
+                if (eng->d_minDc) (void)hipFree(eng->d_minDc);
+                eng->d_minDc = nullptr;
+                eng->minDc_n = 0;
+                HIP_TRY(hipMalloc((void**)&eng->d_minDc, need * sizeof(float)));
+                eng->minDc_n = need;
+            }
+            const size_t need_cm = (size_t)nblocks_delta * PR_CHUNKS;
+            if (eng->opt_delta_colbound >= 2 && eng->cmask_n < need_cm) {
+                if (eng->d_cmask) (void)hipFree(eng->d_cmask);
+                eng->d_cmask = nullptr;
+                eng->cmask_n = 0;
+                HIP_TRY(hipMalloc((void**)&eng->d_cmask, need_cm * sizeof(unsigned long long)));
+                eng->cmask_n = need_cm;
+            }
+        } else if (kind == DK_SPARSE && !eng->d_live) {
+            int rc2;
+            if ((rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_live, sizeof(int32_t) * (size_t)eng->nb_cap * nvc)) ||
+                (rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_nlive, sizeof(int32_t) * eng->nb_cap)))
+                return rc2;
+        }
+        return SHADOWTOPO_OK;
+    };
+    const auto enq_delta = [&](hipStream_t st, int32_t b0, int32_t n, int kind, int32_t par, int32_t thr,
+                               const int32_t* cprev, int32_t* ccur) {
+        const Pools P = pools_from(eng->pools, b0);
+        const int64_t c8 = (nvc + 7) / 8;
+        const uint32_t nbl = (uint32_t)(8 * n * c8);
+        cprev += b0;
+        ccur += b0;
+        if (kind == DK_PRUNED) {
+            // pruned: rows and tiles in the locality order, each block walking only the chunks
+            // whose changed pairs can pass (k_min_d32c bounds, minW64); a round after one that
+            // changed few pairs takes the live-chunk lists instead (C2: 0.95 ms pruned vs 1.05
+            // unpruned after the sweep; 0.03 vs 0.08 ms for the last round's single change).
+            // cmask is per block: a part's blocks take their own region of it
+            float* mdc = eng->d_minDc + (size_t)b0 * nvc * KL;
+            unsigned long long* cm =
+                eng->opt_delta_colbound >= 2 ? eng->d_cmask + (size_t)8 * b0 * c8 * PR_CHUNKS : nullptr;
+            hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, n), dim3(256), 0, st, P, eng->d_perm, V, nvc, par, cprev,
+                               thr, mdc);
+            hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3(nbl), dim3(64 * DW), 0, st, eng->d_W32p, eng->d_W,
+                               eng->d_WI, eng->Vp, g.in_src, g.in_r, P, V, n, nvc, par, thr, cprev, ccur, nullptr,
+                               nullptr, eng->d_perm, eng->d_minW64, mdc, eng->opt_delta_colbound ? eng->d_minW : nullptr,
+                               cm);
+            return;
+        }
+        // a round after one that changed few pairs walks only the chunks holding a changed
+        // row (k_live_chunks); after a full sweep nearly every chunk does
+        int32_t* live = nullptr;
+        int32_t* nlive = nullptr;
+        if (kind == DK_SPARSE) {
+            live = eng->d_live + (size_t)b0 * nvc;
+            nlive = eng->d_nlive + b0;
+            hipLaunchKernelGGL(k_live_chunks, dim3(n), dim3(256), 0, st, P, V, nvc, par, cprev, live, nlive);
+        }
+        hipLaunchKernelGGL(k_relax_dense_delta_s<false>, dim3(nbl), dim3(64 * DW), 0, st, eng->d_W32, eng->d_W,
+                           eng->d_WI, eng->Vp, g.in_src, g.in_r, P, V, n, nvc, par, thr, cprev, ccur, live, nlive,
+                           nullptr, nullptr, nullptr, nullptr, nullptr);
+    };
+    // chained: the blind rounds 1 .. spec_rounds go on each sweep part's stream right behind
+    // its share of the sweep (results are per batch, so a part's delta rounds need nothing
+    // from the other parts) and the parts join once, before the read-back
+    const int32_t nparts = eng->dense ? sweep_parts(eng, nbg) : 1;
+    const bool chain = eng->opt_chain_parts && spec_rounds > 0 && thresh != 0 && nparts >= 2 && !eng->d_prof;
+    int chain_kind[SPEC_MAX + 1] = {};
+    for (int32_t r = 1; chain && r <= spec_rounds; ++r) {
+        chain_kind[r] = delta_kind(eng->opt_delta_live != 2 ? eng->opt_delta_live == 1 : r >= 2);
+        if (int rc2 = delta_bufs(chain_kind[r])) return rc2;
+    }
+    if (chain && eng->opt_timing)
+        for (int k = 0; k < nparts; ++k)
+            if (!eng->ev_sw[k]) HIP_TRY(hipEventCreate(&eng->ev_sw[k]));
+    const PartTail chain_tail = [&](hipStream_t st, int32_t b0, int32_t n, int k) -> hipError_t {
+        if (eng->opt_timing) {
+            hipError_t e = hipEventRecord(eng->ev_sw[k], st);
+            if (e != hipSuccess) return e;
+        }
+        for (int32_t r = 1; r <= spec_rounds; ++r)
+            enq_delta(st, b0, n, chain_kind[r], (int32_t)(r & 1), 0x7f7f7f7e, cnt_row(r - 1), cnt_row(r));
+        return hipGetLastError();
+    };
     for (int64_t round = 0;; ++round) {
         if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
                                             (long long)max_rounds);
         const bool spec = round < spec_rounds;                   // no read-back after this round
         const bool blind = round >= 1 && round <= spec_rounds;  // decided without the last counts
+        // chained rounds 1 .. spec_rounds: enqueued with round 0 (the decisions below are the
+        // same blind ones, kept for the counts)
+        const bool chained = chain && round >= 1 && round <= spec_rounds;
         hipEvent_t e0 = eng->ev0, e1 = eng->ev1;
         if (round <= spec_rounds && !eng->ev_spec.empty()) {
             e0 = eng->ev_spec[2 * round];
@@ -3489,7 +3608,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         int32_t* cnt_cur = eng->dense ? cnt_row(round) : eng->d_cnt + (round & 1) * eng->nb_cap;
         int32_t* cnt_prev = eng->dense ? cnt_row(round - 1) : eng->d_cnt + ((round + 1) & 1) * eng->nb_cap;
         if (!eng->dense || round > spec_rounds) HIP_TRY(hipMemsetAsync(cnt_cur, 0, sizeof(int32_t) * nbg, s));
-        if (eng->opt_timing) HIP_TRY(hipEventRecord(e0, s));
+        if (eng->opt_timing && !chained) HIP_TRY(hipEventRecord(e0, s));
         bool round_full = false, round_delta = false;
         if (eng->dense) {
             // per batch: full sweep when its previous round changed more than `thresh` pairs,
@@ -3523,7 +3642,11 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     hipLaunchKernelGGL(k_relax_dense, dim3((uint32_t)nblocks_dense), dim3(256), 0, s, eng->d_W,
                                        eng->d_WI, eng->Vp, g.in_r, eng->pools, V, nbg, ntb, par, thresh, cnt_prev,
                                        cnt_cur);
-                else
+                else if (chain && round == 0) {
+                    if (std::find(full_b.begin(), full_b.end(), 0) != full_b.end() || any_delta)
+                        return fail(SHADOWTOPO_EINTERNAL, "chained rounds: round 0 is not a full sweep of every batch");
+                    HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, &chain_tail));
+                } else
                     HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s));
                 eng->st.full_sweeps++;
                 for (int32_t b = 0; b < nbg; ++b) eng->st.full_batches += full_b[b];
@@ -3534,60 +3657,14 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     hipLaunchKernelGGL(k_relax_dense_delta, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0, s,
                                        eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V, nbg, nvc, par,
                                        thr, cnt_prev, cnt_cur);
-                else if (eng->vperm_ready && eng->opt_dense_prune && nvc <= PR_CHUNKS && !dsparse) {
-                    // pruned: rows and tiles in the locality order, each block walking only the
-                    // chunks whose changed pairs can pass (k_min_d32c bounds, minW64); a round
-                    // after one that changed few pairs takes the live-chunk lists below instead
-                    // (C2: 0.95 ms pruned vs 1.05 unpruned after the sweep; 0.03 vs 0.08 ms
-                    // for the last round's single change)
-                    const size_t need = (size_t)eng->nb_cap * nvc * KL;
-                    if (eng->minDc_n < need) {
-                        if (eng->d_minDc) (void)hipFree(eng->d_minDc);
-                        eng->d_minDc = nullptr;
-                        eng->minDc_n = 0;
-                        HIP_TRY(hipMalloc((void**)&eng->d_minDc, need * sizeof(float)));
-                        eng->minDc_n = need;
+                else {
+                    const int kind = delta_kind(dsparse);
+                    if (!chained) {
+                        if (int rc2 = delta_bufs(kind)) return rc2;
+                        enq_delta(s, 0, nbg, kind, par, thr, cnt_prev, cnt_cur);
                     }
-                    const size_t need_cm = (size_t)nblocks_delta * PR_CHUNKS;
-                    if (eng->opt_delta_colbound >= 2 && eng->cmask_n < need_cm) {
-                        if (eng->d_cmask) (void)hipFree(eng->d_cmask);
-                        eng->d_cmask = nullptr;
-                        eng->cmask_n = 0;
-                        HIP_TRY(hipMalloc((void**)&eng->d_cmask, need_cm * sizeof(unsigned long long)));
-                        eng->cmask_n = need_cm;
-                    }
-                    hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, nbg), dim3(256), 0, s, eng->pools,
-                                       eng->d_perm, V, nvc, par, cnt_prev, thr, eng->d_minDc);
-                    hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
-                                       s, eng->d_W32p, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
-                                       nbg, nvc, par, thr, cnt_prev, cnt_cur, nullptr, nullptr, eng->d_perm,
-                                       eng->d_minW64, eng->d_minDc, eng->opt_delta_colbound ? eng->d_minW : nullptr,
-                                       eng->opt_delta_colbound >= 2 ? eng->d_cmask : nullptr);
-                    eng->st.pruned_deltas++;
-                } else {
-                    // a round after one that changed few pairs walks only the chunks holding
-                    // a changed row (k_live_chunks); after a full sweep nearly every chunk does
-                    const bool sparse = dsparse;
-                    const int32_t* live = nullptr;
-                    const int32_t* nlive = nullptr;
-                    if (sparse) {
-                        if (!eng->d_live) {
-                            int rc2;
-                            if ((rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_live,
-                                                 sizeof(int32_t) * (size_t)eng->nb_cap * nvc)) ||
-                                (rc2 = dev_alloc(eng->batch_allocs, (void**)&eng->d_nlive, sizeof(int32_t) * eng->nb_cap)))
-                                return rc2;
-                        }
-                        hipLaunchKernelGGL(k_live_chunks, dim3(nbg), dim3(256), 0, s, eng->pools, V, nvc, par, cnt_prev,
-                                           eng->d_live, eng->d_nlive);
-                        live = eng->d_live;
-                        nlive = eng->d_nlive;
-                        eng->st.sparse_deltas++;
-                    }
-                    hipLaunchKernelGGL(k_relax_dense_delta_s<false>, dim3((uint32_t)nblocks_delta), dim3(64 * DW), 0,
-                                       s, eng->d_W32, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, eng->pools, V,
-                                       nbg, nvc, par, thr, cnt_prev, cnt_cur, live, nlive, nullptr, nullptr,
-                                       nullptr, nullptr, nullptr);
+                    eng->st.pruned_deltas += kind == DK_PRUNED;
+                    eng->st.sparse_deltas += kind == DK_SPARSE;
                 }
                 eng->st.delta_sweeps++;
             }
@@ -3605,7 +3682,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                                eng->d_prof);
         }
         HIP_TRY(hipGetLastError());
-        if (eng->opt_timing) HIP_TRY(hipEventRecord(e1, s));
+        if (eng->opt_timing && !chained) HIP_TRY(hipEventRecord(e1, s));
         if (spec) {
             // no read-back: this round's counts come back with the next one (h_cnt_spec)
             spec_fb[round] = full_b;
@@ -3645,7 +3722,23 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     if (!spec_fb[r].empty() && spec_fb[r][b]) eng->st.full_changes += hc[b];
                 }
                 float ms = 0;
-                if (eng->opt_timing) {
+                if (eng->opt_timing && chain) {
+                    // round 0's events span every chained round (recorded before the fork and
+                    // after the join); the sweep ends when its last part's share does
+                    if (r == 0) {
+                        float all = 0, sw = 0;
+                        HIP_TRY(hipEventElapsedTime(&all, eng->ev_spec[0], eng->ev_spec[1]));
+                        for (int k = 0; k < nparts; ++k) {
+                            float t = 0;
+                            HIP_TRY(hipEventElapsedTime(&t, eng->ev_spec[0], eng->ev_sw[k]));
+                            sw = std::max(sw, t);
+                        }
+                        eng->st.relax_ms += all;
+                        eng->st.full_ms += sw;
+                        eng->st.delta_ms += all - sw;
+                        ms = all;
+                    }
+                } else if (eng->opt_timing) {
                     HIP_TRY(hipEventElapsedTime(&ms, eng->ev_spec[2 * r], eng->ev_spec[2 * r + 1]));
                     eng->st.relax_ms += ms;
                     (full ? eng->st.full_ms : eng->st.delta_ms) += ms;
@@ -3655,7 +3748,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                             r, nbg, (long long)nbg * V, full ? "full" : "delta", (long long)ch, ms);
             }
         }
-        if (eng->opt_timing) {
+        if (eng->opt_timing && !(chain && round == spec_rounds)) {  // chained: timed with round 0
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
             eng->st.relax_ms += ms;
@@ -3681,7 +3774,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         }
         if (eng->trace_rounds) {
             float ms = 0;
-            if (eng->opt_timing) (void)hipEventElapsedTime(&ms, eng->ev0, eng->ev1);
+            if (eng->opt_timing && !chained) (void)hipEventElapsedTime(&ms, e0, e1);
             fprintf(stderr, "[shadowtopo] round %lld batches %d items %lld%s%s%s changed %lld %.3f ms\n",
                     (long long)round, nbg, (long long)(round_wl ? wl_total : (int64_t)nbg * V),
                     round_wl ? " (worklist)" : "", round_full ? " full" : "", round_delta ? " delta" : "",
@@ -4775,6 +4868,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
         const char* sh = getenv("SHADOWTOPO_SWEEP_PARTS");  // A/B knob: 1, 2 (default) or 4
         if (sh && (sh[0] == '1' || sh[0] == '2' || sh[0] == '4')) eng->opt_sweep_parts = sh[0] - '0';
+        const char* cp = getenv("SHADOWTOPO_CHAIN_PARTS");  // A/B knob: 0 or 1 (default)
+        if (cp && (cp[0] == '0' || cp[0] == '1')) eng->opt_chain_parts = cp[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
 #endif
@@ -4838,6 +4933,8 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
         if (eng->aux_stream[k]) (void)hipStreamDestroy(eng->aux_stream[k]);
         if (eng->ev_hp[k]) (void)hipEventDestroy(eng->ev_hp[k]);
     }
+    for (auto e : eng->ev_sw)
+        if (e) (void)hipEventDestroy(e);
     if (eng->ev_h0) (void)hipEventDestroy(eng->ev_h0);
     if (eng->own_stream) (void)hipStreamDestroy(eng->own_stream);
     delete eng;
@@ -4951,6 +5048,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_DENSE_W16:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "dense W16 must be 0 or 1");
             eng->opt_dense_w16 = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_CHAIN_PARTS:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "chain parts must be 0 or 1");
+            eng->opt_chain_parts = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SWEEP_PARTS:
             if (value != 1 && value != 2 && value != 4) return fail(SHADOWTOPO_EINVAL, "sweep parts must be 1, 2 or 4");

@@ -653,3 +653,31 @@ def test_dense_sweep_parts(case, parts):
         g.vertex_packetloss = np.where(rng.random(500) < 0.3, 0.01, np.nan)
         g.prefer_direct = True
     compare(g, layout="dense", sweep_parts=parts)
+
+
+@pytest.mark.parametrize("chain", [0, 1])
+@pytest.mark.parametrize("parts,spec", [(2, 1), (2, 2), (4, 2), (2, 4), (4, 4)])
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
+def test_chained_part_rounds(case, parts, spec, chain):
+    """OPT_CHAIN_PARTS: the read-back-free delta rounds (OPT_DENSE_SPEC of them) enqueued on
+    each sweep part's stream behind its share of the sweep, one join before the read-back:
+    pruned, sparse and plain delta kinds on per-part pools, cnt rows, bounds and chunk masks
+    all meet the oracle bit for bit (and the unchained order with them)"""
+    rng = np.random.default_rng(11)
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=900, A=330)       # 6 batches
+    elif case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=8)
+    else:
+        g = synth.geometric_complete_ish(V=500, A=200)
+        g.vertex_packetloss = np.where(rng.random(500) < 0.3, 0.01, np.nan)
+        g.prefer_direct = True
+    compare(g, layout="dense", sweep_parts=parts, dense_spec=spec, chain_parts=chain)
+
+
+@pytest.mark.parametrize("live", [0, 1])
+def test_chained_part_rounds_delta_kinds(live):
+    """chained rounds with the live-chunk lists forced on (every blind round sparse) or off
+    (the pruned round, then plain ones): both kinds' per-part offsets"""
+    g = synth.geometric_complete_ish(V=700, A=260)
+    compare(g, layout="dense", sweep_parts=2, dense_spec=3, chain_parts=1, delta_live=live)
