@@ -427,7 +427,7 @@ def main():
                     "chunk c's all-gather overlaps chunk c+1's computation")
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-spec", type=int, default=-1, help="dense: leading rounds with no host read-back (0..4); -1 = engine default")
-    ap.add_argument("--sweep-parts", type=int, default=0, help="pruned dense sweep: batches in 1, 2 or 4 parts on their own streams (0 = engine default)")
+    ap.add_argument("--sweep-parts", type=int, default=0, help="pruned dense sweep: batches in 1 .. 4 parts on their own streams (0 = engine default)")
     ap.add_argument("--chain-parts", type=int, default=-1, help="read-back-free delta rounds on each sweep part's stream (1) or after the join (0); -1 = engine default")
     ap.add_argument("--exchange", choices=["packed", "raw"], default="packed",
                     help="N > 1, dense graphs: exchange rows packed (EngineRowCodec, default) or raw")

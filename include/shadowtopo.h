@@ -122,7 +122,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DENSE_W16 20       /* pruned dense sweep: 1 = the chunk loop filters with 16-bit weights (fp16,
                                             rounded down; half the LDS slab and the table), 0 (default) = f32.
                                             Results are identical. */
-#define SHADOWTOPO_OPT_SWEEP_PARTS 22     /* pruned dense sweep: the batches in 1, 2 (default) or 4 parts, each part's chunk
+#define SHADOWTOPO_OPT_SWEEP_PARTS 22     /* pruned dense sweep: the batches in 1 .. 4 parts (default 2), each part's chunk
                                             loop and exact pass on a stream of its own, so one part's exact pass overlaps
                                             another's chunk-loop tail. Results are identical. */
 #define SHADOWTOPO_OPT_CHAIN_PARTS 23     /* with a sweep in parts and read-back-free rounds (OPT_DENSE_SPEC > 0): 1

@@ -4866,8 +4866,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (w1 && atoi(w1) >= 0 && atoi(w1) < 64) eng->opt_sweep_win1 = atoi(w1);
         const char* ss = getenv("SHADOWTOPO_SWEEP_SPLIT");  // A/B knob: 0 or 1 (default)
         if (ss && (ss[0] == '0' || ss[0] == '1')) eng->opt_sweep_split = ss[0] - '0';
-        const char* sh = getenv("SHADOWTOPO_SWEEP_PARTS");  // A/B knob: 1, 2 (default) or 4
-        if (sh && (sh[0] == '1' || sh[0] == '2' || sh[0] == '4')) eng->opt_sweep_parts = sh[0] - '0';
+        const char* sh = getenv("SHADOWTOPO_SWEEP_PARTS");  // A/B knob: 1 .. 4 (default 2)
+        if (sh && sh[0] >= '1' && sh[0] <= '4') eng->opt_sweep_parts = sh[0] - '0';
         const char* cp = getenv("SHADOWTOPO_CHAIN_PARTS");  // A/B knob: 0 or 1 (default)
         if (cp && (cp[0] == '0' || cp[0] == '1')) eng->opt_chain_parts = cp[0] - '0';
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
@@ -5054,7 +5054,7 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_chain_parts = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SWEEP_PARTS:
-            if (value != 1 && value != 2 && value != 4) return fail(SHADOWTOPO_EINVAL, "sweep parts must be 1, 2 or 4");
+            if (value < 1 || value > 4) return fail(SHADOWTOPO_EINVAL, "sweep parts must be 1 .. 4");
             eng->opt_sweep_parts = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DENSE_SPEC:

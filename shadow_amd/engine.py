@@ -51,7 +51,7 @@ OPT_PRUNE_PENDANT = 16
 OPT_DEVICE_ROUNDS = 17
 OPT_DENSE_W16 = 20  # pruned dense sweep: 16-bit filter weights in the chunk loop (1) or f32 (0, default)
 OPT_CHAIN_PARTS = 23  # the read-back-free delta rounds on each sweep part's stream (1, default) or after the join (0)
-OPT_SWEEP_PARTS = 22  # pruned dense sweep: batches in 1, 2 (default) or 4 parts on their own streams
+OPT_SWEEP_PARTS = 22  # pruned dense sweep: batches in 1 .. 4 parts (default 2) on their own streams
 OPT_DENSE_SPEC = 21  # dense: leading rounds enqueued without a host read-back (0..4, default 2)
 OPT_DELTA_LIVE = 19  # dense delta rounds over live-chunk lists: 2 when sparse (default), 1 always, 0 never
 CSR_FULL = 1  # pull: recompute every active vertex over all in-arcs (k_relax / k_relax_wl, default)

@@ -635,7 +635,7 @@ def test_row_codec_needs_a_dense_engine():
     eng.close()
 
 
-@pytest.mark.parametrize("parts", [1, 2, 4])
+@pytest.mark.parametrize("parts", [1, 2, 3, 4])
 @pytest.mark.parametrize("case", ["geometric", "geometric_odd", "ties", "vloss_prefer"])
 def test_dense_sweep_parts(case, parts):
     """OPT_SWEEP_PARTS: the pruned sweep's batches in 1 / 2 / 4 parts, each on its own stream
@@ -656,7 +656,7 @@ def test_dense_sweep_parts(case, parts):
 
 
 @pytest.mark.parametrize("chain", [0, 1])
-@pytest.mark.parametrize("parts,spec", [(2, 1), (2, 2), (4, 2), (2, 4), (4, 4)])
+@pytest.mark.parametrize("parts,spec", [(2, 1), (2, 2), (3, 2), (4, 2), (2, 4), (4, 4)])
 @pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
 def test_chained_part_rounds(case, parts, spec, chain):
     """OPT_CHAIN_PARTS: the read-back-free delta rounds (OPT_DENSE_SPEC of them) enqueued on
