@@ -2835,6 +2835,10 @@ struct shadowtopo_engine {
     hipEvent_t ev_h0 = nullptr, ev_hp[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_sw[4] = {nullptr, nullptr, nullptr, nullptr};  // timing: each part's sweep end (chained rounds)
     int32_t opt_chain_parts = 1;       // the read-back-free delta rounds per sweep part, on the part's stream
+    // part 0's share of the batches with 2 sweep parts: it is launched first and its blocks
+    // take the CUs first, so an even split left part 1 finishing last (C2, 16 batches: 9 / 7
+    // runs the step 3.42 -> 3.32 ms, r04zr; 10 / 6 is slower, 3.61 ms)
+    int32_t opt_part0_permille = 562;
     int32_t opt_host_split = 4;        // page-locked host rows: groups a one-group computation is cut into
     int64_t opt_grid_x = (int64_t)1 << 23;  // grid_of's x limit (OPT_GRID_X)
     int32_t* d_live = nullptr;         // [nb_cap][Vp / 64] live chunk lists (k_live_chunks)
@@ -3162,8 +3166,13 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                            eng->opt_sweep_spiral, eng->opt_sweep_win1);
                         if (tail && e == hipSuccess) e = (*tail)(st, b0, n, k);
                     };
+                    auto bound = [&](int k) {
+                        if (parts == 2 && k == 1 && eng->opt_part0_permille > 0)
+                            return std::max<int32_t>(1, std::min<int32_t>(nbg - 1, (int32_t)(((int64_t)nbg * eng->opt_part0_permille + 500) / 1000)));
+                        return (int32_t)((int64_t)nbg * k / parts);
+                    };
                     for (int k = 0; k < parts; ++k) {
-                        const int32_t b0 = (int32_t)((int64_t)nbg * k / parts), b1 = (int32_t)((int64_t)nbg * (k + 1) / parts);
+                        const int32_t b0 = bound(k), b1 = bound(k + 1);
                         part(k == 0 ? s : eng->aux_stream[k - 1], b0, b1 - b0, k);
                     }
                     for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) {
@@ -4870,6 +4879,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (sh && sh[0] >= '1' && sh[0] <= '4') eng->opt_sweep_parts = sh[0] - '0';
         const char* cp = getenv("SHADOWTOPO_CHAIN_PARTS");  // A/B knob: 0 or 1 (default)
         if (cp && (cp[0] == '0' || cp[0] == '1')) eng->opt_chain_parts = cp[0] - '0';
+        const char* p0 = getenv("SHADOWTOPO_PART0_PERMILLE");  // A/B knob: part 0's share with 2 parts
+        if (p0 && atoi(p0) > 0 && atoi(p0) < 1000) eng->opt_part0_permille = atoi(p0);
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
         if (hs && atoi(hs) > 0) eng->opt_host_split = atoi(hs);
 #endif

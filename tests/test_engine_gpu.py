@@ -657,7 +657,7 @@ def test_dense_sweep_parts(case, parts):
 
 @pytest.mark.parametrize("chain", [0, 1])
 @pytest.mark.parametrize("parts,spec", [(2, 1), (2, 2), (3, 2), (4, 2), (2, 4), (4, 4)])
-@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
+@pytest.mark.parametrize("case", ["geometric", "geometric7", "ties", "vloss_prefer"])
 def test_chained_part_rounds(case, parts, spec, chain):
     """OPT_CHAIN_PARTS: the read-back-free delta rounds (OPT_DENSE_SPEC of them) enqueued on
     each sweep part's stream behind its share of the sweep, one join before the read-back:
@@ -666,6 +666,8 @@ def test_chained_part_rounds(case, parts, spec, chain):
     rng = np.random.default_rng(11)
     if case == "geometric":
         g = synth.geometric_complete_ish(V=900, A=330)       # 6 batches
+    elif case == "geometric7":
+        g = synth.geometric_complete_ish(V=900, A=430)       # 7 batches: two parts of 4 + 3 (OPT part-0 share)
     elif case == "ties":
         g = synth.integer_grid(rows=14, cols=15, seed=8)
     else:
