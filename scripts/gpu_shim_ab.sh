@@ -1,5 +1,7 @@
 #!/bin/bash
 # Lookup A/B (verdict r03 item 6): current vs r02k, one harness, warm pass finished before timing
+# (the r02k build, tools/abshim/r02k, is listed in .gpurunignore since the A/B is recorded:
+# drop that line to run this again)
 set -o pipefail
 O=gpurun_out/${1:?tag}
 mkdir -p $O
