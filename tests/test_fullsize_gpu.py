@@ -3,8 +3,8 @@
 The engine computes the bench's own workloads at the real graph size.  The north-star
 matrix (C4: all 10^4 x 10^4 attached pairs) and the whole C3 matrix (7000 x 7000) are
 compared with the CPU oracle bit for bit, every pair (the oracle over the box's CPU share:
-the C4 matrix is ~25 s of heap-exact Dijkstra on 16 threads); C2 (all 1000 rows) with 256
-random rows, so every 64-source batch is sampled; C5 (all 50 000 rows in one call, the
+the C4 matrix is ~25 s of heap-exact Dijkstra on 16 threads), and so is the whole C2 matrix
+(1000 x 1000, the headline workload); C5 (all 50 000 rows in one call, the
 bench's batch groups) with two rows of every group and the last ten.  Every computed row is
 also checked for size-independent properties: the reference's pair kinds, hop/latency
 consistency, and d(s, t) <= w(s, t) wherever the arc exists (a shortest path is never
@@ -144,10 +144,11 @@ def _oracle_rows_check(g, rows, lat, rel, hops, kind):
     assert_bitexact("reliability", rel, orel)
 
 
-def test_c2_every_batch_sampled_vs_oracle():
-    """The bench workload (all 1000 sources, 16 batches of sources in locality order): 256
-    seeded random rows against the oracle, so every batch is sampled (a batch missing all 256
-    has probability (1 - 64/1000)^256 < 1e-7)"""
+def test_c2_whole_matrix_vs_oracle():
+    """The bench workload with the bench's defaults (all 1000 sources, 16 batches in locality
+    order; the sweep in two parts of 9 and 7 batches on two streams, each part's
+    read-back-free delta rounds chained on its stream): the whole 1000 x 1000 matrix against
+    the oracle, every pair bit for bit (~75 s of oracle over the box's 16 threads)"""
     g = synth.geometric_complete_ish(V=10_000, A=1_000)
     eng = E.Engine.from_synth(g)
     eng.set_attached(g.attached)
@@ -155,8 +156,9 @@ def test_c2_every_batch_sampled_vs_oracle():
     st = eng.stats()
     eng.close()
     assert st["dense"] == 1 and st["batches"] == 16
-    rows = np.sort(np.random.default_rng(2024).choice(1000, 256, replace=False)).astype(np.int32)
-    _oracle_rows_check(g, rows, lat[rows], rel[rows], hops[rows], kind[rows])
+    assert st["full_sweeps"] == 1 and st["delta_sweeps"] >= 2
+    rows = np.arange(1000, dtype=np.int32)
+    _oracle_rows_check(g, rows, lat, rel, hops, kind)
 
 
 def test_c2_packed_rows_round_trip():
