@@ -904,9 +904,14 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
                                                const int32_t* __restrict__ WI, int32_t Vp,
                                                const double* __restrict__ in_r, int32_t parity,
                                                int32_t* __restrict__ cnt, int32_t b,
-                                               const int32_t* vids = nullptr, const SeedRows& sr = SeedRows{}) {
+                                               const int32_t* vids = nullptr, const SeedRows& sr = SeedRows{},
+                                               float* __restrict__ mdc = nullptr) {
     unsigned long long* chn = B.chm(parity);
     int32_t nch = 0;
+    // mdc (the chained rounds' pruned delta round 1): the lane's minimum new D32 over its
+    // changed pairs of these destinations, folded into the chunk's minDc entry (k_min_d32c's
+    // value, computed here instead of in a pass over the change masks after the sweep)
+    float mlo = __int_as_float(0x7f800000);
 #pragma unroll
     for (int t = 0; t < TDT; ++t) {
         const int32_t v = vids ? vids[t] : v0 + t;  // vids: the pruned sweep's permuted tile
@@ -935,12 +940,16 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
             }
             B.BDU[idx] = bdu[t];
         }
+        if (mdc && ch) mlo = fminf(mlo, f32_key(bc[t]));
         const unsigned long long m = __ballot(ch);
         if (lane == 0) chn[v] = m;
         nch += __popcll(m);
         __builtin_amdgcn_sched_barrier(0);  // keep the epilogues from being hoisted together (VGPRs)
     }
     if (nch && lane == 0) atomicAdd(&cnt[b], nch);
+    // finite D32 >= 0: the bit patterns order like the values, and the NaN reset (0x7fc00000)
+    // is above every one of them
+    if (mdc && mlo < __int_as_float(0x7f800000)) atomicMin((int*)(mdc + lane), __float_as_int(mlo));
 }
 
 __global__ __launch_bounds__(256) void k_relax_dense(const double* __restrict__ W, const int32_t* __restrict__ WI,
@@ -1050,7 +1059,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        const int32_t* __restrict__ WIp,
                                                        const double* __restrict__ WRp,
                                                        const double* __restrict__ vfac, int32_t spiral,
-                                                       int32_t win1) {
+                                                       int32_t win1, float* __restrict__ mdc_out) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -1555,7 +1564,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                     sr.rs = vfac[sv[k]];
                 }
                 dense_epilogue<TDT>(B[k], lane, sv[k], v0, V, bc[k], bdu[k], bu[k], tie[k], WI, Vp, in_r, parity,
-                                    cnt, b0 + k, vid, sr);
+                                    cnt, b0 + k, vid, sr,
+                                    mdc_out ? mdc_out + ((size_t)(b0 + k) * (Vp / KL) + v0 / KL) * KL : nullptr);
             }
     }
 }
@@ -2835,6 +2845,7 @@ struct shadowtopo_engine {
     hipEvent_t ev_h0 = nullptr, ev_hp[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_sw[4] = {nullptr, nullptr, nullptr, nullptr};  // timing: each part's sweep end (chained rounds)
     int32_t opt_chain_parts = 1;       // the read-back-free delta rounds per sweep part, on the part's stream
+    int32_t opt_fuse_mindc = 1;        // chained: round 1's chunk bounds from the exact passes' epilogues
     // part 0's share of the batches with 2 sweep parts: it is launched first and its blocks
     // take the CUs first, so an even split left part 1 finishing last (C2, 16 batches: 9 / 7
     // runs the step 3.42 -> 3.32 ms, r04zr; 10 / 6 is slower, 3.61 ms)
@@ -3089,7 +3100,8 @@ using PartTail = std::function<hipError_t(hipStream_t, int32_t, int32_t, int)>;
 // the f32-filtered full sweep: 8 destinations per wave, exact rows settled 2 at a time
 template <int TB>
 hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
-                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail) {
+                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail,
+                           float* mdc_out) {
     constexpr int TDT = FTDT, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
@@ -3132,7 +3144,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                        0, s, (const float*)eng->d_W16p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
                                        eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev, cnt_cur, eng->d_prof,
                                        eng->d_hitlog, eng->d_perm, eng->d_minW, eng->d_minD, eng->d_pos, eng->d_WIp,
-                                       eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1);
+                                       eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr);
             }
             if constexpr (TB == 1) {
                 const int32_t parts = sweep_parts(eng, nbg);
@@ -3146,6 +3158,10 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                         if (!eng->aux_stream[k]) e = hipStreamCreateWithFlags(&eng->aux_stream[k], hipStreamNonBlocking);
                         if (e == hipSuccess && !eng->ev_hp[k]) e = hipEventCreateWithFlags(&eng->ev_hp[k], hipEventDisableTiming);
                     }
+                    // mdc_out (chained rounds): minDc, filled by the exact passes' epilogues, reset
+                    // to NaN (no changed pair) first
+                    if (e == hipSuccess && mdc_out)
+                        e = hipMemsetD32Async((hipDeviceptr_t)mdc_out, 0x7fc00000, (size_t)nbg * (eng->Vp / KL) * KL, s);
                     if (e == hipSuccess) e = hipEventRecord(eng->ev_h0, s);
                     for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) e = hipStreamWaitEvent(eng->aux_stream[k], eng->ev_h0, 0);
                     if (e != hipSuccess) return e;
@@ -3158,12 +3174,13 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
-                                           eng->opt_sweep_spiral, eng->opt_sweep_win1);
+                                           eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr);
                         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 2>), dim3((uint32_t)nbl), dim3(256), 0, st,
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
-                                           eng->opt_sweep_spiral, eng->opt_sweep_win1);
+                                           eng->opt_sweep_spiral, eng->opt_sweep_win1,
+                                           mdc_out ? mdc_out + (size_t)b0 * (eng->Vp / KL) * KL : nullptr);
                         if (tail && e == hipSuccess) e = (*tail)(st, b0, n, k);
                     };
                     auto bound = [&](int k) {
@@ -3188,7 +3205,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
                                eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
-                               eng->opt_sweep_win1);
+                               eng->opt_sweep_win1, nullptr);
             // (4 logged rows in flight per wave instead of 2 measured the same, r03u); one batch
             // per wave whatever TB the chunk loop ran with (the f64 state of two would spill)
             const int64_t nblocks1 = 8 * (((int64_t)nbg * ntb + 7) / 8);
@@ -3196,28 +3213,29 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
                                eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
-                               eng->opt_sweep_win1);
+                               eng->opt_sweep_win1, nullptr);
             return hipGetLastError();
         }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par,
                            thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
                            eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
-                               eng->opt_sweep_win1);
+                               eng->opt_sweep_win1, nullptr);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, false>), dim3((uint32_t)nblocks), dim3(256), 0, s, eng->d_W32,
                        eng->d_W, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb, par, thresh, cnt_prev,
-                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0);
+                       cnt_cur, eng->d_prof, eng->d_hitlog, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_dense_f(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
-                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail = nullptr) {
+                          const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail = nullptr,
+                          float* mdc_out = nullptr) {
     switch (eng->opt_dense_tb) {
-        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail);
-        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail);
-        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail);
+        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out);
+        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out);
+        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out);
     }
 }
 
@@ -3532,7 +3550,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         return SHADOWTOPO_OK;
     };
     const auto enq_delta = [&](hipStream_t st, int32_t b0, int32_t n, int kind, int32_t par, int32_t thr,
-                               const int32_t* cprev, int32_t* ccur) {
+                               const int32_t* cprev, int32_t* ccur, bool mindc_ready = false) {
         const Pools P = pools_from(eng->pools, b0);
         const int64_t c8 = (nvc + 7) / 8;
         const uint32_t nbl = (uint32_t)(8 * n * c8);
@@ -3547,8 +3565,9 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             float* mdc = eng->d_minDc + (size_t)b0 * nvc * KL;
             unsigned long long* cm =
                 eng->opt_delta_colbound >= 2 ? eng->d_cmask + (size_t)8 * b0 * c8 * PR_CHUNKS : nullptr;
-            hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, n), dim3(256), 0, st, P, eng->d_perm, V, nvc, par, cprev,
-                               thr, mdc);
+            if (!mindc_ready)
+                hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, n), dim3(256), 0, st, P, eng->d_perm, V, nvc, par,
+                                   cprev, thr, mdc);
             hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3(nbl), dim3(64 * DW), 0, st, eng->d_W32p, eng->d_W,
                                eng->d_WI, eng->Vp, g.in_src, g.in_r, P, V, n, nvc, par, thr, cprev, ccur, nullptr,
                                nullptr, eng->d_perm, eng->d_minW64, mdc, eng->opt_delta_colbound ? eng->d_minW : nullptr,
@@ -3578,6 +3597,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         chain_kind[r] = delta_kind(eng->opt_delta_live != 2 ? eng->opt_delta_live == 1 : r >= 2);
         if (int rc2 = delta_bufs(chain_kind[r])) return rc2;
     }
+    // a pruned round 1 takes its chunk bounds from the sweep's exact passes (k_min_d32c's
+    // values, folded in by their epilogues: the pass over the change masks after the sweep
+    // waited ~0.12 ms for CUs behind the other part's kernels, r04zx)
+    const bool fuse_mindc = chain && eng->opt_fuse_mindc && chain_kind[1] == DK_PRUNED;
     if (chain && eng->opt_timing)
         for (int k = 0; k < nparts; ++k)
             if (!eng->ev_sw[k]) HIP_TRY(hipEventCreate(&eng->ev_sw[k]));
@@ -3587,7 +3610,8 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
         for (int32_t r = 1; r <= spec_rounds; ++r)
-            enq_delta(st, b0, n, chain_kind[r], (int32_t)(r & 1), 0x7f7f7f7e, cnt_row(r - 1), cnt_row(r));
+            enq_delta(st, b0, n, chain_kind[r], (int32_t)(r & 1), 0x7f7f7f7e, cnt_row(r - 1), cnt_row(r),
+                      r == 1 && fuse_mindc);
         return hipGetLastError();
     };
     for (int64_t round = 0;; ++round) {
@@ -3654,7 +3678,8 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                 else if (chain && round == 0) {
                     if (std::find(full_b.begin(), full_b.end(), 0) != full_b.end() || any_delta)
                         return fail(SHADOWTOPO_EINTERNAL, "chained rounds: round 0 is not a full sweep of every batch");
-                    HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, &chain_tail));
+                    HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, &chain_tail,
+                                           fuse_mindc ? eng->d_minDc : nullptr));
                 } else
                     HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s));
                 eng->st.full_sweeps++;
@@ -4879,6 +4904,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
         if (sh && sh[0] >= '1' && sh[0] <= '4') eng->opt_sweep_parts = sh[0] - '0';
         const char* cp = getenv("SHADOWTOPO_CHAIN_PARTS");  // A/B knob: 0 or 1 (default)
         if (cp && (cp[0] == '0' || cp[0] == '1')) eng->opt_chain_parts = cp[0] - '0';
+        const char* fm = getenv("SHADOWTOPO_FUSE_MINDC");  // A/B knob: 0 or 1 (default)
+        if (fm && (fm[0] == '0' || fm[0] == '1')) eng->opt_fuse_mindc = fm[0] - '0';
         const char* p0 = getenv("SHADOWTOPO_PART0_PERMILLE");  // A/B knob: part 0's share with 2 parts
         if (p0 && atoi(p0) > 0 && atoi(p0) < 1000) eng->opt_part0_permille = atoi(p0);
         const char* hs = getenv("SHADOWTOPO_HOST_SPLIT");
