@@ -36,7 +36,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_ENOMEM (-2)   /* host or device allocation failed */
 #define SHADOWTOPO_EDEVICE (-3)  /* HIP runtime error, or no GPU */
 #define SHADOWTOPO_ESTATE (-4)   /* call out of order (e.g. compute before set_attached) */
-#define SHADOWTOPO_EINTERNAL (-5) /* iteration guard tripped */
+#define SHADOWTOPO_EINTERNAL (-5) /* iteration guard tripped, or a path walk left the predecessor tree */
 
 /* graph flags (topology.c:751-790: isDirected, isComplete, prefersDirectPaths) */
 #define SHADOWTOPO_F_DIRECTED 0x1u
@@ -132,6 +132,17 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_DENSE_SPEC 21      /* dense rounds: how many leading rounds (0..4, default 2) are enqueued with no
                                             host read-back of their change counts; a round decided without them runs
                                             the delta kernel over every batch that changed. Results are identical. */
+#define SHADOWTOPO_OPT_HEAVY_FIRST 27       /* pruned dense sweep in parts: 1 (default) = each part's chunk-loop blocks
+                                              in decreasing order of the chunks they staged in the previous sweep of
+                                              the same shape (per XCD), 0 = grid order. Results are identical. */
+/* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
+ * instead of faulting the device */
+#define SHADOWTOPO_OPT_TEST_UNCONVERGED 24  /* 1 = when the iteration guard (OPT_MAX_ROUNDS) trips, compose the state
+                                              the rounds stopped at (bounded path walks), then fail */
+#define SHADOWTOPO_OPT_TEST_SCRAMBLE_TREE 25 /* 1 / 2 = overwrite every reached pair's predecessor arc before compose
+                                               (1: past the arc range, 2: the vertex's first in-arc) */
+#define SHADOWTOPO_OPT_TEST_POOL_ENOMEM 26  /* 1 = the next batch-pool allocation fails after its first buffer, as if
+                                              another engine had taken the HBM (exercises the re-sized retry) */
 #define SHADOWTOPO_OPT_HBM_SHARE 13         /* per mille of the batch-slot HBM budget (55 % of free HBM, at least 24 GB) this
                                               engine may take (default 1000); engines sharing one device split it */
 
@@ -208,6 +219,8 @@ typedef struct shadowtopo_stats {
     int64_t fold_rounds;
     int64_t packed_pairs;    /* row exchange codec: pairs packed, and of them sent explicitly */
     int64_t packed_explicit;
+    double compose_kernel_ms; /* OPT_TIMING: HIP-event time of the pair compose (k_compose + k_walk) */
+    int64_t walk_targets;    /* attached targets whose pairs take the full path fold (vertex loss, multigraphs) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

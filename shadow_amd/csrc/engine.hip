@@ -92,6 +92,7 @@ struct GraphDev {
     const int32_t* out_dst;
     const int64_t* inc_ptr;  // [V+1] igraph_incident(OUT) order, loops included
     const int32_t* inc_eid;
+    const double* inc_lat;   // [inc] elat in that order (k_self's contiguous scan)
     const int32_t* efrom;    // igraph storage (undirected: from = max, to = min)
     const int32_t* eto;
     const double* elat;
@@ -145,6 +146,8 @@ struct Pools {
     double* BDU;        // dense mode: [slot][Vp][64] d(pred) of the recorded predecessor (lex key)
     unsigned long long* chm;   // dense mode: [slot][2][Vp] lanes whose (v, source) state changed, per round parity
     float* D32;         // dense mode: [slot][Vp][64] f32 filter key (distance rounded down, NaN unreached)
+    unsigned long long* err;   // compose: nonzero when a path walk left the predecessor tree (the word
+                               // before mask[0]: reset and read back together with the masks)
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
@@ -1059,7 +1062,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        const int32_t* __restrict__ WIp,
                                                        const double* __restrict__ WRp,
                                                        const double* __restrict__ vfac, int32_t spiral,
-                                                       int32_t win1, float* __restrict__ mdc_out) {
+                                                       int32_t win1, float* __restrict__ mdc_out,
+                                                       const int32_t* __restrict__ border = nullptr,
+                                                       uint32_t* __restrict__ bweight = nullptr) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -1081,7 +1086,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
     __shared__ __attribute__((aligned(16))) float sW[2][H16 ? SRS * BW / 2 : SRS * BW];
     int32_t grp, vt;
-    if (!xcd_tile(blockIdx.x, (nb + TB - 1) / TB, ntb, grp, vt)) return;  // block-uniform exits only (barriers below)
+    // heavy-first (PH 1): border maps the hardware block to a (batch, tile) item of the same
+    // XCD, the items of each XCD in decreasing chunk counts of the previous sweep (k_heavy_order),
+    // so the longest blocks start first and the ragged tail shrinks; any order is exact
+    const int64_t Lb = border ? (int64_t)border[blockIdx.x] : (int64_t)blockIdx.x;
+    if (!xcd_tile(Lb, (nb + TB - 1) / TB, ntb, grp, vt)) return;  // block-uniform exits only (barriers below)
     const int32_t b0 = grp * TB;  // this block's TB batches
     bool live[TB];
     int32_t first = -1;
@@ -1090,9 +1099,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         live[k] = b0 + k < nb && cnt_prev[b0 + k] > thresh;
         if (live[k] && first < 0) first = b0 + k;
     }
-    if (first < 0) return;
+    if (first < 0 || vt * BW >= V) {
+        if (PH == 1 && bweight && threadIdx.x == 0) bweight[Lb] = 0u;
+        return;
+    }
     const int32_t vb = vt * BW;
-    if (vb >= V) return;
     const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int32_t v0 = vb + wave * TDT;
@@ -1342,6 +1353,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     // chunks in flight: itc (in LDS, filtered this iteration), itn (its loads issued this
     // iteration, staged at its end) and itn2 (its rows' perm entries loaded this iteration)
     int32_t prow_n[DQ];
+    uint32_t nvis = 0;  // chunks this block staged (its weight for the next sweep's order)
     int32_t itc = next_live(0);
     if (itc >= 0) {
         perm_of(itc, prow_n);
@@ -1493,7 +1505,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         bufc ^= 1;
         itc = itn;
         itn = itn2;
+        ++nvis;
     }
+    if (PH == 1 && bweight && threadIdx.x == 0) bweight[Lb] = nvis;
     }  // PH != 2
     if constexpr (PH == 1) return;
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
@@ -1567,6 +1581,50 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                     cnt, b0 + k, vid, sr,
                                     mdc_out ? mdc_out + ((size_t)(b0 + k) * (Vp / KL) + v0 / KL) * KL : nullptr);
             }
+    }
+}
+
+// Heavy-first order of a pruned chunk-loop launch (border for k_relax_dense_f<.., PH = 1>):
+// block (x, part) sorts the S = nblocks / 8 items XCD x runs in that part (L = 8 j + x, j < S)
+// by the chunk counts their blocks staged last time, largest first (ties by j), and writes
+// order[8 r + x] = 8 j(r) + x: the hardware block of slot r on XCD x takes the item of rank r.
+// A permutation whatever the weights (read while another part's sweep may rewrite them).
+constexpr int HEAVY_MAX = 2048;  // items per XCD the one-block bitonic sort takes
+struct HeavyArgs {
+    const uint32_t* w[4];  // per part: the chunk counts of its last sweep's blocks
+    int32_t* o[4];         // per part: the order buffer the next sweep reads
+    int32_t slots[4];      // per part: items per XCD (0: no sort)
+};
+__global__ __launch_bounds__(1024) void k_heavy_order(HeavyArgs ha) {
+    __shared__ unsigned long long key[HEAVY_MAX];
+    const int x = blockIdx.x, part = blockIdx.y;
+    const int32_t S = ha.slots[part];
+    if (S <= 0) return;
+    const uint32_t* w = ha.w[part];
+    int32_t* ord = ha.o[part];
+    int n2 = 1;
+    while (n2 < S) n2 <<= 1;
+    for (int j = threadIdx.x; j < n2; j += blockDim.x)
+        key[j] = j < S ? ((unsigned long long)w[8 * j + x] << 32) | (uint32_t)(0xffffffffu - (uint32_t)j) : 0ull;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const unsigned long long a = key[i], b = key[l];
+                    const bool desc = (i & k) == 0;  // descending overall
+                    if (desc ? a < b : a > b) {
+                        key[i] = b;
+                        key[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int r = threadIdx.x; r < S; r += blockDim.x) {
+        const int32_t j = (int32_t)(0xffffffffu - (uint32_t)key[r]);
+        ord[8 * r + x] = 8 * j + x;
     }
 }
 
@@ -2308,16 +2366,25 @@ __global__ __launch_bounds__(256) void k_min_d32c(Pools pools, const int32_t* __
 // _topology_computeShortestPathToSelf (topology.c:1545-1653): first strict minimum of the
 // OUT-incident edges in igraph order, used twice; or (F_SELF_DIJKSTRA_LOOP) the [s] path
 // through the source's self-loop (topology.c:1456-1499).
-// One wave per attached vertex: each lane keeps the first strict minimum of its strided
-// slice of the incidence list (position order), then a wave reduction on (latency,
-// position) picks the first strict minimum overall -- the reference's sequential rule.
-__global__ __launch_bounds__(256) void k_self(GraphDev g, const int32_t* __restrict__ attached, int32_t A,
+// Rows [i0, i1) of the attached list, run inside every computation of those rows (the
+// reference computes the self path per query, so a matrix build includes it).  The
+// incidence latencies are one contiguous array in igraph order (inc_lat): each thread keeps
+// the first strict minimum of its strided slice (positions ascending, so a strict '<' keeps
+// the first), then a reduction on (latency, position) picks the first strict minimum overall
+// -- the reference's sequential rule.  BLK = true: a 256-thread block per vertex (dense
+// graphs: C2's 9 500 incident edges per vertex), else one wave per vertex.
+template <bool BLK>
+__global__ __launch_bounds__(256) void k_self(GraphDev g, const int32_t* __restrict__ attached, int32_t i0, int32_t i1,
                                               double* self_lat, double* self_rel, uint32_t* self_hops,
                                               uint8_t* self_kind) {
-    const int32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (i >= A) return;
+    __shared__ double sl[4];
+    __shared__ int64_t sp[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int32_t i = i0 + (BLK ? (int32_t)blockIdx.x : (int32_t)blockIdx.x * 4 + wave);
+    if (i >= i1) return;  // uniform per block (BLK) or per wave
     const int32_t v = attached[i];
+    const int tid = BLK ? (int)threadIdx.x : lane;
+    constexpr int NT = BLK ? 256 : 64;
     double lat = -1.0, rel = -1.0;
     uint32_t hops = 0;
     uint8_t kind = SHADOWTOPO_KIND_NONE;
@@ -2330,32 +2397,51 @@ __global__ __launch_bounds__(256) void k_self(GraphDev g, const int32_t* __restr
             hops = 1;
             kind = SHADOWTOPO_KIND_DIJKSTRA;
         }
-    } else if (g.inc_ptr[v + 1] > g.inc_ptr[v]) {
+    } else {
         const int64_t beg = g.inc_ptr[v], end = g.inc_ptr[v + 1];
-        double minl = dinf();
-        int64_t pos = INT64_MAX;
-        for (int64_t x = beg + lane; x < end; x += 64) {
-            const double l = g.elat[g.inc_eid[x]];
-            if (l < minl) {
-                minl = l;
-                pos = x;
+        if (end > beg) {
+            double minl = dinf();
+            int64_t pos = INT64_MAX;
+            for (int64_t x = beg + tid; x < end; x += 4 * NT) {
+                double l[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) l[k] = x + k * NT < end ? g.inc_lat[x + k * NT] : dinf();
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (l[k] < minl) {
+                        minl = l[k];
+                        pos = x + k * NT;
+                    }
             }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            const double ol = __shfl_xor(minl, off);
-            const int64_t op = __shfl_xor(pos, off);
-            if (ol < minl || (ol == minl && op < pos)) {
-                minl = ol;
-                pos = op;
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ol = __shfl_xor(minl, off);
+                const int64_t op = __shfl_xor(pos, off);
+                if (ol < minl || (ol == minl && op < pos)) {
+                    minl = ol;
+                    pos = op;
+                }
             }
+            if (BLK) {
+                if (lane == 0) {
+                    sl[wave] = minl;
+                    sp[wave] = pos;
+                }
+                __syncthreads();
+                for (int w = 0; w < 4; ++w)
+                    if (sl[w] < minl || (sl[w] == minl && sp[w] < pos)) {
+                        minl = sl[w];
+                        pos = sp[w];
+                    }
+            }
+            // every incidence latency is finite (validated), so pos is a real entry
+            const double rmin = g.erel[g.inc_eid[pos]];
+            lat = 2.0 * minl;
+            rel = rmin * rmin;
+            hops = 2;
+            kind = SHADOWTOPO_KIND_SELF;
         }
-        const double rmin = g.erel[g.inc_eid[pos]];
-        lat = 2.0 * minl;
-        rel = rmin * rmin;
-        hops = 2;
-        kind = SHADOWTOPO_KIND_SELF;
     }
-    if (lane == 0) {
+    if (tid == 0) {
         self_lat[i] = lat;
         self_rel[i] = rel;
         self_hops[i] = hops;
@@ -2412,20 +2498,128 @@ __device__ __forceinline__ bool dispatch_pair(const GraphDev& g, int32_t s, int3
 }
 
 // forward fold over the tree path (topology.c:1473-1499): lat from 0.0, rel from
-// (1-ls)*(1-lt), each hop's edge = get_eid edge; O(h^2) walk, used only when the target
-// carries vertex loss != 0 or the graph has parallel edges of different latency.
-__device__ void walk_tree(const GraphDev& g, const BatchDev& B, int lane, int32_t s, int32_t t, uint32_t h,
-                          PairOut& o) {
-    double lat = 0.0, rel = g.vfac[s] * g.vfac[t];
-    for (uint32_t i = 0; i < h; ++i) {
-        int32_t x = t;
-        for (uint32_t k = 0; k + 1 + i < h; ++k) x = g.in_src[B.Q[(size_t)x * KL + lane].p];
-        const int32_t arc = B.Q[(size_t)x * KL + lane].p;
-        lat += g.elat[g.in_eid[arc]];
-        rel *= g.in_r[arc];
+// (1-ls)*(1-lt), each hop's edge = get_eid edge; used only when the target carries vertex
+// loss != 0 or the graph has parallel edges of different latency.  The path x_0 = s .. x_h = t
+// is known backwards only (arc a_i = P(x_i) enters x_i from x_{i-1}), and the fold runs
+// forwards, so a walk from t stores the arcs in LDS scratch (WALK_SEG per chain, stride
+// COMPOSE_T) and folds them in order: h steps when h <= WALK_SEG, segments of WALK_SEG arcs
+// (each re-walked from t) beyond.  Two targets' walks run in lockstep per lane (two
+// independent load chains in flight: a step is a dependent record load then an arc-tail
+// load).  Bounded: every step checks the arc and the vertex it leads to, and a walk must
+// arrive at s after exactly h arcs and never before; a walk that fails sets an error bit
+// (1: out of range, 2: hop count disagrees) for compose to report, instead of following
+// garbage through memory (a non-converged state's records need not form a tree).
+constexpr int WALK_SEG = 8;
+struct WalkChain {
+    int32_t s, t;  // source, target (relaxation view ids)
+    int32_t l;     // the source's lane in its batch
+    uint32_t h;    // hop count the tree recorded
+    bool on;       // this chain walks
+    double lat, rel;
+};
+
+// one 16-byte load per hop of a walk: the arc's tail (the next vertex), its get_eid edge (for
+// a multigraph's latency) and its reliability factor in_r (k_arcinfo builds it from the view's
+// in-CSR when some pair needs a walk)
+struct __attribute__((aligned(16))) ArcInfo {
+    int32_t u, eid;
+    double r;
+};
+
+__global__ __launch_bounds__(256) void k_arcinfo(const int32_t* __restrict__ in_src, const int32_t* __restrict__ in_eid,
+                                                 const double* __restrict__ in_r, int64_t n, ArcInfo* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        ArcInfo a;
+        a.u = in_src[i];
+        a.eid = in_eid[i];
+        a.r = in_r[i];
+        out[i] = a;
     }
-    if (g.multigraph) o.lat = (lat == 0) ? 1.0 : lat;
-    o.rel = rel;
+}
+
+// Two walks in lockstep.  A step is two dependent loads: the record's predecessor arc, then
+// the arc's {tail, edge, factor} (ArcInfo); the factors of a segment's arcs go to LDS scratch
+// (sc: slot k of chain c at sc[(c * WALK_SEG + k) * stride], a double, a_{k0+1+k} in slot k)
+// and the fold reads them forwards.
+template <bool MG>
+__device__ uint32_t walk_pair(const GraphDev& g, const ArcInfo* __restrict__ ai, const BatchDev& B, WalkChain* w,
+                              double* sc, int32_t* se, int stride) {
+    const int64_t na = g.in_ptr[g.V];
+    uint32_t err = 0;
+    uint32_t hmax = 0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (w[c].on && (w[c].h == 0 || w[c].h > (uint32_t)g.V)) {
+            err |= 2u;
+            w[c].on = false;
+        }
+        if (w[c].on) {
+            w[c].lat = 0.0;
+            w[c].rel = g.vfac[w[c].s] * g.vfac[w[c].t];
+            hmax = max(hmax, w[c].h);
+        }
+    }
+    for (uint32_t k0 = 0; k0 < hmax; k0 += WALK_SEG) {
+        int32_t x[2];
+        uint32_t i[2];
+        bool a[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            x[c] = w[c].t;
+            i[c] = w[c].h;  // x = x_i: the next step takes a_i and moves to x_{i-1}
+            a[c] = w[c].on && w[c].h > k0;
+        }
+        while (a[0] || a[1]) {
+            int32_t p[2] = {0, 0};
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                if (a[c]) p[c] = B.Q[(size_t)x[c] * KL + w[c].l].p;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                if (a[c] && (p[c] < 0 || (int64_t)p[c] >= na)) {
+                    err |= 1u;
+                    a[c] = w[c].on = false;
+                }
+            u32x4 v[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                if (a[c]) v[c] = *(const __attribute__((address_space(1))) u32x4*)(ai + p[c]);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (!a[c]) continue;
+                const int32_t u = (int32_t)v[c].x;
+                if (i[c] <= k0 + WALK_SEG) {
+                    const size_t k = (size_t)(c * WALK_SEG + (i[c] - k0 - 1)) * stride;
+                    sc[k] = __longlong_as_double((long long)(((unsigned long long)v[c].w << 32) | v[c].z));
+                    if (MG) se[k] = (int32_t)v[c].y;
+                }
+                if (u < 0 || u >= g.V) {
+                    err |= 1u;
+                    a[c] = w[c].on = false;
+                    continue;
+                }
+                if ((u == w[c].s) != (i[c] == 1)) {
+                    err |= 2u;
+                    a[c] = w[c].on = false;
+                    continue;
+                }
+                x[c] = u;
+                --i[c];
+                a[c] = i[c] > k0;
+            }
+        }
+        // fold this segment's factors forwards
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (!w[c].on || w[c].h <= k0) continue;
+            const uint32_t n = min(w[c].h, k0 + (uint32_t)WALK_SEG) - k0;
+            for (uint32_t k = 0; k < n; ++k) {
+                w[c].rel *= sc[(size_t)(c * WALK_SEG + k) * stride];
+                if (MG) w[c].lat += g.elat[se[(size_t)(c * WALK_SEG + k) * stride]];
+            }
+        }
+    }
+    return err;
 }
 
 // 512 threads: 8 targets per wave instead of 16 (the per-lane pair values live in registers
@@ -2470,10 +2664,9 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
                     o.hops = h & HMASK;
                     o.lat = (d == 0) ? 1.0 : d;  // topology.c:1848-1852
                     o.kind = SHADOWTOPO_KIND_DIJKSTRA;
-                    if (g.multigraph || g.vfac[t] != 1.0)
-                        walk_tree(g, B, lane, s, t, o.hops, o);
-                    else
-                        o.rel = q.r;
+                    // the tree fold (k_walk re-folds the targets with vertex loss, and every
+                    // pair of a multigraph, in the reference's order)
+                    o.rel = q.r;
                 }
             }
         }
@@ -2520,6 +2713,69 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
             if (out_kind) out_kind[(size_t)(r - row_base) * A + ti] = (uint8_t)su[64 * 65 + j * 65 + tl];
         }
     }
+}
+
+// The pairs whose path needs the reference's full fold (topology.c:1429-1499): targets that
+// carry vertex loss (rel = ((1 * a_s) * a_t) * e_1 * ... -- a_t enters before the edges, so
+// the tree's fold R(t) is not it), and every pair of a multigraph whose lowest-id parallel
+// edge is not the minimum (lat from the get_eid edges).  After k_compose wrote the rows, this
+// overwrites those pairs' rel (and lat) with the walked fold.  Lane = source, as in the
+// relaxation: the 64 walks of a wave all start at one target, and paths from nearby sources
+// into one target share their last hops, so a step's record loads fall in few lines (lane =
+// target instead measured 4.6 ms of walks on C4L against 4.0).  A block takes one batch and
+// WALK_TPB of the walk targets, each of its 4 waves WALK_TPB / 4 of them, two at a time
+// (walk_pair); blocks go batch-major, so few batches' records are read at once.
+constexpr int WALK_T = 256;
+constexpr int WALK_TPB = 8;
+template <bool MG>
+__global__ __launch_bounds__(WALK_T) void k_walk(GraphDev g, const ArcInfo* __restrict__ ai, Pools pools,
+                                                const int32_t* __restrict__ attached,
+                                                const int32_t* __restrict__ walk_ti, int32_t nw, int32_t A,
+                                                double* out_lat, double* out_rel, int32_t row_base, int32_t ls) {
+    __shared__ double sc[2 * WALK_SEG * WALK_T];
+    __shared__ int32_t se[MG ? 2 * WALK_SEG * WALK_T : 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int32_t sv = B.srcv[lane], row = B.row[lane];
+    const bool prefer = (g.flags & SHADOWTOPO_F_PREFER_DIRECT) != 0;
+    uint32_t err = 0;
+    constexpr int TPW = WALK_TPB / (WALK_T / 64);  // walk targets per wave
+    const int32_t k0 = blockIdx.x * WALK_TPB + wave * TPW;
+    for (int32_t k = k0; k < min(nw, k0 + TPW); k += 2) {
+        WalkChain w[2];
+        int32_t ti[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const bool tk = k + c < min(nw, k0 + TPW);
+            ti[c] = tk ? walk_ti[k + c] : 0;
+            const int32_t t = tk ? attached[ti[c]] : 0;
+            w[c].s = sv;
+            w[c].t = t;
+            w[c].l = lane;
+            w[c].on = false;
+            w[c].h = 0;
+            w[c].lat = 0.0;
+            w[c].rel = 0.0;
+            // a shortest-path pair (the dispatch's rule 3): not the self pair, not a direct
+            // pair of a prefer-direct graph, reached
+            if (tk && sv >= 0 && row >= 0 && sv != t && !(prefer && get_eid(g, sv, t) >= 0)) {
+                const size_t idx = (size_t)t * KL + lane;
+                if (B.D[idx] < dinf()) {
+                    w[c].h = B.Q[idx].h & HMASK;
+                    w[c].on = true;
+                }
+            }
+        }
+        err |= walk_pair<MG>(g, ai, B, w, sc + threadIdx.x, se + (MG ? threadIdx.x : 0), WALK_T);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            if (w[c].on) {
+                const size_t o = ((size_t)(row - row_base) * A + ti[c]) * ls;
+                out_rel[o] = w[c].rel;
+                if (MG) out_lat[o] = (w[c].lat == 0) ? 1.0 : w[c].lat;
+            }
+    }
+    if (err) atomicOr(pools.err, (unsigned long long)err);
 }
 
 // ---------------------------------------------------------------- heap-exact replay
@@ -2710,6 +2966,27 @@ __global__ void k_extract(GraphDev g, Pools pools, int32_t nsrc, double* dist, i
     if (tie) tie[o] = (reached && (B.Q[idx].h & TAINT)) ? 1 : 0;
 }
 
+// testing (OPT_TEST_SCRAMBLE_TREE): overwrite the predecessor arc of every reached
+// (vertex, source) pair but the source's own -- mode 1 past the arc range, mode 2 with the
+// vertex's first in-arc (in range, but no longer a tree) -- so compose's path walks meet the
+// states a convergence bug would leave; they must report an error, not fault.
+__global__ void k_scramble_tree(GraphDev g, Pools pools, int32_t mode) {
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int64_t na = g.in_ptr[g.V];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)g.V * KL;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int32_t v = (int32_t)(i / KL);
+        const int lane = (int)(i % KL);
+        if (!(B.D[i] < dinf()) || B.srcv[lane] == v || B.srcv[lane] < 0) continue;
+        int64_t p = na + v;
+        if (mode == 2) {
+            if (g.in_ptr[v + 1] == g.in_ptr[v]) continue;
+            p = g.in_ptr[v];
+        }
+        B.Q[i].p = (int32_t)p;
+    }
+}
+
 // ---------------------------------------------------------------- host side
 struct DevBuf {
     void* p = nullptr;
@@ -2785,7 +3062,22 @@ struct shadowtopo_engine {
     double* d_self_rel = nullptr;
     uint32_t* d_self_hops = nullptr;
     uint8_t* d_self_kind = nullptr;
-    bool self_ready = false;
+    size_t att_cap = 0;       // entries d_attached / d_self_* hold
+    std::vector<double> h_vfac;  // [V] 1 - vertex packetloss (1.0 when absent)
+    int32_t* d_walk = nullptr;   // attached indices whose pairs k_walk re-folds
+    size_t walk_cap = 0;
+    int32_t n_walk = 0;
+    bool walk_ready = false;
+    ArcInfo* d_arcinfo = nullptr;      // k_walk's per-arc table of the relaxation graph
+    size_t arcinfo_cap = 0;
+    const int32_t* arcinfo_of = nullptr;
+    uint64_t arcinfo_gen = 0;
+    uint64_t view_gen = 0;             // ensure_pruned's rebuilds of the relaxation view
+    int64_t gp_arcs = 0;               // arcs of that view
+    bool self_timed = false;  // the self rule's time of this attached set was measured (self_ms)
+    bool self_blk = false;    // k_self: a block per vertex (>= 128 incidence entries per vertex on average)
+    hipEvent_t ev_self[2] = {nullptr, nullptr};
+    hipEvent_t ev_cmp[2] = {nullptr, nullptr};  // OPT_TIMING: around k_compose
     // batch pool
     int32_t nb_cap = 0;
     Pools pools{};                       // device pools for nb_cap batch slots
@@ -2864,6 +3156,17 @@ struct shadowtopo_engine {
     size_t pk_scratch_n = 0;
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
+    int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
+    uint32_t* d_bweight[4] = {nullptr, nullptr, nullptr, nullptr};  // per part: chunk counts per block
+    int32_t* d_border[4][2] = {};     // per part: two order buffers (ping-pong across sweeps)
+    size_t heavy_cap[4] = {0, 0, 0, 0};
+    int64_t heavy_key[4] = {-1, -1, -1, -1};   // shape (b0, n, ntb) the sorted order buffer is for
+    int64_t heavy_next[4] = {-1, -1, -1, -1};
+    int heavy_buf = 0;
+    int32_t opt_test_unconverged = 0; // testing: an iteration guard hands its state to compose (OPT_TEST_UNCONVERGED)
+    int32_t opt_test_scramble = 0;    // testing: predecessors overwritten before compose (OPT_TEST_SCRAMBLE_TREE)
+    int32_t opt_test_pool_enomem = 0; // testing: the next pool allocation fails midway (OPT_TEST_POOL_ENOMEM)
+    bool unconverged = false;         // the last rounds stopped at the guard (opt_test_unconverged)
     shadowtopo_stats st{};
 };
 
@@ -2952,8 +3255,11 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
 int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     free_batches(eng);
     const auto dev_alloc = [eng](std::vector<void*>& owner, void** p, size_t bytes) {
-        eng->pool_bytes += bytes;  // default_nb counts what the pools hold, not an estimate
-        return ::dev_alloc(owner, p, bytes);
+        // default_nb counts what the pools hold, not an estimate: only allocations that
+        // succeeded (a failed one is not held, and ENOMEM's retry sizes from free + held)
+        const int rc = ::dev_alloc(owner, p, bytes);
+        if (rc == SHADOWTOPO_OK) eng->pool_bytes += bytes;
+        return rc;
     };
     const int32_t pvp = pool_vp(eng);
     const size_t VK = (size_t)pvp * KL;
@@ -2961,13 +3267,18 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     P.vk = (int64_t)VK;
     P.Vp = pvp;
     int rc;
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.D, VK * nb * sizeof(double))) ||
-        (rc = dev_alloc(eng->batch_allocs, (void**)&P.Q, VK * nb * sizeof(Rec))) ||
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.D, VK * nb * sizeof(double)))) return rc;
+    if (eng->opt_test_pool_enomem) {  // testing: HBM taken by someone else after the budget query
+        eng->opt_test_pool_enomem = 0;
+        return fail(SHADOWTOPO_ENOMEM, "injected pool allocation failure (OPT_TEST_POOL_ENOMEM)");
+    }
+    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.Q, VK * nb * sizeof(Rec))) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.act, (size_t)pvp * 2 * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.srcv, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
-        (rc = dev_alloc(eng->batch_allocs, (void**)&P.mask, sizeof(unsigned long long) * nb)))
+        (rc = dev_alloc(eng->batch_allocs, (void**)&P.err, sizeof(unsigned long long) * (nb + 1))))
         return rc;
+    P.mask = P.err + 1;
     // BDU (the lexicographic key) only for the kernels that fold into a recorded state, D32
     // only for the f32-filtered ones: the FULL CSR rounds keep 24 bytes per (vertex, source)
     if (state_bdu(eng) && (rc = dev_alloc(eng->batch_allocs, (void**)&P.BDU, VK * nb * sizeof(double)))) return rc;
@@ -3051,22 +3362,18 @@ int32_t default_nb(shadowtopo_engine* eng, int32_t rows) {
     return std::min(nb, need);
 }
 
-int ensure_self(shadowtopo_engine* eng, hipStream_t s) {
-    if (eng->self_ready) return SHADOWTOPO_OK;
-    if (eng->A > 0) {
-        // timed on its own (one stream synchronisation per attached set): the shim reports it
-        // as the reference's self-path seconds (topology.c:1277-1280)
-        HIP_TRY(hipStreamSynchronize(s));
-        const auto t0 = std::chrono::steady_clock::now();
-        hipLaunchKernelGGL(k_self, dim3((eng->A + 3) / 4), dim3(256), 0, s, eng->g, eng->d_attached, eng->A,
-                           eng->d_self_lat, eng->d_self_rel, eng->d_self_hops, eng->d_self_kind);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipStreamSynchronize(s));
-        eng->st.self_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        eng->st.self_paths += eng->A;
-    }
-    eng->self_ready = true;
-    return SHADOWTOPO_OK;
+// the self rule (k_self) of attached rows [i0, i1) into l / r / h / k, on stream s, with no
+// host synchronisation
+hipError_t launch_self(const shadowtopo_engine* eng, const GraphDev& g, int32_t i0, int32_t i1, double* l, double* r,
+                       uint32_t* h, uint8_t* k, hipStream_t s) {
+    if (i1 <= i0) return hipSuccess;
+    const int32_t n = i1 - i0;
+    if (eng->self_blk)
+        hipLaunchKernelGGL(k_self<true>, dim3((uint32_t)n), dim3(256), 0, s, g, eng->d_attached, i0, i1, l, r, h, k);
+    else
+        hipLaunchKernelGGL(k_self<false>, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, g, eng->d_attached, i0, i1,
+                           l, r, h, k);
+    return hipGetLastError();
 }
 
 // the pools of batches b0, b0 + 1, ... as a pool set of their own (one part of the batches)
@@ -3165,16 +3472,53 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                     if (e == hipSuccess) e = hipEventRecord(eng->ev_h0, s);
                     for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) e = hipStreamWaitEvent(eng->aux_stream[k], eng->ev_h0, 0);
                     if (e != hipSuccess) return e;
+                    // heavy-first block order per part (k_heavy_order): this sweep uses order
+                    // buffer `cur` (sorted after the previous sweep of the same shape), the
+                    // blocks record their chunk counts, and the sort for the next sweep writes
+                    // buffer cur ^ 1 (no running sweep reads it)
+                    const int cur = eng->heavy_buf;
+                    HeavyArgs ha{};
+                    bool sort_any = false;
                     auto part = [&](hipStream_t st, int32_t b0, int32_t n, int k) {
                         const Pools P = pools_from(eng->pools, b0);
                         uint32_t* hl = eng->d_hitlog + (size_t)b0 * (size_t)(eng->Vp / TDT) * nchunks;
                         const float* mD = eng->d_minD + (size_t)b0 * nchunks * KL;
                         const int64_t nbl = 8 * (((int64_t)n * ntb + 7) / 8);
+                        const int64_t key = ((int64_t)b0 << 42) | ((int64_t)n << 21) | ntb;
+                        bool heavy = eng->opt_heavy_first && k < 4 && nbl / 8 <= HEAVY_MAX;
+                        if (heavy && eng->heavy_cap[k] < (size_t)nbl) {
+                            for (void* q : {(void*)eng->d_bweight[k], (void*)eng->d_border[k][0], (void*)eng->d_border[k][1]})
+                                if (q) (void)hipFree(q);
+                            eng->d_bweight[k] = nullptr;
+                            eng->d_border[k][0] = eng->d_border[k][1] = nullptr;
+                            eng->heavy_cap[k] = 0;
+                            eng->heavy_key[k] = -1;
+                            if (hipMalloc((void**)&eng->d_bweight[k], sizeof(uint32_t) * nbl) != hipSuccess ||
+                                hipMalloc((void**)&eng->d_border[k][0], sizeof(int32_t) * nbl) != hipSuccess ||
+                                hipMalloc((void**)&eng->d_border[k][1], sizeof(int32_t) * nbl) != hipSuccess ||
+                                hipMemsetAsync(eng->d_bweight[k], 0, sizeof(uint32_t) * nbl, st) != hipSuccess) {
+                                (void)hipGetLastError();
+                                heavy = false;
+                            } else {
+                                eng->heavy_cap[k] = (size_t)nbl;
+                            }
+                        }
+                        const int32_t* ord = heavy && eng->heavy_key[k] == key ? eng->d_border[k][cur] : nullptr;
                         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1>), dim3((uint32_t)nbl), dim3(256), 0, st,
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
-                                           eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr);
+                                           eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr, ord,
+                                           heavy ? eng->d_bweight[k] : nullptr);
+                        if (heavy) {
+                            ha.w[k] = eng->d_bweight[k];
+                            ha.o[k] = eng->d_border[k][cur ^ 1];
+                            ha.slots[k] = (int32_t)(nbl / 8);
+                            eng->heavy_next[k] = key;
+                            sort_any = true;
+                        } else {
+                            eng->heavy_next[k] = -1;
+                        }
                         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 2>), dim3((uint32_t)nbl), dim3(256), 0, st,
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
@@ -3191,6 +3535,13 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                     for (int k = 0; k < parts; ++k) {
                         const int32_t b0 = bound(k), b1 = bound(k + 1);
                         part(k == 0 ? s : eng->aux_stream[k - 1], b0, b1 - b0, k);
+                    }
+                    if (sort_any && e == hipSuccess) {
+                        // on part 0's stream behind its work (the other parts may still run:
+                        // their weights are then this sweep's or the last one's, either is an order)
+                        hipLaunchKernelGGL(k_heavy_order, dim3(8, (uint32_t)std::min(parts, 4)), dim3(1024), 0, s, ha);
+                        for (int k = 0; k < 4; ++k) eng->heavy_key[k] = k < parts ? eng->heavy_next[k] : -1;
+                        eng->heavy_buf = cur ^ 1;
                     }
                     for (int k = 0; k < parts - 1 && e == hipSuccess; ++k) {
                         e = hipEventRecord(eng->ev_hp[k], eng->aux_stream[k]);
@@ -3311,7 +3662,10 @@ int run_push_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         int rc;
         if ((rc = compact(par0))) return rc;
         for (int64_t r = 0;; ++r) {
-            if (r > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "push rounds did not converge in %lld rounds", (long long)max_rounds);
+            if (r > max_rounds) {
+                if (eng->opt_test_unconverged) return (eng->unconverged = true), SHADOWTOPO_OK;
+                return fail(SHADOWTOPO_EINTERNAL, "push rounds did not converge in %lld rounds", (long long)max_rounds);
+            }
             const int32_t par = (int32_t)((par0 + r) & 1);
             eng->h_wlpre[0] = 0;
             for (int32_t b = 0; b < nbg; ++b) eng->h_wlpre[b + 1] = eng->h_wlpre[b] + eng->h_wlcnt[b];
@@ -3457,8 +3811,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         hipLaunchKernelGGL(k_scan_wl, dim3(1), dim3(256), 0, s, eng->d_wlcnt, nbg, eng->d_wlpre, eng->d_tlog, 0);
         HIP_TRY(hipGetLastError());
         for (int64_t r0 = 0;; r0 += DEV_K) {
-            if (r0 > max_rounds)
+            if (r0 > max_rounds) {
+                if (eng->opt_test_unconverged) return (eng->unconverged = true), SHADOWTOPO_OK;
                 return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds", (long long)max_rounds);
+            }
             for (int64_t round = r0; round < r0 + DEV_K; ++round) {
                 int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;  // written, not read back
                 if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0)], s));
@@ -3615,8 +3971,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
         return hipGetLastError();
     };
     for (int64_t round = 0;; ++round) {
-        if (round > max_rounds) return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds",
-                                            (long long)max_rounds);
+        if (round > max_rounds) {
+            if (eng->opt_test_unconverged) return (eng->unconverged = true), SHADOWTOPO_OK;
+            return fail(SHADOWTOPO_EINTERNAL, "relaxation did not converge in %lld rounds", (long long)max_rounds);
+        }
         const bool spec = round < spec_rounds;                   // no read-back after this round
         const bool blind = round >= 1 && round <= spec_rounds;  // decided without the last counts
         // chained rounds 1 .. spec_rounds: enqueued with round 0 (the decisions below are the
@@ -4132,8 +4490,10 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     eng->prune_allocs.clear();
     eng->h_view_of.clear();
     eng->d_att_view = nullptr;
+    eng->view_gen++;
     if (peeled == 0) {  // nothing to drop: relax over g (and do not peel again for this set)
         eng->gp = eng->g;
+        eng->gp_arcs = eng->n_arcs;
         eng->prune_ready = true;
         return SHADOWTOPO_OK;
     }
@@ -4223,7 +4583,9 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     gp.loop_eid = d_loop;
     gp.inc_ptr = nullptr;  // the self rule and the replay run on g, in the original ids
     gp.inc_eid = nullptr;
+    gp.inc_lat = nullptr;
     eng->gp = gp;
+    eng->gp_arcs = (int64_t)na - CSR_PAD;
     eng->h_view_of = std::move(nid);
     eng->d_att_view = d_att;
     eng->prune_ready = true;
@@ -4241,9 +4603,62 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const int32_t A = eng->A;
     const bool complete = (eng->flags & SHADOWTOPO_F_COMPLETE) != 0;
     int rc;
-    if ((rc = ensure_self(eng, s))) return rc;
+    // the self rule of these rows' diagonal pairs (rule 2 of the pair dispatch), inside every
+    // computation: the reference computes the self path per query (topology.c:1545-1653),
+    // so the matrix build includes it; timed with events once per attached set (the shim
+    // reports it as the reference's selfPathTotalTime, topology.c:1608-1617) or with OPT_TIMING
+    bool self_pending = false;
+    if (!complete) {
+        self_pending = eng->opt_timing || !eng->self_timed;
+        if (self_pending) HIP_TRY(hipEventRecord(eng->ev_self[0], s));
+        HIP_TRY(launch_self(eng, eng->g, row_begin, row_end, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
+                            eng->d_self_kind, s));
+        if (self_pending) HIP_TRY(hipEventRecord(eng->ev_self[1], s));
+        eng->st.self_paths += row_end - row_begin;
+    }
     if ((rc = ensure_pruned(eng, s))) return rc;
     eng->rg = eng->prune_ready ? &eng->gp : &eng->g;  // back to g for sssp (shadowtopo_sssp)
+    if (!eng->walk_ready && !complete) {
+        // the targets whose pairs k_walk re-folds: vertex loss present (a factor != 1), or all
+        // of them in a multigraph (lat from the get_eid edges)
+        std::vector<int32_t> wl;
+        for (int32_t i = 0; i < A; ++i)
+            if (eng->multigraph || eng->h_vfac[(size_t)eng->h_attached[i]] != 1.0) wl.push_back(i);
+        eng->n_walk = (int32_t)wl.size();
+        if (!wl.empty()) {
+            if (eng->walk_cap < wl.size()) {
+                if (eng->d_walk) (void)hipFree(eng->d_walk);
+                eng->d_walk = nullptr;
+                eng->walk_cap = 0;
+                HIP_TRY(hipMalloc((void**)&eng->d_walk, wl.size() * sizeof(int32_t)));
+                eng->walk_cap = wl.size();
+            }
+            HIP_TRY(hipMemcpyAsync(eng->d_walk, wl.data(), wl.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));  // wl is a local
+        }
+        eng->walk_ready = true;
+    }
+    eng->st.walk_targets = eng->n_walk;
+    if (eng->n_walk > 0 && (eng->arcinfo_of != eng->rg->in_src || eng->arcinfo_gen != eng->view_gen)) {
+        // the walks' per-arc table, for the graph the rounds run on (rebuilt with the view)
+        const int64_t na = eng->rg == &eng->g ? eng->n_arcs : eng->gp_arcs;
+        if (eng->arcinfo_cap < (size_t)std::max<int64_t>(na, 1)) {
+            if (eng->d_arcinfo) (void)hipFree(eng->d_arcinfo);
+    for (int k = 0; k < 4; ++k)
+        for (void* q : {(void*)eng->d_bweight[k], (void*)eng->d_border[k][0], (void*)eng->d_border[k][1]})
+            if (q) (void)hipFree(q);
+            eng->d_arcinfo = nullptr;
+            eng->arcinfo_cap = 0;
+            HIP_TRY(hipMalloc((void**)&eng->d_arcinfo, sizeof(ArcInfo) * (size_t)std::max<int64_t>(na, 1)));
+            eng->arcinfo_cap = (size_t)std::max<int64_t>(na, 1);
+        }
+        if (na > 0)
+            hipLaunchKernelGGL(k_arcinfo, dim3((uint32_t)std::min<int64_t>((na + 255) / 256, 8192)), dim3(256), 0, s,
+                               eng->rg->in_src, eng->rg->in_eid, eng->rg->in_r, na, eng->d_arcinfo);
+        HIP_TRY(hipGetLastError());
+        eng->arcinfo_of = eng->rg->in_src;
+        eng->arcinfo_gen = eng->view_gen;
+    }
     // host destinations: rows are composed into device staging and copied out per group;
     // into pinned (page-locked) host memory -- shadowtopo_host_alloc, as the topology shim
     // allocates its matrix -- the copy of group g runs on the copy stream behind group
@@ -4272,6 +4687,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         (void)hipGetLastError();  // the failed hipMalloc's error, not a launch's
         eng->floor_ok = false;
         eng->floor_checked = true;
+        free_batches(eng);  // what the failed attempt did allocate is free again: held = 0
         nb = default_nb(eng, row_end - row_begin);
         rc = ensure_batches(eng, nb);
     }
@@ -4347,31 +4763,70 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                                hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(eng->pools.row, eng->h_row.data(), sizeof(int32_t) * KL * nbg,
                                hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(eng->pools.mask, 0, sizeof(unsigned long long) * nbg, s));
+        HIP_TRY(hipMemsetAsync(eng->pools.err, 0, sizeof(unsigned long long) * (nbg + 1), s));
         if (!complete) {
+            eng->unconverged = false;
             if ((rc = run_rounds(eng, nbg, s))) return rc;
+            // testing options: compose the state an iteration guard stopped at (every stream of
+            // the device drained first: the rounds may have left work on the part streams), or
+            // a scrambled tree
+            if (eng->unconverged) HIP_TRY(hipDeviceSynchronize());
+            if (eng->opt_test_scramble) {
+                hipLaunchKernelGGL(k_scramble_tree, dim3(256, nbg), dim3(256), 0, s, *eng->rg, eng->pools,
+                                   eng->opt_test_scramble);
+                HIP_TRY(hipGetLastError());
+            }
         }
         auto t0 = std::chrono::steady_clock::now();
+        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[0], s));
         if (A > 0) {
             hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(COMPOSE_T), 0, s, *eng->rg, eng->pools,
                                d_att_r, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
                                eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
             HIP_TRY(hipGetLastError());
+            if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
+                const dim3 grid((uint32_t)((eng->n_walk + WALK_TPB - 1) / WALK_TPB), nbg);
+                if (eng->multigraph)
+                    hipLaunchKernelGGL(k_walk<true>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo, eng->pools,
+                                       d_att_r, eng->d_walk, eng->n_walk, A, dl, dr, row_base, ls);
+                else
+                    hipLaunchKernelGGL(k_walk<false>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo, eng->pools,
+                                       d_att_r, eng->d_walk, eng->n_walk, A, dl, dr, row_base, ls);
+                HIP_TRY(hipGetLastError());
+            }
         }
-        // collect tie-tainted sources
-        std::vector<unsigned long long> masks(nbg);
-        HIP_TRY(hipMemcpyAsync(masks.data(), eng->pools.mask, sizeof(unsigned long long) * nbg,
+        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[1], s));
+        // collect tie-tainted sources (masks[1 + b]) and the path walks' error word (masks[0])
+        std::vector<unsigned long long> masks((size_t)nbg + 1);
+        HIP_TRY(hipMemcpyAsync(masks.data(), eng->pools.err, sizeof(unsigned long long) * (nbg + 1),
                                hipMemcpyDeviceToHost, s));
         HIP_TRY(round_sync(eng, s));
         eng->st.compose_ms +=
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (eng->opt_timing) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, eng->ev_cmp[0], eng->ev_cmp[1]));
+            eng->st.compose_kernel_ms += ms;
+        }
+        if (self_pending) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, eng->ev_self[0], eng->ev_self[1]));
+            eng->st.self_ms += ms;
+            eng->self_timed = true;
+            self_pending = false;
+        }
+        if (masks[0] || eng->unconverged)
+            return fail(SHADOWTOPO_EINTERNAL,
+                        !masks[0] ? "relaxation stopped at the iteration guard (composed for testing)" :
+                        "a path walk left the predecessor tree (%s): the relaxation state is not a converged "
+                        "shortest-path tree", masks[0] & 1 ? "arc or vertex out of range" : "hop count disagrees");
         std::vector<std::pair<int32_t, int32_t>> jobs;  // (vertex, row)
         for (int32_t b = 0; b < nbg; ++b) {
             for (int j = 0; j < KL; ++j) {
                 const int32_t row = lane_row[(size_t)b * KL + j];
                 if (row < 0) continue;
                 if (complete) continue;
-                if (eng->opt_force_replay || (masks[b] >> j) & 1ull) jobs.emplace_back(eng->h_attached[row], row);
+                if (eng->opt_force_replay || (masks[1 + b] >> j) & 1ull) jobs.emplace_back(eng->h_attached[row], row);
             }
         }
         if (!jobs.empty()) {
@@ -4652,7 +5107,7 @@ void prep_work(int device) {
         if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
         hipFuncAttributes a;
         (void)graph_build::preload();
-        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_self));
+        (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_self<true>));
         g_prep.spare = st;  // read only after the thread is joined
     }
     g_prep.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -4805,6 +5260,7 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     eng->flags = flags;
     eng->multigraph = multigraph;
     eng->n_arcs = gb.n_arcs;
+    eng->self_blk = (directed ? n_edges : 2 * n_edges) >= 128 * (int64_t)V;
     eng->Vp = (V + 63) / 64 * 64;  // dense tiles of 64 destinations, 32-row LDS chunks
     {
         const double VV = (double)V * (double)V;
@@ -4830,11 +5286,13 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     g.in_eid = gb.in_eid;
     g.inc_ptr = gb.inc_ptr;
     g.inc_eid = gb.inc_eid;
+    g.inc_lat = gb.inc_lat;
     g.efrom = gb.efrom;
     g.eto = gb.eto;
     g.elat = gb.elat;
     g.erel = gb.erel;
     g.loop_eid = gb.loop_eid;
+    eng->h_vfac = vfac;
     if ((rc = upload(eng, vfac, &g.vfac))) {
         shadowtopo_destroy(eng);
         return rc;
@@ -4881,6 +5339,8 @@ int shadowtopo_create(int32_t n_vertices, int64_t n_edges, const int32_t* edge_s
     }
     if (hipEventCreate(&eng->ev0) != hipSuccess || hipEventCreate(&eng->ev1) != hipSuccess ||
         hipEventCreate(&eng->evm) != hipSuccess || hipEventCreate(&eng->evm2) != hipSuccess ||
+        hipEventCreate(&eng->ev_self[0]) != hipSuccess || hipEventCreate(&eng->ev_self[1]) != hipSuccess ||
+        hipEventCreate(&eng->ev_cmp[0]) != hipSuccess || hipEventCreate(&eng->ev_cmp[1]) != hipSuccess ||
         hipEventCreateWithFlags(&eng->ev_spin, hipEventDisableTiming) != hipSuccess) {
         shadowtopo_destroy(eng);
         return fail(SHADOWTOPO_EDEVICE, "stream/event create failed");
@@ -4942,6 +5402,11 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->d_self_rel) (void)hipFree(eng->d_self_rel);
     if (eng->d_self_hops) (void)hipFree(eng->d_self_hops);
     if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
+    if (eng->d_walk) (void)hipFree(eng->d_walk);
+    if (eng->d_arcinfo) (void)hipFree(eng->d_arcinfo);
+    for (int k = 0; k < 4; ++k)
+        for (void* q : {(void*)eng->d_bweight[k], (void*)eng->d_border[k][0], (void*)eng->d_border[k][1]})
+            if (q) (void)hipFree(q);
     if (eng->stage) (void)hipFree(eng->stage);
     if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
     if (eng->d_perm) (void)hipFree(eng->d_perm);
@@ -4961,6 +5426,10 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     if (eng->evm) (void)hipEventDestroy(eng->evm);
     if (eng->evm2) (void)hipEventDestroy(eng->evm2);
     if (eng->ev_spin) (void)hipEventDestroy(eng->ev_spin);
+    for (auto e : eng->ev_self)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : eng->ev_cmp)
+        if (e) (void)hipEventDestroy(e);
     if (eng->copy_stream) (void)hipStreamSynchronize(eng->copy_stream);
     for (int k = 0; k < 2; ++k) {
         if (eng->ev_comp[k]) (void)hipEventDestroy(eng->ev_comp[k]);
@@ -4990,27 +5459,34 @@ int shadowtopo_set_attached(shadowtopo_engine* eng, const int32_t* attached, int
         return SHADOWTOPO_OK;
     eng->prune_ready = false;
     eng->rg = nullptr;
-    if (eng->d_attached) (void)hipFree(eng->d_attached);
-    if (eng->d_self_lat) (void)hipFree(eng->d_self_lat);
-    if (eng->d_self_rel) (void)hipFree(eng->d_self_rel);
-    if (eng->d_self_hops) (void)hipFree(eng->d_self_hops);
-    if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
-    eng->d_attached = nullptr;
-    eng->d_self_lat = eng->d_self_rel = nullptr;
-    eng->d_self_hops = nullptr;
-    eng->d_self_kind = nullptr;
+    const size_t n = (size_t)std::max(count, 1);
+    // a new list of a size the buffers already hold reuses them (a hipFree waits for the
+    // whole device; a new attach epoch pays for the rebuild of what depends on the list)
+    if (n > eng->att_cap) {
+        if (eng->d_attached) (void)hipFree(eng->d_attached);
+        if (eng->d_self_lat) (void)hipFree(eng->d_self_lat);
+        if (eng->d_self_rel) (void)hipFree(eng->d_self_rel);
+        if (eng->d_self_hops) (void)hipFree(eng->d_self_hops);
+        if (eng->d_self_kind) (void)hipFree(eng->d_self_kind);
+        eng->d_attached = nullptr;
+        eng->d_self_lat = eng->d_self_rel = nullptr;
+        eng->d_self_hops = nullptr;
+        eng->d_self_kind = nullptr;
+        eng->att_cap = 0;
+        HIP_TRY(hipMalloc((void**)&eng->d_attached, n * sizeof(int32_t)));
+        HIP_TRY(hipMalloc((void**)&eng->d_self_lat, n * sizeof(double)));
+        HIP_TRY(hipMalloc((void**)&eng->d_self_rel, n * sizeof(double)));
+        HIP_TRY(hipMalloc((void**)&eng->d_self_hops, n * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&eng->d_self_kind, n));
+        eng->att_cap = n;
+    }
     eng->h_attached.assign(attached, attached + count);
     eng->key_ready = false;
     eng->A = count;
-    const size_t n = (size_t)std::max(count, 1);
-    HIP_TRY(hipMalloc((void**)&eng->d_attached, n * sizeof(int32_t)));
-    HIP_TRY(hipMalloc((void**)&eng->d_self_lat, n * sizeof(double)));
-    HIP_TRY(hipMalloc((void**)&eng->d_self_rel, n * sizeof(double)));
-    HIP_TRY(hipMalloc((void**)&eng->d_self_hops, n * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc((void**)&eng->d_self_kind, n));
     if (count > 0)
         HIP_TRY(hipMemcpy(eng->d_attached, attached, sizeof(int32_t) * count, hipMemcpyHostToDevice));
-    eng->self_ready = false;
+    eng->self_timed = false;
+    eng->walk_ready = false;
     eng->st.n_attached = count;
     return SHADOWTOPO_OK;
 }
@@ -5110,6 +5586,20 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_HBM_SHARE:
             if (value < 1 || value > 1000) return fail(SHADOWTOPO_EINVAL, "HBM share must be in [1, 1000] per mille");
             eng->opt_hbm_share = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_HEAVY_FIRST:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "heavy first must be 0 or 1");
+            eng->opt_heavy_first = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_TEST_UNCONVERGED:
+            eng->opt_test_unconverged = value ? 1 : 0;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_TEST_POOL_ENOMEM:
+            eng->opt_test_pool_enomem = value ? 1 : 0;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_TEST_SCRAMBLE_TREE:
+            if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "scramble mode must be 0, 1 or 2");
+            eng->opt_test_scramble = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_DELTA_PERMILLE:
             if (value < 0 || value > 1000) return fail(SHADOWTOPO_EINVAL, "delta per mille must be in [0, 1000]");
@@ -5528,8 +6018,7 @@ int shadowtopo_self_rule_paths(shadowtopo_engine* eng, double* lat, double* rel,
     uint32_t* dh = (uint32_t*)(dr + A);
     uint8_t* dk = (uint8_t*)(dh + A);
     hipStream_t s = eng->own_stream;
-    hipLaunchKernelGGL(k_self, dim3((A + 3) / 4), dim3(256), 0, s, g, eng->d_attached, A, dl, dr, dh, dk);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_self(eng, g, 0, A, dl, dr, dh, dk, s);
     if (e == hipSuccess) e = hipMemcpyAsync(lat, dl, sizeof(double) * A, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(rel, dr, sizeof(double) * A, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(kind, dk, A, hipMemcpyDeviceToHost, s);

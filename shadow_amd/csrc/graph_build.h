@@ -27,6 +27,7 @@ struct Built {
     int32_t* out_dst = nullptr;
     int64_t* inc_ptr = nullptr;  // [V+1] igraph_incident(OUT) order
     int32_t* inc_eid = nullptr;
+    double* inc_lat = nullptr;   // [inc] latency of each incidence entry (the self rule's contiguous scan)
     int32_t* efrom = nullptr;    // igraph storage: undirected from = max, to = min
     int32_t* eto = nullptr;
     double* elat = nullptr;

@@ -187,11 +187,14 @@ __global__ void k_inc_count(int32_t V, const int64_t* __restrict__ os, const int
 
 __global__ void k_inc_fill(int64_t E, const int32_t* __restrict__ row, const int32_t* __restrict__ eid,
                            const int64_t* __restrict__ seg, const int64_t* __restrict__ os,
-                           const int64_t* __restrict__ inc_ptr, int after_out, int32_t* inc_eid) {
+                           const int64_t* __restrict__ inc_ptr, int after_out, int32_t* inc_eid,
+                           const double* __restrict__ elat, double* inc_lat) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < E; x += (int64_t)gridDim.x * blockDim.x) {
         const int32_t v = row[x];
         const int64_t base = inc_ptr[v] + (after_out ? os[v + 1] - os[v] : 0);
-        inc_eid[base + (x - seg[v])] = eid[x];
+        const int32_t e = eid[x];
+        inc_eid[base + (x - seg[v])] = e;
+        inc_lat[base + (x - seg[v])] = elat[e];
     }
 }
 
@@ -413,11 +416,13 @@ hipError_t build(int32_t V, int64_t E, int64_t n_loops, bool directed, int pad, 
     GB_TRY(exclusive_sum(sc, cnt, g.inc_ptr, (int64_t)V + 1, s));
     const int64_t ninc = directed ? E : 2 * E;
     GB_TRY(dalloc(allocs, &g.inc_eid, ninc));
+    GB_TRY(dalloc(allocs, &g.inc_lat, ninc));
     if (E > 0) {
-        hipLaunchKernelGGL(k_inc_fill, dim3(grid_of(E)), dim3(256), 0, s, E, orow, oval, os, os, g.inc_ptr, 0, g.inc_eid);
+        hipLaunchKernelGGL(k_inc_fill, dim3(grid_of(E)), dim3(256), 0, s, E, orow, oval, os, os, g.inc_ptr, 0, g.inc_eid,
+                           g.elat, g.inc_lat);
         if (!directed)
             hipLaunchKernelGGL(k_inc_fill, dim3(grid_of(E)), dim3(256), 0, s, E, irow, ival, is, os, g.inc_ptr, 1,
-                               g.inc_eid);
+                               g.inc_eid, g.elat, g.inc_lat);
     }
     stamp("incidence");
     int32_t* d_ok = nullptr;

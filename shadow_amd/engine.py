@@ -54,6 +54,12 @@ OPT_CHAIN_PARTS = 23  # the read-back-free delta rounds on each sweep part's str
 OPT_SWEEP_PARTS = 22  # pruned dense sweep: batches in 1 .. 4 parts (default 2) on their own streams
 OPT_DENSE_SPEC = 21  # dense: leading rounds enqueued without a host read-back (0..4, default 2)
 OPT_DELTA_LIVE = 19  # dense delta rounds over live-chunk lists: 2 when sparse (default), 1 always, 0 never
+OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order
+# testing: the failure paths a convergence bug or a full device would take (SHADOWTOPO_EINTERNAL /
+# the re-sized pool retry instead of a fault)
+OPT_TEST_UNCONVERGED = 24  # compose the state the iteration guard stopped at, then fail
+OPT_TEST_SCRAMBLE_TREE = 25  # 1 / 2: predecessors overwritten before compose (out of range / not a tree)
+OPT_TEST_POOL_ENOMEM = 26  # the next batch-pool allocation fails midway (ENOMEM retry)
 CSR_FULL = 1  # pull: recompute every active vertex over all in-arcs (k_relax / k_relax_wl, default)
 CSR_PUSH = 2  # push: distance pushes with a u64 atomicMin, then a predecessor pass and fold rounds (undirected)
 
@@ -63,6 +69,7 @@ ENGINE_SYMBOLS = (
     "shadowtopo_set_attached", "shadowtopo_set_option", "shadowtopo_compute_rows", "shadowtopo_sssp",
     "shadowtopo_get_stats", "shadowtopo_reset_stats", "shadowtopo_is_complete", "shadowtopo_get_eid",
     "shadowtopo_host_alloc", "shadowtopo_host_free", "shadowtopo_self_rule_paths",
+    "shadowtopo_packed_capacity", "shadowtopo_pack_rows", "shadowtopo_unpack_rows",
 )
 
 
@@ -93,6 +100,7 @@ class Stats(ctypes.Structure):
         ("push_ms", ctypes.c_double), ("pred_ms", ctypes.c_double), ("fold_ms", ctypes.c_double),
         ("push_rounds", ctypes.c_int64), ("fold_rounds", ctypes.c_int64),
         ("packed_pairs", ctypes.c_int64), ("packed_explicit", ctypes.c_int64),
+        ("compose_kernel_ms", ctypes.c_double), ("walk_targets", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -87,8 +87,16 @@ class EngineRowCodec:
     ranks moves ~11 MB per rank instead of 160 MB.  Rows are the packed_views of a chunk."""
 
     def __init__(self, eng, stream_of=None):
+        """`stream_of()` -> the hipStream_t the codec's kernels run on.  The default is torch's
+        current stream on the engine's device: the payload all-gather and the row buffers are
+        ordered on that stream, so packing and unpacking must be too (the engine's own stream
+        would let unpack read a payload before the collective has written it)."""
         self.eng = eng
-        self.stream_of = stream_of or (lambda: None)
+        if stream_of is None:
+            import torch
+            dev = torch.device("cuda", eng.device)
+            stream_of = lambda: torch.cuda.current_stream(dev).cuda_stream  # noqa: E731
+        self.stream_of = stream_of
 
     def capacity(self, rows: int, A: int) -> int:
         return self.eng.packed_capacity(rows, A)
@@ -127,7 +135,9 @@ class RowExchange:
         self.exchanged_bytes = 0  # payload bytes one rank contributed over the steps (codec)
         if self.codec is not None:
             self.payloads = [torch.empty(codec.capacity(n, A), dtype=torch.uint8, device=device) for _, n in self.bounds]
-            self.gpay = [torch.empty(world * p.numel(), dtype=torch.uint8, device=device) for p in self.payloads]
+            # the gathered payloads are sized from the agreed payload size (grown on demand):
+            # a packed C2 chunk is ~1/15 of its worst-case capacity
+            self.gpay = [torch.empty(0, dtype=torch.uint8, device=device) for _ in self.payloads]
             self.size_t = torch.zeros(1, dtype=torch.int64, device=device)
             self.sizes = torch.zeros(world, dtype=torch.int64, device=device)
 
@@ -155,6 +165,9 @@ class RowExchange:
         self.size_t.fill_(nbytes)
         self.dist.all_gather_into_tensor(self.sizes, self.size_t)
         m = max(256, int(self.sizes.max().item()))  # every rank's slot in the gathered payloads
+        if self.gpay[c].numel() < self.world * m:
+            import torch
+            self.gpay[c] = torch.empty(self.world * m, dtype=torch.uint8, device=self.payloads[c].device)
         self.exchanged_bytes += m
         self.dist.all_gather_into_tensor(self.gpay[c][:self.world * m], self.payloads[c][:m])
         parts = unpack_gathered(self.gathered[c], self.world, n, self.A)

@@ -187,6 +187,18 @@ def chung_lu(V=1_000_000, mean_degree=4.0, gamma=2.5, A=50_000, seeds=(7, 8)):
                    gamma=gamma)
 
 
+def with_vertex_loss(g: SynthGraph, frac=0.3, hi=0.02, seed=9) -> SynthGraph:
+    """The same graph with a vertex `packetloss` attribute on a `frac` share of the vertices,
+    U[0, hi] (seed 9); the rest leave it absent (NaN).  Targets with vertex loss take the
+    reference's full path fold (topology.c:1429-1462), the C4 vertex-loss variant ("C4L")."""
+    import copy
+    rng = np.random.default_rng(seed)
+    out = copy.copy(g)
+    out.vertex_packetloss = np.where(rng.random(g.n) < frac, rng.uniform(0.0, hi, g.n), np.nan)
+    out.name = g.name + "+vloss"
+    return out
+
+
 def integer_grid(rows=20, cols=20, seed=11, max_lat=3, A=None):
     """Tie-stress: grid with small integer latencies, so many vertices have several
     shortest-path predecessors at identical distance (heap-order ties)."""

@@ -7,7 +7,7 @@ reference's order, topology.c:1429-1499); the north-star tolerance for reliabili
 import numpy as np
 import pytest
 
-from paritylib import assert_bitexact, compare, oracle_for, oracle_matrix
+from paritylib import assert_bitexact, compare, engine_matrix, oracle_for, oracle_matrix
 from shadow_amd import engine as E
 from shadow_amd import synth
 
@@ -683,3 +683,140 @@ def test_chained_part_rounds_delta_kinds(live):
     (the pruned round, then plain ones): both kinds' per-part offsets"""
     g = synth.geometric_complete_ish(V=700, A=260)
     compare(g, layout="dense", sweep_parts=2, dense_spec=3, chain_parts=1, delta_live=live)
+
+
+def _vloss_graph(V=300, seed=31):
+    rng = np.random.default_rng(seed)
+    vl = np.where(rng.random(V) < 0.5, rng.uniform(0, 0.1, V), np.nan)
+    return synth.random_sparse(V=V, avg_deg=4, seed=seed, vloss=vl)
+
+
+@pytest.mark.parametrize("layout", ["csr", "dense"])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_scrambled_tree_reports_an_error(mode, layout):
+    """compose's path walks (targets with vertex loss) on predecessor records that are no
+    longer a tree -- arcs past the range (1), or every vertex's first in-arc (2) -- end in
+    SHADOWTOPO_EINTERNAL, not a device fault; the engine then computes correctly"""
+    g = _vloss_graph()
+    eng = E.Engine.from_synth(g, layout=layout)
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_TEST_SCRAMBLE_TREE, mode)
+    with pytest.raises(E.ShadowTopoError, match="error -5: a path walk left the predecessor tree"):
+        eng.compute_rows()
+    eng.set_option(E.OPT_TEST_SCRAMBLE_TREE, 0)
+    lat, rel, hops, kind = eng.compute_rows()
+    eng.close()
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                       ("reliability", rel, orel)):
+        assert_bitexact(name, x, y)
+
+
+@pytest.mark.parametrize("layout", ["csr", "dense"])
+def test_unconverged_state_composes_without_fault(layout):
+    """the iteration guard tripped after one round (OPT_MAX_ROUNDS 1) with the testing option
+    that composes the state it stopped at: the bounded walks read a non-converged state and
+    the call fails with SHADOWTOPO_EINTERNAL; the same engine then computes correctly"""
+    g = _vloss_graph(V=400, seed=33)
+    eng = E.Engine.from_synth(g, layout=layout)
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_MAX_ROUNDS, 1)
+    eng.set_option(E.OPT_TEST_UNCONVERGED, 1)
+    with pytest.raises(E.ShadowTopoError, match="error -5"):
+        eng.compute_rows()
+    eng.set_option(E.OPT_MAX_ROUNDS, 0)
+    eng.set_option(E.OPT_TEST_UNCONVERGED, 0)
+    lat, rel, hops, kind = eng.compute_rows()
+    eng.close()
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                       ("reliability", rel, orel)):
+        assert_bitexact(name, x, y)
+
+
+def test_long_paths_walk_in_segments():
+    """vertex-loss targets whose paths have more hops than one walk segment (16 arcs): a
+    path graph (every vertex on one chain, hops up to V - 1) with vertex loss everywhere"""
+    V = 90
+    src = np.arange(V - 1, dtype=np.int32)
+    dst = np.arange(1, V, dtype=np.int32)
+    rng = np.random.default_rng(4)
+    g = synth._finish("chain", V, src, dst, rng.uniform(1, 5, V - 1), rng.uniform(0, 0.05, V - 1),
+                      np.arange(0, V, 3, dtype=np.int32))
+    g.vertex_packetloss = rng.uniform(0, 0.05, V)
+    compare(g)
+    _, _, hops, _, _ = engine_matrix(g)
+    assert hops.max() > 48
+
+
+def test_pool_enomem_retry():
+    """a batch-pool allocation that fails after the budget was computed (another engine or
+    process took the HBM: OPT_TEST_POOL_ENOMEM injects it) is retried with pools sized from
+    a fresh free-memory query, and the results are the oracle's"""
+    g = synth.random_sparse(V=400, avg_deg=4, seed=35)
+    eng = E.Engine.from_synth(g)
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_TEST_POOL_ENOMEM, 1)
+    lat, rel, hops, kind = eng.compute_rows()
+    st = eng.stats()
+    eng.close()
+    assert st["pool_allocs"] == 2, st["pool_allocs"]
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                       ("reliability", rel, orel)):
+        assert_bitexact(name, x, y)
+
+
+@pytest.mark.parametrize("layout", ["csr", "dense"])
+def test_alternating_attached_sets(layout):
+    """set_attached with a new list before every computation (bench --fresh-attach): the self
+    rule, source order and relaxation view of each set are rebuilt, and every matrix is the
+    oracle's; the self rule runs inside each computation"""
+    g = synth.random_sparse(V=500, avg_deg=5, seed=37, A=120) if layout == "csr" else \
+        synth.geometric_complete_ish(V=700, A=120)
+    rng = np.random.default_rng(5)
+    other = np.sort(rng.choice(g.n, size=len(g.attached), replace=False)).astype(np.int32)
+    eng = E.Engine.from_synth(g, layout=layout)
+    for k, att in enumerate([g.attached, other, g.attached, other]):
+        eng.set_attached(att)
+        lat, rel, hops, kind = eng.compute_rows()
+        g.attached = att
+        olat, orel, ohops, okind, og = oracle_matrix(g)
+        og.close()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"set {k} {name}", x, y)
+    st = eng.stats()
+    eng.close()
+    assert st["self_paths"] == 4 * len(other)
+
+
+@pytest.mark.parametrize("parts", [2, 3, 4])
+@pytest.mark.parametrize("case", ["geometric", "ties"])
+def test_heavy_first_sweep_order(case, parts):
+    """OPT_HEAVY_FIRST: each part's chunk-loop blocks in the order of the chunk counts the
+    previous sweep of the same shape recorded (k_heavy_order, ping-pong order buffers): the
+    first computation runs in grid order, the next ones heavy-first, every one the oracle's
+    matrices bit for bit, and the same as with the order off; a new attached set (another
+    shape) falls back to grid order"""
+    g = synth.geometric_complete_ish(V=900, A=330) if case == "geometric" else synth.integer_grid(rows=14, cols=15, seed=6)
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    eng = E.Engine.from_synth(g, layout="dense")
+    eng.set_option(E.OPT_SWEEP_PARTS, parts)
+    eng.set_attached(g.attached)
+    for step in range(4):
+        eng.set_option(E.OPT_HEAVY_FIRST, 0 if step == 2 else 1)
+        lat, rel, hops, kind = eng.compute_rows()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"step {step} {name}", x, y)
+    sub = g.attached[: len(g.attached) // 2]
+    eng.set_attached(sub)
+    lat, rel, hops, kind = eng.compute_rows()
+    eng.close()
+    assert_bitexact("new set latency", lat, olat[: len(sub), : len(sub)])
+    assert_bitexact("new set hops", hops, ohops[: len(sub), : len(sub)])

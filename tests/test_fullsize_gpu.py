@@ -4,8 +4,9 @@ The engine computes the bench's own workloads at the real graph size.  The north
 matrix (C4: all 10^4 x 10^4 attached pairs) and the whole C3 matrix (7000 x 7000) are
 compared with the CPU oracle bit for bit, every pair (the oracle over the box's CPU share:
 the C4 matrix is ~25 s of heap-exact Dijkstra on 16 threads), and so is the whole C2 matrix
-(1000 x 1000, the headline workload); C5 (all 50 000 rows in one call, the
-bench's batch groups) with two rows of every group and the last ten.  Every computed row is
+(1000 x 1000, the headline workload), and the north-star matrix with vertex loss on 30 % of
+the vertices (C4L); C5 (all 50 000 rows in one call, the bench's batch groups) with 64 rows
+of every group and the last 64.  Every computed row is
 also checked for size-independent properties: the reference's pair kinds, hop/latency
 consistency, and d(s, t) <= w(s, t) wherever the arc exists (a shortest path is never
 longer than the edge); C5's whole matrix also for d(s, t) = d(t, s) to rounding.
@@ -131,6 +132,17 @@ def test_c4_north_star_whole_matrix_vs_oracle():
     _run(g, 0, A, sample=[], block=(0, A))
 
 
+def test_c4_vertex_loss_whole_matrix_vs_oracle():
+    """The north-star workload with vertex loss on 30 % of the vertices (U[0, 0.02], the
+    bench's C4L variant): every pair whose target carries loss takes the reference's full
+    path fold (topology.c:1429-1462, compose's bounded path walk); all 10^4 x 10^4 pairs bit
+    for bit against the oracle"""
+    g = synth.with_vertex_loss(synth.barabasi_albert(V=100_000, A=10_000))
+    A = len(g.attached)
+    assert 0.25 < np.mean(~np.isnan(g.vertex_packetloss[g.attached])) < 0.35
+    _run(g, 0, A, sample=[], block=(0, A))
+
+
 def _oracle_rows_check(g, rows, lat, rel, hops, kind):
     """the oracle's rows `rows` (one OpenMP call over the list) against the engine's rows,
     given as host arrays whose row q is matrix row rows[q]"""
@@ -197,8 +209,8 @@ def test_c5_whole_matrix_on_device():
     (batch groups sized by HBM, the pools reused across them, grids past 2^24 blocks going
     2-D), the 50 GB of rows left on the device.  Every row is checked there for the
     size-independent properties (kinds, hop / latency / reliability ranges, d(s, t) = d(t, s)
-    to rounding in this undirected graph, d(s, t) <= w(s, t) over every attached arc), and two
-    rows of every group plus the last ten rows against the oracle bit for bit."""
+    to rounding in this undirected graph, d(s, t) <= w(s, t) over every attached arc), and 64
+    rows of every group plus the last 64 rows against the oracle bit for bit."""
     torch = pytest.importorskip("torch")
     g = synth.chung_lu(V=1_000_000, A=50_000)
     A = len(g.attached)
@@ -239,13 +251,16 @@ def test_c5_whole_matrix_on_device():
     w = torch.as_tensor(g.latency[keep], device=dev)
     for x, y in ((ia, ib), (ib, ia)):
         assert bool(((kind[x, y] != KIND_DIJKSTRA) | (lat[x, y] <= w)).all())
-    # the oracle: two rows of every batch group's row range, and the last ten rows
+    # the oracle: 64 rows spread over every batch group's row range (a batch's worth per
+    # group; which rows share a batch follows the engine's locality order), and the last 64
+    # rows, the short last batch's range (~450 rows, ~20 s of oracle over 16 threads)
     G = nb * 64
     rows = []
     for r0 in range(0, A, G):
         r1 = min(A, r0 + G)
-        rows += [r0 + (r1 - r0) // 3, r0 + 2 * (r1 - r0) // 3]
-    rows = np.array(sorted(set(rows + list(range(A - 10, A)))), np.int32)
+        rows += list(np.linspace(r0, r1 - 1, 64).round().astype(int))
+    rows = np.array(sorted(set(rows + list(range(A - 64, A)))), np.int32)
+    assert len(rows) >= 64 * st["groups"]
     idx = torch.as_tensor(rows.astype(np.int64), device=dev)
     _oracle_rows_check(g, rows, lat[idx].cpu().numpy(), rel[idx].cpu().numpy(),
                        hops[idx].cpu().numpy().astype(np.uint32), kind[idx].cpu().numpy())

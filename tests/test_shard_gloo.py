@@ -242,6 +242,13 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False):
         ok &= 0 < run["allgather_bytes"] <= sum(p.numel() for p in run["exchange"].packs) * world * 2
     else:
         ok &= run["allgather_bytes"] == sum(p.numel() for p in run["exchange"].packs) * world
+    # the N-rank fields the bench line carries (sharded_report): each rank's relax time and
+    # rows, the exchange alone and its bytes, the same on every rank
+    rep = bench.sharded_report(dist, world, run, 3, relax_ms_per_step=1.0 + rank, rows=run["exchange"].rows)
+    ok &= rep["per_rank_relax_ms"] == [1.0 + r for r in range(world)]
+    ok &= sum(rep["per_rank_rows"]) == A and rep["per_rank_rows"][rank] == run["exchange"].rows
+    ok &= rep["step_includes_exchange"] and rep["exchange_ms"] > 0
+    ok &= rep["exchange_ms"] == run["allgather_s"] / 3 * 1e3 and rep["allgather_bytes"] == run["allgather_bytes"]
     # the reported time is the max over ranks: every rank holds the same number
     t = torch.tensor([run["elapsed_s"]], dtype=torch.float64)
     tl = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
