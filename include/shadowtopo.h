@@ -135,6 +135,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_HEAVY_FIRST 27       /* pruned dense sweep in parts: 1 (default) = each part's chunk-loop blocks
                                               in decreasing order of the chunks they staged in the previous sweep of
                                               the same shape (per XCD), 0 = grid order. Results are identical. */
+#define SHADOWTOPO_OPT_WALK_TPW 28          /* path walks (vertex loss, multigraphs): k_walk takes 1 target per wave with one
+                                              walk per lane (1, default) or 2 targets per wave, two walks per lane in
+                                              lockstep (2). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
  * instead of faulting the device */
 #define SHADOWTOPO_OPT_TEST_UNCONVERGED 24  /* 1 = when the iteration guard (OPT_MAX_ROUNDS) trips, compose the state
@@ -221,6 +224,8 @@ typedef struct shadowtopo_stats {
     int64_t packed_explicit;
     double compose_kernel_ms; /* OPT_TIMING: HIP-event time of the pair compose (k_compose + k_walk) */
     int64_t walk_targets;    /* attached targets whose pairs take the full path fold (vertex loss, multigraphs) */
+    double attach_prep_ms;   /* host wall time in compute calls of the work a new attached set needs first: the
+                                relaxation view, the walk list and arc table, the pools, the source order */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -2537,91 +2537,6 @@ __global__ __launch_bounds__(256) void k_arcinfo(const int32_t* __restrict__ in_
     }
 }
 
-// Two walks in lockstep.  A step is two dependent loads: the record's predecessor arc, then
-// the arc's {tail, edge, factor} (ArcInfo); the factors of a segment's arcs go to LDS scratch
-// (sc: slot k of chain c at sc[(c * WALK_SEG + k) * stride], a double, a_{k0+1+k} in slot k)
-// and the fold reads them forwards.
-template <bool MG>
-__device__ uint32_t walk_pair(const GraphDev& g, const ArcInfo* __restrict__ ai, const BatchDev& B, WalkChain* w,
-                              double* sc, int32_t* se, int stride) {
-    const int64_t na = g.in_ptr[g.V];
-    uint32_t err = 0;
-    uint32_t hmax = 0;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        if (w[c].on && (w[c].h == 0 || w[c].h > (uint32_t)g.V)) {
-            err |= 2u;
-            w[c].on = false;
-        }
-        if (w[c].on) {
-            w[c].lat = 0.0;
-            w[c].rel = g.vfac[w[c].s] * g.vfac[w[c].t];
-            hmax = max(hmax, w[c].h);
-        }
-    }
-    for (uint32_t k0 = 0; k0 < hmax; k0 += WALK_SEG) {
-        int32_t x[2];
-        uint32_t i[2];
-        bool a[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            x[c] = w[c].t;
-            i[c] = w[c].h;  // x = x_i: the next step takes a_i and moves to x_{i-1}
-            a[c] = w[c].on && w[c].h > k0;
-        }
-        while (a[0] || a[1]) {
-            int32_t p[2] = {0, 0};
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-                if (a[c]) p[c] = B.Q[(size_t)x[c] * KL + w[c].l].p;
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-                if (a[c] && (p[c] < 0 || (int64_t)p[c] >= na)) {
-                    err |= 1u;
-                    a[c] = w[c].on = false;
-                }
-            u32x4 v[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-                if (a[c]) v[c] = *(const __attribute__((address_space(1))) u32x4*)(ai + p[c]);
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                if (!a[c]) continue;
-                const int32_t u = (int32_t)v[c].x;
-                if (i[c] <= k0 + WALK_SEG) {
-                    const size_t k = (size_t)(c * WALK_SEG + (i[c] - k0 - 1)) * stride;
-                    sc[k] = __longlong_as_double((long long)(((unsigned long long)v[c].w << 32) | v[c].z));
-                    if (MG) se[k] = (int32_t)v[c].y;
-                }
-                if (u < 0 || u >= g.V) {
-                    err |= 1u;
-                    a[c] = w[c].on = false;
-                    continue;
-                }
-                if ((u == w[c].s) != (i[c] == 1)) {
-                    err |= 2u;
-                    a[c] = w[c].on = false;
-                    continue;
-                }
-                x[c] = u;
-                --i[c];
-                a[c] = i[c] > k0;
-            }
-        }
-        // fold this segment's factors forwards
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if (!w[c].on || w[c].h <= k0) continue;
-            const uint32_t n = min(w[c].h, k0 + (uint32_t)WALK_SEG) - k0;
-            for (uint32_t k = 0; k < n; ++k) {
-                w[c].rel *= sc[(size_t)(c * WALK_SEG + k) * stride];
-                if (MG) w[c].lat += g.elat[se[(size_t)(c * WALK_SEG + k) * stride]];
-            }
-        }
-    }
-    return err;
-}
-
 // 512 threads: 8 targets per wave instead of 16 (the per-lane pair values live in registers
 // until the transposes: 132 VGPRs at 16, occupancy 3)
 constexpr int COMPOSE_T = 512;
@@ -2719,61 +2634,128 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
 // carry vertex loss (rel = ((1 * a_s) * a_t) * e_1 * ... -- a_t enters before the edges, so
 // the tree's fold R(t) is not it), and every pair of a multigraph whose lowest-id parallel
 // edge is not the minimum (lat from the get_eid edges).  After k_compose wrote the rows, this
-// overwrites those pairs' rel (and lat) with the walked fold.  Lane = source, as in the
-// relaxation: the 64 walks of a wave all start at one target, and paths from nearby sources
-// into one target share their last hops, so a step's record loads fall in few lines (lane =
-// target instead measured 4.6 ms of walks on C4L against 4.0).  A block takes one batch and
-// WALK_TPB of the walk targets, each of its 4 waves WALK_TPB / 4 of them, two at a time
-// (walk_pair); blocks go batch-major, so few batches' records are read at once.
+// overwrites those pairs' rel (and lat) with the walked fold.
+//  * Lane = source, as in the relaxation: the walks of a wave start at one target and paths
+//    from nearby sources into it share their last hops, so a step's record loads fall in few
+//    lines (lane = target measured 4.6 ms of walks on C4L against 4.0).
+//  * A path x_0 = s .. x_h = t is known backwards only (arc a_i = P(x_i) enters x_i from
+//    x_{i-1}) and the fold runs forwards, so a walk from t stores the factors of a segment
+//    of WALK_SEG arcs in LDS (slot k: a_{k0+1+k}) and folds them in order: h steps when
+//    h <= WALK_SEG, each further segment re-walked from t.  A step is two dependent loads:
+//    the record's predecessor arc, then the arc's {tail, edge, factor} (ArcInfo).
+//  * Each lane runs two walk chains, each its own state machine over the wave's list of
+//    targets (chain c takes targets c, c + 2, ...): a chain that finishes a walk starts its
+//    next target at once, so no lane waits for the wave's longest walk of a target.
+//  * Bounded: every step checks the arc and the vertex it leads to, a walk must arrive at s
+//    after exactly h arcs and never before; a failing walk sets an error bit (1: out of range,
+//    2: hop count disagrees) that compute_rows reports, instead of following garbage through
+//    memory (a non-converged state's records need not form a tree).
 constexpr int WALK_T = 256;
-constexpr int WALK_TPB = 8;
-template <bool MG>
+template <bool MG, int TPW, int NC>
 __global__ __launch_bounds__(WALK_T) void k_walk(GraphDev g, const ArcInfo* __restrict__ ai, Pools pools,
                                                 const int32_t* __restrict__ attached,
                                                 const int32_t* __restrict__ walk_ti, int32_t nw, int32_t A,
                                                 double* out_lat, double* out_rel, int32_t row_base, int32_t ls) {
-    __shared__ double sc[2 * WALK_SEG * WALK_T];
-    __shared__ int32_t se[MG ? 2 * WALK_SEG * WALK_T : 1];
+    __shared__ double sc[NC * WALK_SEG * WALK_T];
+    __shared__ int32_t se[MG ? NC * WALK_SEG * WALK_T : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int32_t sv = B.srcv[lane], row = B.row[lane];
     const bool prefer = (g.flags & SHADOWTOPO_F_PREFER_DIRECT) != 0;
+    const int64_t na = g.in_ptr[g.V];
+    const double fs = sv >= 0 ? g.vfac[sv] : 1.0;
+    const int32_t kb = (blockIdx.x * (WALK_T / 64) + wave) * TPW;
+    const int32_t ke = min(nw, kb + TPW);
     uint32_t err = 0;
-    constexpr int TPW = WALK_TPB / (WALK_T / 64);  // walk targets per wave
-    const int32_t k0 = blockIdx.x * WALK_TPB + wave * TPW;
-    for (int32_t k = k0; k < min(nw, k0 + TPW); k += 2) {
-        WalkChain w[2];
-        int32_t ti[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const bool tk = k + c < min(nw, k0 + TPW);
-            ti[c] = tk ? walk_ti[k + c] : 0;
-            const int32_t t = tk ? attached[ti[c]] : 0;
-            w[c].s = sv;
-            w[c].t = t;
-            w[c].l = lane;
-            w[c].on = false;
-            w[c].h = 0;
-            w[c].lat = 0.0;
-            w[c].rel = 0.0;
-            // a shortest-path pair (the dispatch's rule 3): not the self pair, not a direct
-            // pair of a prefer-direct graph, reached
-            if (tk && sv >= 0 && row >= 0 && sv != t && !(prefer && get_eid(g, sv, t) >= 0)) {
-                const size_t idx = (size_t)t * KL + lane;
-                if (B.D[idx] < dinf()) {
-                    w[c].h = B.Q[idx].h & HMASK;
-                    w[c].on = true;
-                }
+    int32_t j[NC], ti[NC], t[NC], x[NC];
+    uint32_t h[NC], i[NC], k0[NC];
+    double rel[NC], lat[NC];
+    bool act[NC];
+    // chain c's next walkable target of the list (a shortest-path pair of the dispatch's rule
+    // 3: not the self pair, not a direct pair of a prefer-direct graph, reached), set up
+    auto start = [&](int c) {
+        act[c] = false;
+        while (j[c] < ke) {
+            const int32_t k = j[c];
+            j[c] += NC;
+            const int32_t tk = walk_ti[k], tv = attached[tk];
+            if (sv < 0 || row < 0 || sv == tv || (prefer && get_eid(g, sv, tv) >= 0)) continue;
+            const size_t idx = (size_t)tv * KL + lane;
+            if (!(B.D[idx] < dinf())) continue;
+            const uint32_t hh = B.Q[idx].h & HMASK;
+            if (hh == 0 || hh > (uint32_t)g.V) {
+                err |= 2u;
+                continue;
             }
+            ti[c] = tk;
+            t[c] = x[c] = tv;
+            h[c] = i[c] = hh;  // x = x_i: the next step takes a_i and moves to x_{i-1}
+            k0[c] = 0;
+            rel[c] = fs * g.vfac[tv];
+            lat[c] = 0.0;
+            act[c] = true;
+            return;
         }
-        err |= walk_pair<MG>(g, ai, B, w, sc + threadIdx.x, se + (MG ? threadIdx.x : 0), WALK_T);
+    };
+    double* scl = sc + threadIdx.x;
+    int32_t* sel = se + (MG ? threadIdx.x : 0);
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-            if (w[c].on) {
-                const size_t o = ((size_t)(row - row_base) * A + ti[c]) * ls;
-                out_rel[o] = w[c].rel;
-                if (MG) out_lat[o] = (w[c].lat == 0) ? 1.0 : w[c].lat;
+    for (int c = 0; c < NC; ++c) {
+        j[c] = kb + c;
+        start(c);
+    }
+    auto any_act = [&]() {
+        bool r = false;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) r |= act[c];
+        return r;
+    };
+    while (any_act()) {
+        int32_t p[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) p[c] = act[c] ? B.Q[(size_t)x[c] * KL + lane].p : 0;
+        u32x4 v[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const bool okp = p[c] >= 0 && (int64_t)p[c] < na;
+            if (act[c] && !okp) err |= 1u;
+            act[c] = act[c] && okp;
+            if (act[c]) v[c] = *(const __attribute__((address_space(1))) u32x4*)(ai + p[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (!act[c]) continue;
+            const int32_t u = (int32_t)v[c].x;
+            if (i[c] <= k0[c] + WALK_SEG) {
+                const size_t q = (size_t)(c * WALK_SEG + (i[c] - k0[c] - 1)) * WALK_T;
+                scl[q] = __longlong_as_double((long long)(((unsigned long long)v[c].w << 32) | v[c].z));
+                if (MG) sel[q] = (int32_t)v[c].y;
             }
+            if (u < 0 || u >= g.V || (u == sv) != (i[c] == 1)) {
+                err |= (u < 0 || u >= g.V) ? 1u : 2u;
+                start(c);  // this walk is abandoned; compute_rows reports the error
+                continue;
+            }
+            x[c] = u;
+            if (--i[c] > k0[c]) continue;
+            // the segment's arcs a_{k0+1} .. a_{k1} are in slots 0 .. k1 - k0 - 1: fold them forwards
+            const uint32_t n = min(h[c], k0[c] + (uint32_t)WALK_SEG) - k0[c];
+            for (uint32_t k = 0; k < n; ++k) {
+                const size_t q = (size_t)(c * WALK_SEG + k) * WALK_T;
+                rel[c] *= scl[q];
+                if (MG) lat[c] += g.elat[sel[q]];
+            }
+            k0[c] += WALK_SEG;
+            if (k0[c] < h[c]) {  // the next segment: walk again from t
+                x[c] = t[c];
+                i[c] = h[c];
+                continue;
+            }
+            const size_t o = ((size_t)(row - row_base) * A + ti[c]) * ls;
+            out_rel[o] = rel[c];
+            if (MG) out_lat[o] = (lat[c] == 0) ? 1.0 : lat[c];
+            start(c);
+        }
     }
     if (err) atomicOr(pools.err, (unsigned long long)err);
 }
@@ -3047,6 +3029,8 @@ struct shadowtopo_engine {
     int mirrors_rc = 0;
     std::vector<int64_t> h_in_ptr;
     std::vector<int32_t> h_in_src, h_in_eid, h_loop_eid;
+    std::vector<double> h_in_w, h_in_r;  // ensure_pruned's mirrors of the arc weights (sparse graphs)
+    std::vector<float> h_in_w32;
     hipStream_t own_stream = nullptr;
     // attached
     int32_t A = 0;
@@ -3157,6 +3141,7 @@ struct shadowtopo_engine {
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
+    int32_t opt_walk_tpw = 1;         // k_walk shape (OPT_WALK_TPW): 1 target / 1 chain, or 2 / 2
     uint32_t* d_bweight[4] = {nullptr, nullptr, nullptr, nullptr};  // per part: chunk counts per block
     int32_t* d_border[4][2] = {};     // per part: two order buffers (ping-pong across sweeps)
     size_t heavy_cap[4] = {0, 0, 0, 0};
@@ -3245,7 +3230,10 @@ double state_bytes(const shadowtopo_engine* eng) {
 
 int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb);
 int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
-    if (eng->nb_cap >= nb && eng->pools.Vp == pool_vp(eng)) return SHADOWTOPO_OK;
+    // pools with at least the rows the relaxation graph needs are kept (their row stride is
+    // pools.Vp everywhere): a new attached set's pendant-pruned view differs by a few rows,
+    // and reallocating C5's ~140 GB of pools for that cost 1.2 s of a fresh build (r05j)
+    if (eng->nb_cap >= nb && eng->pools.Vp >= pool_vp(eng)) return SHADOWTOPO_OK;
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = ensure_batches_impl(eng, nb);
     eng->st.pool_allocs++;
@@ -3261,7 +3249,9 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
         if (rc == SHADOWTOPO_OK) eng->pool_bytes += bytes;
         return rc;
     };
-    const int32_t pvp = pool_vp(eng);
+    // a pruned view's rows with 1/64 headroom (another attached set's view fits the same pools)
+    const int32_t pvp0 = pool_vp(eng);
+    const int32_t pvp = pvp0 < eng->Vp ? std::min(eng->Vp, (pvp0 + pvp0 / 64 + 63) / 64 * 64) : pvp0;
     const size_t VK = (size_t)pvp * KL;
     Pools& P = eng->pools;
     P.vk = (int64_t)VK;
@@ -4504,17 +4494,28 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     int32_t Vc = 0;
     for (int32_t v = 0; v < V; ++v)
         if (keep[v]) nid[v] = Vc++;
-    // the filtered arrays, row order kept, with the builder's padding arcs at the end
-    std::vector<double> w((size_t)M), r((size_t)M);
-    std::vector<float> w32((size_t)M);
-    HIP_TRY(hipMemcpy(w.data(), eng->g.in_w, 8 * (size_t)M, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(w32.data(), eng->g.in_w32, 4 * (size_t)M, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(r.data(), eng->g.in_r, 8 * (size_t)M, hipMemcpyDeviceToHost));
+    // the filtered arrays, row order kept, with the builder's padding arcs at the end (the
+    // arc weights come from host mirrors copied once per engine: every attach epoch peels)
+    if (eng->h_in_w.size() != (size_t)M) {
+        eng->h_in_w.resize((size_t)M);
+        eng->h_in_w32.resize((size_t)M);
+        eng->h_in_r.resize((size_t)M);
+        HIP_TRY(hipMemcpy(eng->h_in_w.data(), eng->g.in_w, 8 * (size_t)M, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(eng->h_in_w32.data(), eng->g.in_w32, 4 * (size_t)M, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(eng->h_in_r.data(), eng->g.in_r, 8 * (size_t)M, hipMemcpyDeviceToHost));
+    }
+    const std::vector<double>& w = eng->h_in_w;
+    const std::vector<double>& r = eng->h_in_r;
+    const std::vector<float>& w32 = eng->h_in_w32;
     std::vector<int64_t> nptr((size_t)Vc + 1, 0);
     std::vector<int32_t> nsrc, neid;
     std::vector<double> nw, nr;
     std::vector<float> nw32;
-    nsrc.reserve((size_t)M);
+    nsrc.reserve((size_t)M + CSR_PAD);
+    neid.reserve((size_t)M + CSR_PAD);
+    nw.reserve((size_t)M + CSR_PAD);
+    nr.reserve((size_t)M + CSR_PAD);
+    nw32.reserve((size_t)M + CSR_PAD);
     for (int32_t v = 0; v < V; ++v) {
         if (!keep[v]) continue;
         for (int64_t e = ptr[v]; e < ptr[v + 1]; ++e)
@@ -4528,8 +4529,8 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
         nptr[(size_t)nid[v] + 1] = (int64_t)nsrc.size();
     }
     // per-vertex tables the rounds and the pair dispatch read, in the view's ids
-    std::vector<double> vf((size_t)V), nvf((size_t)Vc);
-    HIP_TRY(hipMemcpy(vf.data(), eng->g.vfac, 8 * (size_t)V, hipMemcpyDeviceToHost));
+    const std::vector<double>& vf = eng->h_vfac;
+    std::vector<double> nvf((size_t)Vc);
     std::vector<int32_t> nloop((size_t)Vc), natt((size_t)std::max<int32_t>(1, eng->A));
     for (int32_t v = 0; v < V; ++v)
         if (nid[v] >= 0) {
@@ -4593,6 +4594,38 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     return SHADOWTOPO_OK;
 }
 
+// k_walk over the group's nbg batches: a block = 4 waves of TPW walk targets each, NC walk
+// chains per lane
+template <bool MG, int TPW, int NC>
+void launch_walk_t(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl, double* dr,
+                   int32_t row_base, int32_t ls, hipStream_t s) {
+    constexpr int TPB = TPW * (WALK_T / 64);
+    hipLaunchKernelGGL((k_walk<MG, TPW, NC>), dim3((uint32_t)((eng->n_walk + TPB - 1) / TPB), nbg), dim3(WALK_T), 0, s,
+                       *eng->rg, eng->d_arcinfo, eng->pools, att, eng->d_walk, eng->n_walk, A, dl, dr, row_base, ls);
+}
+// shape 1 (default): one walk target per wave, one chain per lane.  Walks are bound by the
+// tree records' cache footprint (a batch's 16-byte records are ~100 MB on C4): the fewer
+// targets a wave takes, the fewer batches are walked at once and the more record lines
+// stay in the Infinity Cache.  C4L, compose + walks per build (r05i): 1 target / 1 chain
+// 3.48 ms, 2 / 2 3.67, 2 / 1 4.18, 4 / 2 4.67; a chain that refills itself from the
+// wave's targets lost the same way (8 targets per wave 5.8 ms, 16 6.7)
+template <bool MG>
+void launch_walk_m(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl, double* dr,
+                   int32_t row_base, int32_t ls, hipStream_t s) {
+    if (eng->opt_walk_tpw == 2)
+        launch_walk_t<MG, 2, 2>(eng, nbg, att, A, dl, dr, row_base, ls, s);
+    else
+        launch_walk_t<MG, 1, 1>(eng, nbg, att, A, dl, dr, row_base, ls, s);
+}
+hipError_t launch_walk(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl, double* dr,
+                       int32_t row_base, int32_t ls, hipStream_t s) {
+    if (eng->multigraph)
+        launch_walk_m<true>(eng, nbg, att, A, dl, dr, row_base, ls, s);
+    else
+        launch_walk_m<false>(eng, nbg, att, A, dl, dr, row_base, ls, s);
+    return hipGetLastError();
+}
+
 int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, double* lat, double* rel,
                       uint32_t* hops, uint8_t* kind, int32_t mem, hipStream_t s) {
     // MEM_HOST_LR: host rows of {lat, rel} pairs in `lat` (the shim's per-packet layout); the
@@ -4616,6 +4649,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         if (self_pending) HIP_TRY(hipEventRecord(eng->ev_self[1], s));
         eng->st.self_paths += row_end - row_begin;
     }
+    const auto t_att = std::chrono::steady_clock::now();
     if ((rc = ensure_pruned(eng, s))) return rc;
     eng->rg = eng->prune_ready ? &eng->gp : &eng->g;  // back to g for sssp (shadowtopo_sssp)
     if (!eng->walk_ready && !complete) {
@@ -4700,6 +4734,8 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const bool order = eng->opt_source_order && (!eng->dense || eng->vperm_ready) && !complete &&
                        row_end - row_begin > KL;
     if (order && (rc = ensure_locality(eng, s))) return rc;
+    // host wall time of what depends on the attached set (zero when the set is unchanged)
+    eng->st.attach_prep_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_att).count();
     std::vector<int32_t> lane_row;
     // a renumbered relaxation view: sources and targets in its ids
     const bool view = eng->rg == &eng->gp && !eng->h_view_of.empty();
@@ -4785,14 +4821,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                                eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
             HIP_TRY(hipGetLastError());
             if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
-                const dim3 grid((uint32_t)((eng->n_walk + WALK_TPB - 1) / WALK_TPB), nbg);
-                if (eng->multigraph)
-                    hipLaunchKernelGGL(k_walk<true>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo, eng->pools,
-                                       d_att_r, eng->d_walk, eng->n_walk, A, dl, dr, row_base, ls);
-                else
-                    hipLaunchKernelGGL(k_walk<false>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo, eng->pools,
-                                       d_att_r, eng->d_walk, eng->n_walk, A, dl, dr, row_base, ls);
-                HIP_TRY(hipGetLastError());
+                HIP_TRY(launch_walk(eng, nbg, d_att_r, A, dl, dr, row_base, ls, s));
             }
         }
         if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[1], s));
@@ -5586,6 +5615,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_HBM_SHARE:
             if (value < 1 || value > 1000) return fail(SHADOWTOPO_EINVAL, "HBM share must be in [1, 1000] per mille");
             eng->opt_hbm_share = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_WALK_TPW:
+            if (value != 1 && value != 2) return fail(SHADOWTOPO_EINVAL, "walk shape must be 1 or 2");
+            eng->opt_walk_tpw = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_HEAVY_FIRST:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "heavy first must be 0 or 1");

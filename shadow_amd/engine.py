@@ -54,6 +54,7 @@ OPT_CHAIN_PARTS = 23  # the read-back-free delta rounds on each sweep part's str
 OPT_SWEEP_PARTS = 22  # pruned dense sweep: batches in 1 .. 4 parts (default 2) on their own streams
 OPT_DENSE_SPEC = 21  # dense: leading rounds enqueued without a host read-back (0..4, default 2)
 OPT_DELTA_LIVE = 19  # dense delta rounds over live-chunk lists: 2 when sparse (default), 1 always, 0 never
+OPT_WALK_TPW = 28  # path walks: 1 target per wave, one walk per lane (1, default) or 2 targets, two walks per lane (2)
 OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order
 # testing: the failure paths a convergence bug or a full device would take (SHADOWTOPO_EINTERNAL /
 # the re-sized pool retry instead of a fault)
@@ -101,6 +102,7 @@ class Stats(ctypes.Structure):
         ("push_rounds", ctypes.c_int64), ("fold_rounds", ctypes.c_int64),
         ("packed_pairs", ctypes.c_int64), ("packed_explicit", ctypes.c_int64),
         ("compose_kernel_ms", ctypes.c_double), ("walk_targets", ctypes.c_int64),
+        ("attach_prep_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

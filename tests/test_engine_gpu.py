@@ -42,11 +42,13 @@ def test_no_self_loops():
     compare(g)
 
 
-def test_vertex_loss_walk():
+@pytest.mark.parametrize("shape", [1, 2])
+def test_vertex_loss_walk(shape):
+    """targets with vertex loss take k_walk's full fold; both walk shapes (OPT_WALK_TPW)"""
     rng = np.random.default_rng(3)
     vl = np.where(rng.random(300) < 0.5, rng.uniform(0, 0.1, 300), np.nan)
     g = synth.random_sparse(V=300, avg_deg=4, seed=12, vloss=vl)
-    compare(g)
+    compare(g, walk_tpw=shape)
 
 
 def test_prefer_direct():
@@ -77,7 +79,8 @@ def test_force_replay_matches():
     assert st["replayed_sources"] == g.attached.size
 
 
-def test_multigraph_parallel_edges():
+@pytest.mark.parametrize("shape", [1, 2])
+def test_multigraph_parallel_edges(shape):
     g = synth.random_sparse(V=150, avg_deg=4, seed=17)
     # duplicate 40 edges with different latency/loss (parallel edges)
     rng = np.random.default_rng(0)
@@ -86,7 +89,7 @@ def test_multigraph_parallel_edges():
     g.dst = np.concatenate([g.dst, g.src[pick]])
     g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.3, 1.7, 40)])
     g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 40)])
-    compare(g)
+    compare(g, walk_tpw=shape)
 
 
 def test_complete_graph_direct_rule():
@@ -736,7 +739,8 @@ def test_unconverged_state_composes_without_fault(layout):
         assert_bitexact(name, x, y)
 
 
-def test_long_paths_walk_in_segments():
+@pytest.mark.parametrize("shape", [1, 2])
+def test_long_paths_walk_in_segments(shape):
     """vertex-loss targets whose paths have more hops than one walk segment (16 arcs): a
     path graph (every vertex on one chain, hops up to V - 1) with vertex loss everywhere"""
     V = 90
@@ -746,7 +750,7 @@ def test_long_paths_walk_in_segments():
     g = synth._finish("chain", V, src, dst, rng.uniform(1, 5, V - 1), rng.uniform(0, 0.05, V - 1),
                       np.arange(0, V, 3, dtype=np.int32))
     g.vertex_packetloss = rng.uniform(0, 0.05, V)
-    compare(g)
+    compare(g, walk_tpw=shape)
     _, _, hops, _, _ = engine_matrix(g)
     assert hops.max() > 48
 
