@@ -554,6 +554,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--vertex-loss", action="store_true",
                     help="vertex packetloss on 30 %% of the vertices (synth.with_vertex_loss: C4L for --config C4)")
+    ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-attached-set builds (rocprof counter passes "
+                                                               "read the last dispatches, which must be the timed steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-rate", action="store_true", help="skip the host-buffer (PCIe-inclusive) timing")
     ap.add_argument("--cpu-sources", type=int, default=12)
@@ -696,8 +698,10 @@ def main():
 
     # the build a Shadow run pays once per attach epoch: a new attached set (same size, seed
     # 13) before every timed build, so the set-dependent work is inside the timed region
-    other = np.sort(np.random.default_rng(13).choice(g.n, size=A, replace=False)).astype(np.int32)
-    fresh_ms, fresh_prep_ms = fresh_build_ms(eng, [g.attached, other], r0, r1, args.steps, run["timed"], dev)
+    fresh_ms = fresh_prep_ms = None
+    if not args.no_fresh:
+        other = np.sort(np.random.default_rng(13).choice(g.n, size=A, replace=False)).astype(np.int32)
+        fresh_ms, fresh_prep_ms = fresh_build_ms(eng, [g.attached, other], r0, r1, args.steps, run["timed"], dev)
     sharding = sharded_report(dist, world, run, args.steps, st["relax_ms"] / args.steps, rows)
 
     # the drop-in boundary hands host buffers over (topology_hip.c: MEM_HOST); its

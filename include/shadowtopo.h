@@ -138,6 +138,8 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_WALK_TPW 28          /* path walks (vertex loss, multigraphs): k_walk takes 1 target per wave with one
                                               walk per lane (1, default) or 2 targets per wave, two walks per lane in
                                               lockstep (2). Results are identical. */
+#define SHADOWTOPO_OPT_PART0_PERMILLE 29    /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
+                                              takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
  * instead of faulting the device */
 #define SHADOWTOPO_OPT_TEST_UNCONVERGED 24  /* 1 = when the iteration guard (OPT_MAX_ROUNDS) trips, compose the state

@@ -14,7 +14,7 @@ SCALE=${3:-1.0}
 KERNEL=${4:-k_relax_dense_f<8, 2, 1, true>}
 EXTRA=${5:-}
 PER=${6:-1}
-B="bench.py --config $CFG --scale $SCALE --steps 3 --warmup 1 --no-cpu-baseline --no-host-rate --no-north-star $EXTRA"
+B="bench.py --config $CFG --scale $SCALE --steps 3 --warmup 1 --no-cpu-baseline --no-host-rate --no-north-star --no-fresh $EXTRA"
 O=gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 $B > $O/kt.json 2> $O/kt.err || { echo "kernel-trace failed"; tail -20 $O/kt.err; exit 1; }

@@ -5616,6 +5616,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value < 1 || value > 1000) return fail(SHADOWTOPO_EINVAL, "HBM share must be in [1, 1000] per mille");
             eng->opt_hbm_share = (int32_t)value;
             return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_PART0_PERMILLE:
+            if (value < 1 || value > 999) return fail(SHADOWTOPO_EINVAL, "part 0 share must be in [1, 999] per mille");
+            eng->opt_part0_permille = (int32_t)value;
+            return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_WALK_TPW:
             if (value != 1 && value != 2) return fail(SHADOWTOPO_EINVAL, "walk shape must be 1 or 2");
             eng->opt_walk_tpw = (int32_t)value;
