@@ -24,5 +24,5 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE -d $O
 python3 scripts/roofline_counters.py "$CFG@$SCALE@1" "$KERNEL" $O/kt.json $O/pf $O/pw $O/ps $PER || exit 1
 cp $O/kt/run_kernel_stats.csv $O/kernel_stats.csv 2>/dev/null || find $O/kt -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 cp profiles/roofline_counters.json $O/roofline_counters.json
-timeout -k 10 300 python3 -u bench.py --config $CFG --scale $SCALE --steps 10 --warmup 2 $EXTRA > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+timeout -k 10 300 python3 -u bench.py --config $CFG --scale $SCALE --steps 3 --warmup 1 --no-cpu-baseline $EXTRA > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
