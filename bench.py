@@ -379,7 +379,7 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
                "value": A * steps / elapsed, "unit": "source-paths/s",
                "parallelism": f"{A} sources sharded x{world} (rows [{ex.r0},{ex.r1}) on rank {rank})"
                               + (f" + RCCL all-gather ({len(ex.bounds)} chunks)" if world > 1 else ""),
-               "rounds_per_step": st["rounds"] / steps,
+               "rounds_per_step": st["rounds"] / steps, "lean_rounds": st["lean_groups"] > 0,
                "roofline": roofline_of(st, g, "C4", 1.0, world, ex.rows, steps)}
         rec["compose_kernel_ms"] = st["compose_kernel_ms"] / steps
         rec["sharding"] = sharded_report(dist, world, run, steps, st["relax_ms"] / steps, ex.rows)
@@ -811,6 +811,7 @@ def main():
                        "compose_ms_per_step": st["compose_ms"] / args.steps,
                        "compose_kernel_ms_per_step": st["compose_kernel_ms"] / args.steps,
                        "self_paths_per_step": st["self_paths"] / args.steps, "dense": st["dense"],
+                       "lean_rounds": st["lean_groups"] > 0, "walk_targets": st["walk_targets"],
                        "engine_wall_ms_per_step": st["wall_ms"] / args.steps,
                        "pool_allocs_in_timed_steps": st["pool_allocs"],
                        "pool_alloc_ms_per_step": st["pool_alloc_ms"] / args.steps,

@@ -138,6 +138,12 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_WALK_TPW 28          /* path walks (vertex loss, multigraphs): k_walk takes 1 target per wave with one
                                               walk per lane (1, default) or 2 targets per wave, two walks per lane in
                                               lockstep (2). Results are identical. */
+#define SHADOWTOPO_OPT_CSR_LEAN 30          /* sparse (CSR pull) rounds: 1 = lean -- the rounds keep d and the predecessor arc
+                                              with a local-tie bit (12 B per (vertex, source) instead of 24), only a
+                                              distance change activates the out-neighbours, and a walk of every pair's
+                                              tree path after the rounds yields hops, reliability and the taint;
+                                              0 = the tree fold inside the rounds; 2 (default) = lean when the relaxation
+                                              graph has at least 32 arcs per attached vertex. Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29    /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
@@ -228,6 +234,7 @@ typedef struct shadowtopo_stats {
     int64_t walk_targets;    /* attached targets whose pairs take the full path fold (vertex loss, multigraphs) */
     double attach_prep_ms;   /* host wall time in compute calls of the work a new attached set needs first: the
                                 relaxation view, the walk list and arc table, the pools, the source order */
+    int64_t lean_groups;     /* batch groups computed with lean sparse rounds (OPT_CSR_LEAN) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

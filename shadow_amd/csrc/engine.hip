@@ -148,10 +148,13 @@ struct Pools {
     float* D32;         // dense mode: [slot][Vp][64] f32 filter key (distance rounded down, NaN unreached)
     unsigned long long* err;   // compose: nonzero when a path walk left the predecessor tree (the word
                                // before mask[0]: reset and read back together with the masks)
+    int32_t* P32;       // lean sparse rounds (Q = NULL): [slot][Vp][64] predecessor arc | LT_BIT (local tie)
     int64_t vk;         // Vp * 64
     int32_t Vp;
     int32_t pad_;
 };
+constexpr int32_t LT_BIT = (int32_t)0x80000000u;  // P32: the predecessor choice here is a heap-order tie
+constexpr int32_t P_MASK = 0x7fffffff;
 
 struct BatchDev {
     gdouble* D;
@@ -165,6 +168,7 @@ struct BatchDev {
     unsigned long long* chm0;
     unsigned long long* chm1;
     gfloat* D32;
+    gint* P32;  // lean rounds only (Q NULL)
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
     __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
@@ -173,7 +177,7 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     BatchDev B;
     const size_t o = (size_t)b * (size_t)p.vk;
     B.D = (gdouble*)(p.D + o);
-    B.Q = (gRec*)(p.Q + o);
+    B.Q = p.Q ? (gRec*)(p.Q + o) : nullptr;  // NULL with lean rounds (P32 instead)
     B.act0 = (gbyte*)(p.act + (size_t)b * 2 * p.Vp);
     B.act1 = B.act0 + p.Vp;
     B.srcv = p.srcv + (size_t)b * KL;
@@ -183,6 +187,7 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.chm0 = p.chm ? p.chm + (size_t)b * 2 * p.Vp : nullptr;
     B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
     B.D32 = p.D32 ? (gfloat*)(p.D32 + o) : nullptr;
+    B.P32 = p.P32 ? (gint*)(p.P32 + o) : nullptr;
     return B;
 }
 
@@ -310,7 +315,7 @@ __global__ void k_seed(GraphDev g, Pools pools) {
     if (threadIdx.x == 0) {
         const size_t idx = (size_t)s * KL + j;
         B.D[idx] = 0.0;
-        rec_store(B.Q + idx, g.vfac[s], 0u, -1);
+        if (B.Q) rec_store(B.Q + idx, g.vfac[s], 0u, -1);  // lean rounds: the source's P32 is never read
         // dense mode: f32 filter key NaN (the source's own row never passes a dense filter:
         // its seed candidate starts every lexicographic state, k_relax_dense_f), and the
         // first delta round reads the change masks of a virtual round -1
@@ -327,6 +332,15 @@ __device__ __forceinline__ bool finish_vertex(const BatchDev& B, int lane, int32
                                               double bdu, bool tie, const double* __restrict__ in_r, double curD,
                                               uint32_t curH, double curR, int32_t curP) {
     const size_t idx = (size_t)v * KL + lane;
+    if (B.P32) {  // lean rounds: D and the predecessor arc with its local tie bit, nothing folded
+        const int32_t np = arc | ((tie || bdu == bc) ? LT_BIT : 0);
+        if (bc != curD || np != curP) {
+            B.D[idx] = bc;
+            B.P32[idx] = np;
+            return true;
+        }
+        return false;
+    }
     const size_t uidx = (size_t)u * KL + lane;
     const Rec qu = rec_load(B.Q + uidx);  // the predecessor's record: one line per lane
     const uint32_t hu = qu.h;
@@ -377,10 +391,17 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
     const int32_t sv = B.srcv[lane];
     const size_t idx = (size_t)v * KL + lane;
     const double curD = B.D[idx];
-    const Rec cur = rec_load(B.Q + idx);
-    const uint32_t curH = cur.h;
-    const double curR = cur.r;
-    const int32_t curP = cur.p;
+    uint32_t curH = 0;
+    double curR = 0.0;
+    int32_t curP;
+    if (B.P32) {
+        curP = B.P32[idx];
+    } else {
+        const Rec cur = rec_load(B.Q + idx);
+        curH = cur.h;
+        curR = cur.r;
+        curP = cur.p;
+    }
     const gdouble* Dl = B.D + lane;
     // (unlike the dense kernel, the running best is not seeded with curD here: rows are
     // short, and seeding would put curD's load latency in front of the first row loads)
@@ -406,6 +427,9 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
 
     bool ch = false;
     if (be >= 0 && sv >= 0 && sv != v) ch = finish_vertex(B, lane, v, be, bu, bc, bdu, tie, in_r, curD, curH, curR, curP);
+    // lean rounds: only a distance change reaches the out-neighbours (their candidates depend
+    // on d alone; with the tree fold in the rounds a changed hop count or reliability has to)
+    if (B.P32) ch = ch && bc != curD;
     if (__ballot(ch)) {
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
@@ -2573,15 +2597,17 @@ __global__ __launch_bounds__(COMPOSE_T) void k_compose(GraphDev g, Pools pools,
                 const size_t idx = (size_t)t * KL + lane;
                 const double d = B.D[idx];
                 if (d < dinf()) {
-                    const Rec q = rec_load(B.Q + idx);
-                    const uint32_t h = q.h;
-                    o.taint = (h & TAINT) != 0;
-                    o.hops = h & HMASK;
                     o.lat = (d == 0) ? 1.0 : d;  // topology.c:1848-1852
                     o.kind = SHADOWTOPO_KIND_DIJKSTRA;
-                    // the tree fold (k_walk re-folds the targets with vertex loss, and every
-                    // pair of a multigraph, in the reference's order)
-                    o.rel = q.r;
+                    if (B.Q) {
+                        const Rec q = rec_load(B.Q + idx);
+                        const uint32_t h = q.h;
+                        o.taint = (h & TAINT) != 0;
+                        o.hops = h & HMASK;
+                        // the tree fold (k_walk re-folds the targets with vertex loss, and every
+                        // pair of a multigraph, in the reference's order)
+                        o.rel = q.r;
+                    }  // lean rounds: hops, rel and the taint come from k_walk_lean
                 }
             }
         }
@@ -2757,6 +2783,108 @@ __global__ __launch_bounds__(WALK_T) void k_walk(GraphDev g, const ArcInfo* __re
             start(c);
         }
     }
+    if (err) atomicOr(pools.err, (unsigned long long)err);
+}
+
+// Lean rounds (OPT_CSR_LEAN): the rounds kept D and the predecessor arc with its local tie bit
+// (P32) only, so every shortest-path pair's hop count, reliability fold and taint come from a
+// walk of its tree path here, after k_compose wrote the rows (lat = d(t) and the kinds; the
+// direct and self pairs are complete).  One target per wave, lane = source (as k_walk).  The
+// hop count is unknown until the walk reaches s, so the first pass keeps the factors of the
+// last WALK_SEG arcs it took in a ring (slot = step mod WALK_SEG): those are a_1 .. a_min(h, 8),
+// the fold's first segment; paths longer than a segment re-walk from t per further segment.
+// The taint is the OR of the local tie bits along the path (the rounds with the tree fold
+// carry it down the tree instead).  Bounded like k_walk: every arc and vertex range-checked,
+// at most V hops, an error bit instead of a wild walk.
+template <bool MG>
+__global__ __launch_bounds__(WALK_T) void k_walk_lean(GraphDev g, const ArcInfo* __restrict__ ai, Pools pools,
+                                                     const int32_t* __restrict__ attached, int32_t A, double* out_lat,
+                                                     double* out_rel, uint32_t* out_hops, int32_t row_base,
+                                                     int32_t ls) {
+    __shared__ double sc[WALK_SEG * WALK_T];
+    __shared__ int32_t se[MG ? WALK_SEG * WALK_T : 1];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int32_t ti = blockIdx.x * (WALK_T / 64) + wave;
+    if (ti >= A) return;  // wave-uniform; no barriers below
+    const BatchDev B = batch_view(pools, blockIdx.y);
+    const int32_t sv = B.srcv[lane], row = B.row[lane];
+    const int32_t t = attached[ti];
+    const bool prefer = (g.flags & SHADOWTOPO_F_PREFER_DIRECT) != 0;
+    const int64_t na = g.in_ptr[g.V];
+    double* scl = sc + threadIdx.x;
+    int32_t* sel = se + (MG ? threadIdx.x : 0);
+    // a shortest-path pair (the dispatch's rule 3): not the self pair, not a direct pair of a
+    // prefer-direct graph, reached
+    bool on = sv >= 0 && row >= 0 && sv != t && !(prefer && get_eid(g, sv, t) >= 0) &&
+              B.D[(size_t)t * KL + lane] < dinf();
+    uint32_t err = 0, h = 0;
+    bool taint = false;
+    double rel = on ? g.vfac[sv] * g.vfac[t] : 0.0, lat = 0.0;
+    // pass 1: t -> s
+    int32_t x = t;
+    bool act = on;
+    while (act) {
+        const int32_t q = B.P32[(size_t)x * KL + lane];
+        const int32_t p = q & P_MASK;
+        if ((int64_t)p >= na) {
+            err |= 1u;
+            on = act = false;
+            break;
+        }
+        taint |= q < 0;
+        const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(ai + p);
+        const int32_t u = (int32_t)v.x;
+        const size_t k = (size_t)(h % WALK_SEG) * WALK_T;
+        scl[k] = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
+        if (MG) sel[k] = (int32_t)v.y;
+        ++h;
+        if (u < 0 || u >= g.V) {
+            err |= 1u;
+            on = act = false;
+            break;
+        }
+        if (u == sv) break;
+        if (h >= (uint32_t)g.V) {  // longer than any simple path: not a tree
+            err |= 2u;
+            on = act = false;
+            break;
+        }
+        x = u;
+    }
+    if (on) {
+        // a_i (i = 1 .. min(h, SEG)) was taken at step h - i
+        const uint32_t n0 = min(h, (uint32_t)WALK_SEG);
+        for (uint32_t i = 1; i <= n0; ++i) {
+            const size_t k = (size_t)((h - i) % WALK_SEG) * WALK_T;
+            rel *= scl[k];
+            if (MG) lat += g.elat[sel[k]];
+        }
+        // further segments: a_{k0+1} .. a_{k1}, walking from t again down to x_{k0}
+        for (uint32_t k0 = WALK_SEG; k0 < h; k0 += WALK_SEG) {
+            const uint32_t k1 = min(h, k0 + (uint32_t)WALK_SEG);
+            int32_t y = t;
+            for (uint32_t i = h; i > k0; --i) {  // y = x_i
+                const int32_t p = B.P32[(size_t)y * KL + lane] & P_MASK;
+                const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(ai + p);
+                if (i <= k1) {
+                    const size_t k = (size_t)(i - k0 - 1) * WALK_T;
+                    scl[k] = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
+                    if (MG) sel[k] = (int32_t)v.y;
+                }
+                y = (int32_t)v.x;  // the first pass checked this path
+            }
+            for (uint32_t k = 0; k < k1 - k0; ++k) {
+                rel *= scl[(size_t)k * WALK_T];
+                if (MG) lat += g.elat[sel[(size_t)k * WALK_T]];
+            }
+        }
+        const size_t o = (size_t)(row - row_base) * A + ti;
+        out_rel[o * ls] = rel;
+        if (MG) out_lat[o * ls] = (lat == 0) ? 1.0 : lat;
+        if (out_hops) out_hops[o] = h;
+    }
+    const unsigned long long tm = __ballot(on && taint);
+    if (lane == 0 && tm) atomicOr(B.mask, tm);
     if (err) atomicOr(pools.err, (unsigned long long)err);
 }
 
@@ -2965,7 +3093,10 @@ __global__ void k_scramble_tree(GraphDev g, Pools pools, int32_t mode) {
             if (g.in_ptr[v + 1] == g.in_ptr[v]) continue;
             p = g.in_ptr[v];
         }
-        B.Q[i].p = (int32_t)p;
+        if (B.P32)
+            B.P32[i] = (int32_t)p;
+        else
+            B.Q[i].p = (int32_t)p;
     }
 }
 
@@ -3141,6 +3272,8 @@ struct shadowtopo_engine {
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
+    int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
+    bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
     int32_t opt_walk_tpw = 1;         // k_walk shape (OPT_WALK_TPW): 1 target / 1 chain, or 2 / 2
     uint32_t* d_bweight[4] = {nullptr, nullptr, nullptr, nullptr};  // per part: chunk counts per block
     int32_t* d_border[4][2] = {};     // per part: two order buffers (ping-pong across sweeps)
@@ -3225,7 +3358,7 @@ bool state_bdu(const shadowtopo_engine* eng) { return eng->dense != 0; }
 bool state_d32(const shadowtopo_engine* eng) { return eng->dense != 0; }
 // bytes per (vertex, source) of the batch pools
 double state_bytes(const shadowtopo_engine* eng) {
-    return 24.0 + (state_bdu(eng) ? 8.0 : 0.0) + (state_d32(eng) ? 4.0 : 0.0);
+    return (eng->lean_next ? 12.0 : 24.0) + (state_bdu(eng) ? 8.0 : 0.0) + (state_d32(eng) ? 4.0 : 0.0);
 }
 
 int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb);
@@ -3233,7 +3366,8 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
     // pools with at least the rows the relaxation graph needs are kept (their row stride is
     // pools.Vp everywhere): a new attached set's pendant-pruned view differs by a few rows,
     // and reallocating C5's ~140 GB of pools for that cost 1.2 s of a fresh build (r05j)
-    if (eng->nb_cap >= nb && eng->pools.Vp >= pool_vp(eng)) return SHADOWTOPO_OK;
+    if (eng->nb_cap >= nb && eng->pools.Vp >= pool_vp(eng) && (eng->pools.P32 != nullptr) == eng->lean_next)
+        return SHADOWTOPO_OK;
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = ensure_batches_impl(eng, nb);
     eng->st.pool_allocs++;
@@ -3262,7 +3396,9 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
         eng->opt_test_pool_enomem = 0;
         return fail(SHADOWTOPO_ENOMEM, "injected pool allocation failure (OPT_TEST_POOL_ENOMEM)");
     }
-    if ((rc = dev_alloc(eng->batch_allocs, (void**)&P.Q, VK * nb * sizeof(Rec))) ||
+    // the tree record (R, H, P: 16 B) or, for lean rounds, the predecessor arc alone (4 B)
+    if ((rc = eng->lean_next ? dev_alloc(eng->batch_allocs, (void**)&P.P32, VK * nb * sizeof(int32_t))
+                             : dev_alloc(eng->batch_allocs, (void**)&P.Q, VK * nb * sizeof(Rec))) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.act, (size_t)pvp * 2 * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.srcv, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
@@ -3371,7 +3507,8 @@ Pools pools_from(const Pools& in, int32_t b0) {
     Pools P = in;
     const size_t o = (size_t)b0 * (size_t)P.vk;
     P.D += o;
-    P.Q += o;
+    if (P.Q) P.Q += o;
+    if (P.P32) P.P32 += o;
     P.act += (size_t)b0 * 2 * P.Vp;
     P.srcv += (size_t)b0 * KL;
     P.row += (size_t)b0 * KL;
@@ -4652,6 +4789,16 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const auto t_att = std::chrono::steady_clock::now();
     if ((rc = ensure_pruned(eng, s))) return rc;
     eng->rg = eng->prune_ready ? &eng->gp : &eng->g;  // back to g for sssp (shadowtopo_sssp)
+    // lean sparse rounds (D + the predecessor arc, 12 B per pair instead of 24; no predecessor
+    // gathers in the rounds; hops, reliability and the taint come from a walk per pair after
+    // the rounds, k_walk_lean) pay when the walks are cheap against the rounds: a walk costs
+    // ~3.5 arc-row visits per hop (r05), the tree fold ~20 % of the rounds, so lean when the
+    // graph has many arcs per attached target (C4: 60, C5: 72 -> lean; C3: 16 -> fold)
+    {
+        const int64_t arcs = eng->rg == &eng->g ? eng->n_arcs : eng->gp_arcs;
+        eng->lean_next = !eng->dense && !complete && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL &&
+                         (eng->opt_csr_lean == 1 || (eng->opt_csr_lean == 2 && arcs >= 32 * (int64_t)A));
+    }
     if (!eng->walk_ready && !complete) {
         // the targets whose pairs k_walk re-folds: vertex loss present (a factor != 1), or all
         // of them in a multigraph (lat from the get_eid edges)
@@ -4673,7 +4820,8 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         eng->walk_ready = true;
     }
     eng->st.walk_targets = eng->n_walk;
-    if (eng->n_walk > 0 && (eng->arcinfo_of != eng->rg->in_src || eng->arcinfo_gen != eng->view_gen)) {
+    if ((eng->n_walk > 0 || eng->lean_next) &&
+        (eng->arcinfo_of != eng->rg->in_src || eng->arcinfo_gen != eng->view_gen)) {
         // the walks' per-arc table, for the graph the rounds run on (rebuilt with the view)
         const int64_t na = eng->rg == &eng->g ? eng->n_arcs : eng->gp_arcs;
         if (eng->arcinfo_cap < (size_t)std::max<int64_t>(na, 1)) {
@@ -4820,7 +4968,16 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                                d_att_r, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
                                eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
             HIP_TRY(hipGetLastError());
-            if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
+            if (eng->pools.P32) {  // lean rounds: every shortest-path pair's hops, rel and taint
+                const dim3 grid((uint32_t)((A + 3) / 4), nbg);
+                if (eng->multigraph)
+                    hipLaunchKernelGGL(k_walk_lean<true>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo,
+                                       eng->pools, d_att_r, A, dl, dr, dh, row_base, ls);
+                else
+                    hipLaunchKernelGGL(k_walk_lean<false>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo,
+                                       eng->pools, d_att_r, A, dl, dr, dh, row_base, ls);
+                HIP_TRY(hipGetLastError());
+            } else if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
                 HIP_TRY(launch_walk(eng, nbg, d_att_r, A, dl, dr, row_base, ls, s));
             }
         }
@@ -4902,6 +5059,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         }
         eng->st.sources += r1 - r0;
         eng->st.batches += nbg;
+        if (eng->pools.P32) eng->st.lean_groups++;
         eng->st.groups++;
         eng->st.group_batches = std::max<int64_t>(gidx == 0 ? 0 : eng->st.group_batches, nbg);
     }
@@ -5616,6 +5774,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value < 1 || value > 1000) return fail(SHADOWTOPO_EINVAL, "HBM share must be in [1, 1000] per mille");
             eng->opt_hbm_share = (int32_t)value;
             return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_CSR_LEAN:
+            if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "CSR lean must be 0, 1 or 2");
+            eng->opt_csr_lean = (int32_t)value;
+            return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_PART0_PERMILLE:
             if (value < 1 || value > 999) return fail(SHADOWTOPO_EINVAL, "part 0 share must be in [1, 999] per mille");
             eng->opt_part0_permille = (int32_t)value;
@@ -5673,6 +5835,7 @@ int shadowtopo_sssp(shadowtopo_engine* eng, const int32_t* sources, int32_t n_so
     hipStream_t s = eng->own_stream;
     int rc;
     eng->rg = &eng->g;  // full rows: every vertex, the unpruned graph (and pools sized for it)
+    eng->lean_next = false;  // hops, predecessors and ties per vertex: the tree-fold state
     if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
     const size_t V = (size_t)eng->V;
     double* d_dist = nullptr;

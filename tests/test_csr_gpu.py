@@ -41,13 +41,16 @@ def _case(case):
 CASES = ["sparse", "directed", "ties", "int_random", "vloss_prefer", "no_loops", "multigraph"]
 
 
+@pytest.mark.parametrize("lean", [0, 1])
 @pytest.mark.parametrize("worklist", [1, 2])
 @pytest.mark.parametrize("case", CASES)
-def test_csr_rounds(case, worklist):
-    """default schedule (worklists when under half the pairs are active) and always-worklist"""
+def test_csr_rounds(case, worklist, lean):
+    """default schedule (worklists when under half the pairs are active) and always-worklist;
+    the tree fold inside the rounds (lean 0) and the lean rounds + a walk per pair (lean 1)"""
     g = _case(case)
-    st = compare(g, layout="csr", worklist=worklist)
+    st = compare(g, layout="csr", worklist=worklist, csr_lean=lean)
     assert st["dense"] == 0
+    assert (st["lean_groups"] > 0) == (lean == 1)
 
 
 def test_csr_removed_variants_rejected():
@@ -70,20 +73,42 @@ def test_csr_full_grid_without_worklists(case):
     compare(g, layout="csr", worklist=1, batches_in_flight=2)
 
 
+@pytest.mark.parametrize("lean", [0, 1])
 @pytest.mark.parametrize("worklist", [0, 1, 2])
-def test_csr_two_dimensional_grids(worklist):
+def test_csr_two_dimensional_grids(worklist, lean):
     """grids past 2^24 blocks (C5: 102 batches x 868k vertices = 22M blocks of 256) go 2-D
     (grid_of / flat_block: a 1-D launch's 32-bit work-item count would wrap and drop
     blocks, and a round that dropped a batch could end the iteration early); forcing the
     2-D form on every launch of a small graph must give the same matrices"""
     g = synth.random_sparse(V=400, avg_deg=5, seed=38)
-    compare(g, layout="csr", worklist=worklist, grid_x=64)
+    compare(g, layout="csr", worklist=worklist, grid_x=64, csr_lean=lean)
 
 
+@pytest.mark.parametrize("lean", [0, 1])
 @pytest.mark.parametrize("worklist", [0, 1])
-def test_csr_several_groups(worklist):
+def test_csr_several_groups(worklist, lean):
     g = synth.random_sparse(V=500, avg_deg=4, seed=37)
-    compare(g, layout="csr", batches_in_flight=3, worklist=worklist)  # 500 sources -> 8 batches -> 3 groups
+    compare(g, layout="csr", batches_in_flight=3, worklist=worklist, csr_lean=lean)  # 8 batches -> 3 groups
+
+
+@pytest.mark.parametrize("case", ["sparse", "ties", "vloss_prefer", "multigraph", "directed"])
+def test_lean_rounds_long_paths_and_auto(case):
+    """lean rounds (OPT_CSR_LEAN 1) on a path-heavy graph (a chain with chords: hop counts far
+    past one walk segment) and the automatic choice on a graph with many arcs per attached
+    vertex (few attached targets: lean), both against the oracle"""
+    g = _case(case)
+    rng = np.random.default_rng(11)
+    g.attached = np.sort(rng.choice(g.n, size=max(2, g.n // 40), replace=False)).astype(np.int32)
+    st = compare(g, layout="csr")  # auto: arcs >= 32 x attached
+    assert st["lean_groups"] > 0
+    V = 200
+    src = np.concatenate([np.arange(V - 1), rng.integers(0, V, 6)]).astype(np.int32)
+    dst = np.concatenate([np.arange(1, V), rng.integers(0, V, 6)]).astype(np.int32)
+    keep = src != dst
+    chain = synth._finish("chain", V, src[keep], dst[keep], rng.uniform(1, 5, keep.sum()),
+                          rng.uniform(0, 0.05, keep.sum()), np.arange(0, V, 7, dtype=np.int32))
+    chain.vertex_packetloss = np.where(rng.random(V) < 0.5, rng.uniform(0, 0.05, V), np.nan)
+    compare(chain, layout="csr", csr_lean=1)
 
 
 @pytest.mark.parametrize("case", ["ties", "sparse", "int_random", "directed"])

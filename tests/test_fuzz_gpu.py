@@ -2,7 +2,7 @@
 each engine matrix compared with the oracle bit for bit (latency, reliability, hops, kind).
 The named tests pin one feature at a time; this sweep crosses them (directed x multigraph
 x integer ties x vertex loss x prefer-direct x layout x worklist / device rounds / batch
-groups / read-back-free dense rounds / push rounds / pendant pruning), so a combination no
+groups / read-back-free dense rounds / push rounds / pendant pruning / lean rounds), so a combination no
 named test covers still meets the oracle.  Fixed seeds: a failure names its case."""
 import numpy as np
 import pytest
@@ -44,6 +44,9 @@ def _case(seed):
         opts["dense_prune"] = int(rng.integers(0, 2))
     if rng.random() < 0.4:
         opts["batches_in_flight"] = int(rng.integers(1, 3))
+    lean = int(rng.integers(0, 3))  # drawn last: the draws above are the r04 sweep's
+    if layout != "dense" and opts.get("csr_variant") != 2:
+        opts["csr_lean"] = lean
     return g, layout, opts
 
 
@@ -73,6 +76,7 @@ def _big_case(seed):
     else:
         g = synth.integer_grid(rows=int(rng.integers(10, 30)), cols=int(rng.integers(10, 30)), seed=int(rng.integers(1 << 20)))
     opts = {"batches_in_flight": int(rng.integers(1, 4))} if rng.random() < 0.5 else {}
+    opts["csr_lean"] = int(rng.integers(0, 3))  # (dense graphs ignore it)
     return g, opts
 
 
