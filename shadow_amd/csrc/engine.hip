@@ -2796,94 +2796,150 @@ __global__ __launch_bounds__(WALK_T) void k_walk(GraphDev g, const ArcInfo* __re
 // The taint is the OR of the local tie bits along the path (the rounds with the tree fold
 // carry it down the tree instead).  Bounded like k_walk: every arc and vertex range-checked,
 // at most V hops, an error bit instead of a wild walk.
-template <bool MG>
+template <bool MG, int TPW, int NC>
 __global__ __launch_bounds__(WALK_T) void k_walk_lean(GraphDev g, const ArcInfo* __restrict__ ai, Pools pools,
                                                      const int32_t* __restrict__ attached, int32_t A, double* out_lat,
                                                      double* out_rel, uint32_t* out_hops, int32_t row_base,
                                                      int32_t ls) {
-    __shared__ double sc[WALK_SEG * WALK_T];
-    __shared__ int32_t se[MG ? WALK_SEG * WALK_T : 1];
+    // NC walks per lane in lockstep, each a state machine over the wave's TPW targets
+    // (chain c takes targets c, c + NC, ...): phase 0 walks t -> s keeping the last WALK_SEG
+    // factors in a ring (the hop count is unknown until s), phase 1 re-walks a further segment
+    __shared__ double sc[NC * WALK_SEG * WALK_T];
+    __shared__ int32_t se[MG ? NC * WALK_SEG * WALK_T : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int32_t ti = blockIdx.x * (WALK_T / 64) + wave;
-    if (ti >= A) return;  // wave-uniform; no barriers below
     const BatchDev B = batch_view(pools, blockIdx.y);
     const int32_t sv = B.srcv[lane], row = B.row[lane];
-    const int32_t t = attached[ti];
     const bool prefer = (g.flags & SHADOWTOPO_F_PREFER_DIRECT) != 0;
     const int64_t na = g.in_ptr[g.V];
-    double* scl = sc + threadIdx.x;
-    int32_t* sel = se + (MG ? threadIdx.x : 0);
-    // a shortest-path pair (the dispatch's rule 3): not the self pair, not a direct pair of a
-    // prefer-direct graph, reached
-    bool on = sv >= 0 && row >= 0 && sv != t && !(prefer && get_eid(g, sv, t) >= 0) &&
-              B.D[(size_t)t * KL + lane] < dinf();
-    uint32_t err = 0, h = 0;
-    bool taint = false;
-    double rel = on ? g.vfac[sv] * g.vfac[t] : 0.0, lat = 0.0;
-    // pass 1: t -> s
-    int32_t x = t;
-    bool act = on;
-    while (act) {
-        const int32_t q = B.P32[(size_t)x * KL + lane];
-        const int32_t p = q & P_MASK;
-        if ((int64_t)p >= na) {
-            err |= 1u;
-            on = act = false;
-            break;
+    const double fs = sv >= 0 ? g.vfac[sv] : 1.0;
+    const int32_t kb = (blockIdx.x * (WALK_T / 64) + wave) * TPW;
+    const int32_t ke = min(A, kb + TPW);
+    uint32_t err = 0;
+    unsigned long long tmask = 0ull;  // this lane's tainted pairs (any target): one bit, the lane's
+    int32_t j[NC], ti[NC], t[NC], x[NC];
+    uint32_t h[NC], i[NC], k0[NC];
+    int phase[NC];
+    bool act[NC], taint[NC];
+    double rel[NC], lat[NC];
+    auto slot = [&](int c, uint32_t k) { return (size_t)(c * WALK_SEG + k) * WALK_T + threadIdx.x; };
+    // chain c's next walkable target (a shortest-path pair of the dispatch's rule 3: not the
+    // self pair, not a direct pair of a prefer-direct graph, reached)
+    auto start = [&](int c) {
+        act[c] = false;
+        while (j[c] < ke) {
+            const int32_t k = j[c];
+            j[c] += NC;
+            const int32_t tv = attached[k];
+            if (sv < 0 || row < 0 || sv == tv || (prefer && get_eid(g, sv, tv) >= 0)) continue;
+            if (!(B.D[(size_t)tv * KL + lane] < dinf())) continue;
+            ti[c] = k;
+            t[c] = x[c] = tv;
+            h[c] = 0;
+            k0[c] = 0;
+            phase[c] = 0;
+            taint[c] = false;
+            rel[c] = fs * g.vfac[tv];
+            lat[c] = 0.0;
+            act[c] = true;
+            return;
         }
-        taint |= q < 0;
-        const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(ai + p);
-        const int32_t u = (int32_t)v.x;
-        const size_t k = (size_t)(h % WALK_SEG) * WALK_T;
-        scl[k] = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
-        if (MG) sel[k] = (int32_t)v.y;
-        ++h;
-        if (u < 0 || u >= g.V) {
-            err |= 1u;
-            on = act = false;
-            break;
+    };
+    auto finish = [&](int c) {
+        const size_t o = (size_t)(row - row_base) * A + ti[c];
+        out_rel[o * ls] = rel[c];
+        if (MG) out_lat[o * ls] = (lat[c] == 0) ? 1.0 : lat[c];
+        if (out_hops) out_hops[o] = h[c];
+        if (taint[c]) tmask = 1ull;
+        start(c);
+    };
+    auto fold = [&](int c, uint32_t n, bool ring) {  // a_{k0+1} .. a_{k0+n} forwards
+        for (uint32_t k = 0; k < n; ++k) {
+            // ring (phase 0): a_i was taken at step h - i; segments: slot i - k0 - 1
+            const size_t q = slot(c, ring ? (h[c] - 1 - k) % WALK_SEG : k);
+            rel[c] *= sc[q];
+            if (MG) lat[c] += g.elat[se[q]];
         }
-        if (u == sv) break;
-        if (h >= (uint32_t)g.V) {  // longer than any simple path: not a tree
-            err |= 2u;
-            on = act = false;
-            break;
-        }
-        x = u;
+    };
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        j[c] = kb + c;
+        start(c);
     }
-    if (on) {
-        // a_i (i = 1 .. min(h, SEG)) was taken at step h - i
-        const uint32_t n0 = min(h, (uint32_t)WALK_SEG);
-        for (uint32_t i = 1; i <= n0; ++i) {
-            const size_t k = (size_t)((h - i) % WALK_SEG) * WALK_T;
-            rel *= scl[k];
-            if (MG) lat += g.elat[sel[k]];
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) any |= act[c];
+        if (!any) break;
+        int32_t q[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) q[c] = act[c] ? B.P32[(size_t)x[c] * KL + lane] : 0;
+        u32x4 v[NC];
+        bool okp[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            okp[c] = act[c] && (int64_t)(q[c] & P_MASK) < na;
+            if (okp[c]) v[c] = *(const __attribute__((address_space(1))) u32x4*)(ai + (q[c] & P_MASK));
         }
-        // further segments: a_{k0+1} .. a_{k1}, walking from t again down to x_{k0}
-        for (uint32_t k0 = WALK_SEG; k0 < h; k0 += WALK_SEG) {
-            const uint32_t k1 = min(h, k0 + (uint32_t)WALK_SEG);
-            int32_t y = t;
-            for (uint32_t i = h; i > k0; --i) {  // y = x_i
-                const int32_t p = B.P32[(size_t)y * KL + lane] & P_MASK;
-                const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(ai + p);
-                if (i <= k1) {
-                    const size_t k = (size_t)(i - k0 - 1) * WALK_T;
-                    scl[k] = __longlong_as_double((long long)(((unsigned long long)v.w << 32) | v.z));
-                    if (MG) sel[k] = (int32_t)v.y;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (!act[c]) continue;
+            if (!okp[c]) {  // an arc past the range: abandoned, compute_rows reports the error
+                err |= 1u;
+                start(c);
+                continue;
+            }
+            const int32_t u = (int32_t)v[c].x;
+            const double r = __longlong_as_double((long long)(((unsigned long long)v[c].w << 32) | v[c].z));
+            if (u < 0 || u >= g.V) {
+                err |= 1u;
+                start(c);
+                continue;
+            }
+            if (phase[c] == 0) {
+                taint[c] |= q[c] < 0;
+                const size_t qs = slot(c, h[c] % WALK_SEG);
+                sc[qs] = r;
+                if (MG) se[qs] = (int32_t)v[c].y;
+                ++h[c];
+                if (u != sv) {
+                    if (h[c] >= (uint32_t)g.V) {  // longer than any simple path: not a tree
+                        err |= 2u;
+                        start(c);
+                    } else {
+                        x[c] = u;
+                    }
+                    continue;
                 }
-                y = (int32_t)v.x;  // the first pass checked this path
+                fold(c, min(h[c], (uint32_t)WALK_SEG), true);
+                if (h[c] <= WALK_SEG) {
+                    finish(c);
+                    continue;
+                }
+                phase[c] = 1;  // further segments, each walked from t again
+                k0[c] = WALK_SEG;
+                x[c] = t[c];
+                i[c] = h[c];
+                continue;
             }
-            for (uint32_t k = 0; k < k1 - k0; ++k) {
-                rel *= scl[(size_t)k * WALK_T];
-                if (MG) lat += g.elat[sel[(size_t)k * WALK_T]];
+            // phase 1: x = x_i, taking a_i; the segment holds a_{k0+1} .. a_{k1}
+            if (i[c] <= k0[c] + WALK_SEG) {
+                const size_t qs = slot(c, i[c] - k0[c] - 1);
+                sc[qs] = r;
+                if (MG) se[qs] = (int32_t)v[c].y;
+            }
+            x[c] = u;
+            if (--i[c] > k0[c]) continue;
+            fold(c, min(h[c], k0[c] + (uint32_t)WALK_SEG) - k0[c], false);
+            k0[c] += WALK_SEG;
+            if (k0[c] < h[c]) {
+                x[c] = t[c];
+                i[c] = h[c];
+            } else {
+                finish(c);
             }
         }
-        const size_t o = (size_t)(row - row_base) * A + ti;
-        out_rel[o * ls] = rel;
-        if (MG) out_lat[o * ls] = (lat == 0) ? 1.0 : lat;
-        if (out_hops) out_hops[o] = h;
     }
-    const unsigned long long tm = __ballot(on && taint);
+    const unsigned long long tm = __ballot(tmask != 0ull);
     if (lane == 0 && tm) atomicOr(B.mask, tm);
     if (err) atomicOr(pools.err, (unsigned long long)err);
 }
@@ -4754,6 +4810,34 @@ void launch_walk_m(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int3
     else
         launch_walk_t<MG, 1, 1>(eng, nbg, att, A, dl, dr, row_base, ls, s);
 }
+// k_walk_lean: TPW targets per wave, NC walks per lane (OPT_WALK_TPW: 1 = 1 / 1, 2 = 2 / 2,
+// 3 = 4 / 2, 4 = 8 / 2)
+template <bool MG, int TPW, int NC>
+void launch_walk_lean_t(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl, double* dr,
+                        uint32_t* dh, int32_t row_base, int32_t ls, hipStream_t s) {
+    constexpr int TPB = TPW * (WALK_T / 64);
+    hipLaunchKernelGGL((k_walk_lean<MG, TPW, NC>), dim3((uint32_t)((A + TPB - 1) / TPB), nbg), dim3(WALK_T), 0, s,
+                       *eng->rg, eng->d_arcinfo, eng->pools, att, A, dl, dr, dh, row_base, ls);
+}
+template <bool MG>
+void launch_walk_lean_m(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl, double* dr,
+                        uint32_t* dh, int32_t row_base, int32_t ls, hipStream_t s) {
+    switch (eng->opt_walk_tpw) {
+        case 2: launch_walk_lean_t<MG, 2, 2>(eng, nbg, att, A, dl, dr, dh, row_base, ls, s); break;
+        case 3: launch_walk_lean_t<MG, 4, 2>(eng, nbg, att, A, dl, dr, dh, row_base, ls, s); break;
+        case 4: launch_walk_lean_t<MG, 8, 2>(eng, nbg, att, A, dl, dr, dh, row_base, ls, s); break;
+        default: launch_walk_lean_t<MG, 1, 1>(eng, nbg, att, A, dl, dr, dh, row_base, ls, s); break;
+    }
+}
+hipError_t launch_walk_lean(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl,
+                            double* dr, uint32_t* dh, int32_t row_base, int32_t ls, hipStream_t s) {
+    if (eng->multigraph)
+        launch_walk_lean_m<true>(eng, nbg, att, A, dl, dr, dh, row_base, ls, s);
+    else
+        launch_walk_lean_m<false>(eng, nbg, att, A, dl, dr, dh, row_base, ls, s);
+    return hipGetLastError();
+}
+
 hipError_t launch_walk(shadowtopo_engine* eng, int32_t nbg, const int32_t* att, int32_t A, double* dl, double* dr,
                        int32_t row_base, int32_t ls, hipStream_t s) {
     if (eng->multigraph)
@@ -4863,6 +4947,15 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             row_bytes >= 0.5 * (double)eng->n_arcs)
             nb = std::max(1, (need + eng->opt_host_split - 1) / eng->opt_host_split);
     }
+    {
+        // groups of equal size: C5's 782 batches at 260 per group ran as 260 / 260 / 260 / 2,
+        // and the last group's ~19 rounds over 2 batches were nearly all overhead
+        const int32_t need = (row_end - row_begin + KL - 1) / KL;
+        if (nb < need) {
+            const int32_t ng = (need + nb - 1) / nb;
+            nb = (need + ng - 1) / ng;
+        }
+    }
     if ((rc = ensure_batches(eng, nb)) == SHADOWTOPO_ENOMEM && eng->floor_ok) {
         // the 24 GB floor was free once, but something else has taken HBM since (another
         // engine or process on the device): size the pools from a fresh free-memory query
@@ -4969,14 +5062,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                                eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
             HIP_TRY(hipGetLastError());
             if (eng->pools.P32) {  // lean rounds: every shortest-path pair's hops, rel and taint
-                const dim3 grid((uint32_t)((A + 3) / 4), nbg);
-                if (eng->multigraph)
-                    hipLaunchKernelGGL(k_walk_lean<true>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo,
-                                       eng->pools, d_att_r, A, dl, dr, dh, row_base, ls);
-                else
-                    hipLaunchKernelGGL(k_walk_lean<false>, grid, dim3(WALK_T), 0, s, *eng->rg, eng->d_arcinfo,
-                                       eng->pools, d_att_r, A, dl, dr, dh, row_base, ls);
-                HIP_TRY(hipGetLastError());
+                HIP_TRY(launch_walk_lean(eng, nbg, d_att_r, A, dl, dr, dh, row_base, ls, s));
             } else if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
                 HIP_TRY(launch_walk(eng, nbg, d_att_r, A, dl, dr, row_base, ls, s));
             }
@@ -5783,7 +5869,7 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             eng->opt_part0_permille = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_WALK_TPW:
-            if (value != 1 && value != 2) return fail(SHADOWTOPO_EINVAL, "walk shape must be 1 or 2");
+            if (value < 1 || value > 4) return fail(SHADOWTOPO_EINVAL, "walk shape must be 1 .. 4");
             eng->opt_walk_tpw = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_HEAVY_FIRST:
