@@ -144,7 +144,11 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               tree path after the rounds yields hops, reliability and the taint;
                                               0 = the tree fold inside the rounds; 2 (default) = lean when the relaxation
                                               graph has at least 32 arcs per attached vertex. Results are identical. */
-#define SHADOWTOPO_OPT_PART0_PERMILLE 29    /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
+#define SHADOWTOPO_OPT_CSR_INCREMENTAL 31   /* lean sparse rounds: n > 0 = a visit of a vertex with more than n in-arcs
+                                              re-reads only the in-arcs whose tail's distance changed in the last two
+                                              rounds (a per-(vertex, batch) change stamp), starting from the stored
+                                              state (default 32); 0 = every in-arc. Results are identical. */
+#define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
  * instead of faulting the device */

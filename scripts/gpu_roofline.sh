@@ -3,7 +3,7 @@
 # (FETCH_SIZE, WRITE_SIZE, SQ) over the SAME bench command, summarised into
 # profiles/roofline_counters.json (key CFG@SCALE@1), then the bench line that reads them.
 # usage: scripts/gpu_roofline.sh TAG CFG SCALE KERNEL_RE ["extra bench args"] [DISPATCHES_PER_LAUNCH]
-# (KERNEL_RE: a Python regex over rocprof kernel names, e.g. "k_relax_dense_f<8, 2, 1, true>" or "k_relax\(|k_relax_wl\(")
+# (KERNEL_RE: a Python regex over rocprof kernel names, e.g. "k_relax_dense_f<8, 2, 1, true>" or "k_relax<|k_relax_wl<" (the sparse relax kernels are templates)
 # DISPATCHES_PER_LAUNCH: C2's sweep is 4 (chunk loop + exact pass, per part of OPT_SWEEP_PARTS = 2)
 set -o pipefail
 mkdir -p gpurun_out

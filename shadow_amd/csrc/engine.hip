@@ -149,12 +149,15 @@ struct Pools {
     unsigned long long* err;   // compose: nonzero when a path walk left the predecessor tree (the word
                                // before mask[0]: reset and read back together with the masks)
     int32_t* P32;       // lean sparse rounds (Q = NULL): [slot][Vp][64] predecessor arc | LT_BIT (local tie)
+    uint8_t* stamp;     // lean sparse rounds: [slot][Vp] round (mod 256) of a vertex's last distance change
     int64_t vk;         // Vp * 64
     int32_t Vp;
-    int32_t pad_;
+    int32_t inc;        // incremental lean rounds (OPT_CSR_INCREMENTAL): 0 = off, else the in-degree
+                        // above which a visit reads only the fresh tails
 };
 constexpr int32_t LT_BIT = (int32_t)0x80000000u;  // P32: the predecessor choice here is a heap-order tie
 constexpr int32_t P_MASK = 0x7fffffff;
+constexpr uint8_t STAMP_NONE = 0x80;  // stamp of a vertex no round has changed (a stale match only costs a re-read)
 
 struct BatchDev {
     gdouble* D;
@@ -169,6 +172,8 @@ struct BatchDev {
     unsigned long long* chm1;
     gfloat* D32;
     gint* P32;  // lean rounds only (Q NULL)
+    gbyte* st;  // incremental lean rounds only: per-vertex change stamps
+    int32_t inc_min;  // incremental lean rounds: in-degree above which a visit reads fresh tails only
     __device__ gbyte* act(int32_t parity) const { return parity ? act1 : act0; }
     __device__ unsigned long long* chm(int32_t parity) const { return parity ? chm1 : chm0; }
 };
@@ -188,6 +193,8 @@ __device__ __forceinline__ BatchDev batch_view(const Pools& p, int32_t b) {
     B.chm1 = B.chm0 ? B.chm0 + p.Vp : nullptr;
     B.D32 = p.D32 ? (gfloat*)(p.D32 + o) : nullptr;
     B.P32 = p.P32 ? (gint*)(p.P32 + o) : nullptr;
+    B.st = p.inc && p.stamp ? (gbyte*)(p.stamp + (size_t)b * p.Vp) : nullptr;
+    B.inc_min = p.inc;
     return B;
 }
 
@@ -292,6 +299,7 @@ __global__ void k_init(Pools pools, int32_t V, int32_t tree) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)V; i += (size_t)gridDim.x * blockDim.x) {
         B.act0[i] = 0;
         B.act1[i] = 0;
+        if (B.st) B.st[i] = STAMP_NONE;
     }
     if (B.chm0) {
         if (tree)
@@ -316,6 +324,7 @@ __global__ void k_seed(GraphDev g, Pools pools) {
         const size_t idx = (size_t)s * KL + j;
         B.D[idx] = 0.0;
         if (B.Q) rec_store(B.Q + idx, g.vfac[s], 0u, -1);  // lean rounds: the source's P32 is never read
+        if (B.st) B.st[s] = 0xFF;  // changed in round -1: round 0's visits read the source's row
         // dense mode: f32 filter key NaN (the source's own row never passes a dense filter:
         // its seed candidate starts every lexicographic state, k_relax_dense_f), and the
         // first delta round reads the change masks of a virtual round -1
@@ -385,8 +394,9 @@ __device__ __forceinline__ void relax_arc(double du, double w, int32_t e, int32_
 __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                             const double* __restrict__ in_w, const double* __restrict__ in_r,
                                             const int64_t* __restrict__ out_ptr, const int32_t* __restrict__ out_dst,
-                                            const BatchDev& B, int32_t b, int32_t v, int lane, int32_t parity,
+                                            const BatchDev& B, int32_t b, int32_t v, int lane, int32_t round,
                                             int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
+    const int32_t parity = round & 1;
     const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
     const int32_t sv = B.srcv[lane];
     const size_t idx = (size_t)v * KL + lane;
@@ -433,18 +443,164 @@ __device__ __forceinline__ void relax_visit(const int64_t* __restrict__ in_ptr, 
     if (__ballot(ch)) {
         gbyte* act_nxt = B.act(parity ^ 1);
         for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
-        if (lane == 0) cnt[b] = 1;  // idempotent flag, no atomic contention
+        if (lane == 0) {
+            cnt[b] = 1;  // idempotent flag, no atomic contention
+            if (B.st) B.st[v] = (uint8_t)round;  // incremental lean rounds: v's row is fresh
+        }
         if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
     }
     if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
 }
 
-// one wave per (destination, batch) of the whole grid; inactive pairs exit after their flag
+// Incremental lean visit (OPT_CSR_INCREMENTAL).  The state (d, predecessor arc | tie bit) of
+// (v, lane) is already the lexicographic minimum over every in-arc at the values its tail had
+// when last read, and distances only fall; so a visit only has to fold in the arcs whose tail
+// changed since: a change in round q stamps the tail (u, batch) with q and activates v for
+// round q + 1, whose visit reads the tails stamped q or q + 1 (a later change stamps and
+// activates again).  A tail's row is loaded only when its stamp is fresh -- one byte per
+// (tail, batch) instead of 512 bytes per arc.  The running best starts from the stored state;
+// its d(pred), the second key, is gathered only when a candidate meets it at an equal
+// distance.  The tie bit is carried while the key holds and cleared when a strictly better
+// candidate replaces it: an arc that ties the final key is read at its final value after its
+// tail's last change, which is when that key is already the running best or becomes it, so
+// no tie the full visit finds is lost; a bit that outlives its tie (the predecessor's d fell
+// at the same fl sum) only sends the source to the heap-exact replay.  Same distances, same
+// predecessor wherever the path is untied.
+__device__ __forceinline__ void relax_arc_inc(const int32_t* __restrict__ in_src, const gdouble* Dl, double du,
+                                              double w, int32_t e, double& bc, double& bdu, int32_t& be, bool& tie,
+                                              bool& known) {
+    const double c = du + w;
+    if (c < bc) {
+        bc = c;
+        bdu = du;
+        be = e;
+        tie = false;
+        known = true;
+    } else if (c == bc && e != be) {
+        if (!known) {  // the stored predecessor's d, now (only ever falls: a stale key is re-decided)
+            bdu = Dl[(size_t)in_src[be] * KL];
+            known = true;
+        }
+        if (du < bdu) {
+            bdu = du;
+            be = e;
+            tie = false;
+        } else if (du == bdu) {
+            tie = true;
+        }
+    }
+}
+
+__device__ __forceinline__ void relax_visit_inc(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                                const int64_t* __restrict__ out_ptr,
+                                                const int32_t* __restrict__ out_dst, const BatchDev& B, int32_t b,
+                                                int32_t v, int lane, int32_t round, int32_t* __restrict__ cnt,
+                                                unsigned long long* __restrict__ prof) {
+    const int32_t beg = (int32_t)in_ptr[v], end = (int32_t)in_ptr[v + 1];
+    // a short in-list costs one chunk of row loads either way: the full visit (it stamps too)
+    // has one dependent load fewer than the stamp filter
+    if (end - beg <= B.inc_min) {
+        relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
+        return;
+    }
+    const int32_t sv = B.srcv[lane];
+    const size_t idx = (size_t)v * KL + lane;
+    const double curD = B.D[idx];
+    const int32_t curP = B.P32[idx];
+    const gdouble* Dl = B.D + lane;
+    const uint32_t s_prev = (uint32_t)(round - 1) & 0xffu, s_cur = (uint32_t)round & 0xffu;
+    double bc = dmax(), bdu = dinf();
+    int32_t be = -1;
+    bool tie = false, known = true;
+    const int32_t a0 = curP & P_MASK;
+    if (curD < dinf() && sv >= 0 && sv != v && a0 >= beg && a0 < end) {
+        bc = curD;
+        be = a0;
+        tie = curP < 0;  // LT_BIT
+        known = false;
+    }
+    // 64 in-arcs at a time: lane i reads arc i's tail, weight and the tail's stamp; the ballot
+    // is the fresh-arc mask, whose arcs then go 8 rows in flight
+    for (int32_t e0 = beg; e0 < end; e0 += 64) {
+        const int32_t e = e0 + lane;
+        int32_t ul = 0;
+        double wl = 0.0;
+        bool fresh = false;
+        if (e < end) {
+            ul = in_src[e];
+            wl = in_w[e];
+            const uint32_t t = B.st[ul];
+            fresh = t == s_prev || t == s_cur;
+        }
+        uint64_t m = __ballot(fresh);
+        while (m) {
+            int32_t uq[8], eq[8];
+            double wq[8], dq[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                eq[q] = -1;
+                uq[q] = 0;
+                wq[q] = 0.0;
+                if (m) {
+                    const int i = __builtin_ctzll(m);
+                    m &= m - 1;
+                    eq[q] = e0 + i;
+                    uq[q] = __builtin_amdgcn_readlane(ul, i);
+                    wq[q] = readlane_d(wl, i);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dq[q] = eq[q] >= 0 ? Dl[(size_t)uq[q] * KL] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (eq[q] >= 0) relax_arc_inc(in_src, Dl, dq[q], wq[q], eq[q], bc, bdu, be, tie, known);
+        }
+    }
+    bool ch = false;
+    if (be >= 0 && sv >= 0 && sv != v) {
+        const int32_t np = be | ((tie || (known && bdu == bc)) ? LT_BIT : 0);
+        if (bc != curD) {
+            B.D[idx] = bc;
+            B.P32[idx] = np;
+            ch = true;
+        } else if (np != curP) {
+            B.P32[idx] = np;  // a tie found at the same distance: no activation
+        }
+    }
+    if (__ballot(ch)) {
+        gbyte* act_nxt = B.act((round & 1) ^ 1);
+        for (int64_t x = out_ptr[v] + lane; x < out_ptr[v + 1]; x += 64) act_nxt[out_dst[x]] = 1;
+        if (lane == 0) {
+            B.st[v] = (uint8_t)round;
+            cnt[b] = 1;
+        }
+        if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7)) + 1], 1ull);
+    }
+    if (prof && lane == 0) atomicAdd(&prof[2 * (8 * b + (blockIdx.x & 7))], 1ull);
+}
+
+template <bool INC>
+__device__ __forceinline__ void relax_visit_any(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
+                                                const double* __restrict__ in_w, const double* __restrict__ in_r,
+                                                const int64_t* __restrict__ out_ptr,
+                                                const int32_t* __restrict__ out_dst, const BatchDev& B, int32_t b,
+                                                int32_t v, int lane, int32_t round, int32_t* __restrict__ cnt,
+                                                unsigned long long* __restrict__ prof) {
+    if (INC)
+        relax_visit_inc(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
+    else
+        relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
+}
+
+// one wave per (destination, batch) of the whole grid; inactive pairs exit after their flag.
+// INC: incremental lean visits (the batch views carry stamps; see relax_visit_inc)
+template <bool INC>
 __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                const int64_t* __restrict__ out_ptr,
                                                const int32_t* __restrict__ out_dst, Pools pools,
-                                               int32_t V, int32_t nb, int32_t nvb, int32_t parity,
+                                               int32_t V, int32_t nb, int32_t nvb, int32_t round,
                                                int32_t* __restrict__ cnt, unsigned long long* __restrict__ prof) {
     int32_t b, vt;
     if (!xcd_tile(flat_block(), nb, nvb, b, vt)) return;
@@ -453,10 +609,10 @@ __global__ __launch_bounds__(256) void k_relax(const int64_t* __restrict__ in_pt
     if (v >= V) return;
     const int lane = threadIdx.x & 63;
     const BatchDev B = batch_view(pools, b);
-    gbyte* act_cur = B.act(parity);
+    gbyte* act_cur = B.act(round & 1);
     if (act_cur[v] == 0) return;
     if (lane == 0) act_cur[v] = 0;
-    relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+    relax_visit_any<INC>(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
 }
 
 // Frontier worklists (default for sparse graphs): the active destinations of each batch for
@@ -525,10 +681,11 @@ __device__ __forceinline__ int32_t wl_batch(const int64_t* __restrict__ prefix, 
 // one wave per listed (vertex, batch): the T items of all batches in batch-major order
 // (prefix[b] = items before batch b), XCD x (block % 8) takes the contiguous slice
 // [x*S, (x+1)*S) -- a batch's state stays in one XCD's L2, as with xcd_tile
+template <bool INC>
 __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                   const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                   const int64_t* __restrict__ out_ptr,
-                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t parity,
+                                                  const int32_t* __restrict__ out_dst, Pools pools, int32_t round,
                                                   const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
                                                   int32_t nb, int64_t S, int32_t* __restrict__ cnt,
                                                   unsigned long long* __restrict__ prof) {
@@ -543,10 +700,10 @@ __global__ __launch_bounds__(256) void k_relax_wl(const int64_t* __restrict__ in
     // SGPRs, as in k_relax, instead of occupying VGPRs (84 -> occupancy 5 of 8)
     const int32_t v = __builtin_amdgcn_readfirstlane(wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x);
     const BatchDev B = batch_view(pools, b);
-    relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+    relax_visit_any<INC>(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
     // cleared after the visit (this round sets only the other parity's flags): a store ahead
     // of the arc-list loads would keep them off the scalar unit (they could alias it)
-    if (lane == 0) B.act(parity)[v] = 0;
+    if (lane == 0) B.act(round & 1)[v] = 0;
 }
 
 // Device-driven worklist rounds (graphs whose batches x vertices fit OPT_DEVICE_ROUNDS'
@@ -599,10 +756,11 @@ __global__ __launch_bounds__(256) void k_scan_wl(uint32_t* __restrict__ wlcnt, i
 // virtual grid of k_relax instead -- block vb = blockIdx.x + k * gridDim.x, the same XCD
 // (vb % 8) and xcd_tile mapping, one activity flag per (vertex, batch): a worklist entry load
 // in front of every visit made these rounds 22-25 % slower (r04l, C4 groups of 20 / 40 batches)
+template <bool INC>
 __global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ in_ptr, const int32_t* __restrict__ in_src,
                                                    const double* __restrict__ in_w, const double* __restrict__ in_r,
                                                    const int64_t* __restrict__ out_ptr,
-                                                   const int32_t* __restrict__ out_dst, Pools pools, int32_t parity,
+                                                   const int32_t* __restrict__ out_dst, Pools pools, int32_t round,
                                                    const int4* __restrict__ wl, const int64_t* __restrict__ prefix,
                                                    int32_t nb, int32_t* __restrict__ cnt,
                                                    unsigned long long* __restrict__ prof, int32_t V) {
@@ -619,9 +777,9 @@ __global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ i
             const int32_t v = vt * 4 + wave;
             if (v >= V) continue;
             const BatchDev B = batch_view(pools, b);
-            gbyte* act_cur = B.act(parity);
+            gbyte* act_cur = B.act(round & 1);
             if (act_cur[v] == 0) continue;
-            relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
+            relax_visit_any<INC>(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
             if (lane == 0) act_cur[v] = 0;  // cleared after the visit, as k_relax_wl does
         }
         return;
@@ -635,8 +793,8 @@ __global__ __launch_bounds__(256) void k_relax_wlp(const int64_t* __restrict__ i
         const int32_t b = __builtin_amdgcn_readfirstlane(wl_batch(prefix, nb, i, lane));
         const int32_t v = __builtin_amdgcn_readfirstlane(wl[(size_t)b * pools.Vp + (size_t)(i - prefix[b])].x);
         const BatchDev B = batch_view(pools, b);
-        relax_visit(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, parity, cnt, prof);
-        if (lane == 0) B.act(parity)[v] = 0;
+        relax_visit_any<INC>(in_ptr, in_src, in_w, in_r, out_ptr, out_dst, B, b, v, lane, round, cnt, prof);
+        if (lane == 0) B.act(round & 1)[v] = 0;
     }
 }
 
@@ -3330,6 +3488,8 @@ struct shadowtopo_engine {
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
+    int32_t opt_csr_incremental = 32; // OPT_CSR_INCREMENTAL: lean visits of vertices with more in-arcs than this
+                                      // read only the tails changed since (0 = off)
     int32_t opt_walk_tpw = 1;         // k_walk shape (OPT_WALK_TPW): 1 target / 1 chain, or 2 / 2
     uint32_t* d_bweight[4] = {nullptr, nullptr, nullptr, nullptr};  // per part: chunk counts per block
     int32_t* d_border[4][2] = {};     // per part: two order buffers (ping-pong across sweeps)
@@ -3456,6 +3616,7 @@ int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
     if ((rc = eng->lean_next ? dev_alloc(eng->batch_allocs, (void**)&P.P32, VK * nb * sizeof(int32_t))
                              : dev_alloc(eng->batch_allocs, (void**)&P.Q, VK * nb * sizeof(Rec))) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.act, (size_t)pvp * 2 * nb)) ||
+        (eng->lean_next && (rc = dev_alloc(eng->batch_allocs, (void**)&P.stamp, (size_t)pvp * nb))) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.srcv, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.row, sizeof(int32_t) * KL * nb)) ||
         (rc = dev_alloc(eng->batch_allocs, (void**)&P.err, sizeof(unsigned long long) * (nb + 1))))
@@ -3565,6 +3726,7 @@ Pools pools_from(const Pools& in, int32_t b0) {
     P.D += o;
     if (P.Q) P.Q += o;
     if (P.P32) P.P32 += o;
+    if (P.stamp) P.stamp += (size_t)b0 * P.Vp;
     P.act += (size_t)b0 * 2 * P.Vp;
     P.srcv += (size_t)b0 * KL;
     P.row += (size_t)b0 * KL;
@@ -3902,6 +4064,11 @@ int run_push_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
 int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     const GraphDev& g = eng->rg ? *eng->rg : eng->g;
     const int32_t V = g.V;
+    // incremental lean rounds (OPT_CSR_INCREMENTAL): k_init / k_seed set the change stamps the
+    // relax kernels' batch views then carry
+    eng->pools.inc = eng->pools.P32 && eng->pools.stamp && !eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_FULL
+                         ? eng->opt_csr_incremental
+                         : 0;
     if (!eng->dense && eng->opt_csr_variant == SHADOWTOPO_CSR_PUSH && eng->d_wl) return run_push_rounds(eng, nbg, s);
     const bool fused_seed = eng->dense && eng->opt_dense_seed && eng->d_WR && eng->pools.D32 && eng->pools.BDU && eng->pools.chm;
     // dense: the first spec_rounds rounds are enqueued back to back, with no host read-back
@@ -4001,9 +4168,14 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             for (int64_t round = r0; round < r0 + DEV_K; ++round) {
                 int32_t* cnt_cur = eng->d_cnt + (round & 1) * eng->nb_cap;  // written, not read back
                 if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0)], s));
-                hipLaunchKernelGGL(k_relax_wlp, dim3(G), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r, g.out_ptr,
-                                   g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl, eng->d_wlpre, nbg, cnt_cur,
-                                   eng->d_prof, V);
+                if (eng->pools.inc)
+                    hipLaunchKernelGGL(k_relax_wlp<true>, dim3(G), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
+                                       g.out_ptr, g.out_dst, eng->pools, (int32_t)round, eng->d_wl, eng->d_wlpre, nbg,
+                                       cnt_cur, eng->d_prof, V);
+                else
+                    hipLaunchKernelGGL(k_relax_wlp<false>, dim3(G), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
+                                       g.out_ptr, g.out_dst, eng->pools, (int32_t)round, eng->d_wl, eng->d_wlpre, nbg,
+                                       cnt_cur, eng->d_prof, V);
                 if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_dev[2 * (round - r0) + 1], s));
                 hipLaunchKernelGGL(k_compact, dim3((uint32_t)ncb, nbg), dim3(256), 0, s, eng->pools, V,
                                    (int32_t)((round + 1) & 1), eng->d_wl, eng->d_wlcnt, g.in_ptr);
@@ -4247,14 +4419,24 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             eng->st.relax_batches += nbg;
             eng->st.wl_launches++;
             const int64_t S = (wl_total + 8 * 4 - 1) / (8 * 4) * 4;  // items per XCD slice, whole blocks
-            hipLaunchKernelGGL(k_relax_wl, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
-                               g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)(round & 1), eng->d_wl,
-                               eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
+            if (eng->pools.inc)
+                hipLaunchKernelGGL(k_relax_wl<true>, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src,
+                                   g.in_w, g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)round, eng->d_wl,
+                                   eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
+            else
+                hipLaunchKernelGGL(k_relax_wl<false>, grid_of(eng, 8 * (S / 4)), dim3(256), 0, s, g.in_ptr, g.in_src,
+                                   g.in_w, g.in_r, g.out_ptr, g.out_dst, eng->pools, (int32_t)round, eng->d_wl,
+                                   eng->d_wlpre, nbg, S, cnt_cur, eng->d_prof);
         } else {
             eng->st.relax_batches += nbg;
-            hipLaunchKernelGGL(k_relax, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w, g.in_r,
-                               g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)(round & 1), cnt_cur,
-                               eng->d_prof);
+            if (eng->pools.inc)
+                hipLaunchKernelGGL(k_relax<true>, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                                   g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)round, cnt_cur,
+                                   eng->d_prof);
+            else
+                hipLaunchKernelGGL(k_relax<false>, grid_of(eng, nblocks), dim3(256), 0, s, g.in_ptr, g.in_src, g.in_w,
+                                   g.in_r, g.out_ptr, g.out_dst, eng->pools, V, nbg, nvb, (int32_t)round, cnt_cur,
+                                   eng->d_prof);
         }
         HIP_TRY(hipGetLastError());
         if (eng->opt_timing && !chained) HIP_TRY(hipEventRecord(e1, s));
@@ -5863,6 +6045,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_CSR_LEAN:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "CSR lean must be 0, 1 or 2");
             eng->opt_csr_lean = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_CSR_INCREMENTAL:
+            if (value < 0 || value > (1 << 20)) return fail(SHADOWTOPO_EINVAL, "CSR incremental must be in [0, 2^20]");
+            eng->opt_csr_incremental = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_PART0_PERMILLE:
             if (value < 1 || value > 999) return fail(SHADOWTOPO_EINVAL, "part 0 share must be in [1, 999] per mille");

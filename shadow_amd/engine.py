@@ -56,6 +56,7 @@ OPT_DENSE_SPEC = 21  # dense: leading rounds enqueued without a host read-back (
 OPT_DELTA_LIVE = 19  # dense delta rounds over live-chunk lists: 2 when sparse (default), 1 always, 0 never
 OPT_WALK_TPW = 28  # path walks: 1 target per wave, one walk per lane (1, default) or 2 targets, two walks per lane (2)
 OPT_CSR_LEAN = 30  # sparse rounds: lean D + predecessor state and a walk per pair (1), tree fold (0), auto (2, default)
+OPT_CSR_INCREMENTAL = 31  # lean rounds: visits of vertices with more than n in-arcs re-read only fresh tails (default 32, 0 = off)
 OPT_PART0_PERMILLE = 29  # two sweep parts: part 0's share of the batches, per mille (default 562)
 OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order
 # testing: the failure paths a convergence bug or a full device would take (SHADOWTOPO_EINTERNAL /

@@ -41,16 +41,23 @@ def _case(case):
 CASES = ["sparse", "directed", "ties", "int_random", "vloss_prefer", "no_loops", "multigraph"]
 
 
-@pytest.mark.parametrize("lean", [0, 1])
+# the sparse round state: the tree fold inside the rounds, lean rounds + a walk per pair, and
+# lean rounds whose visits re-read only the tails changed since (OPT_CSR_INCREMENTAL; 1: every
+# vertex with more than one in-arc, so the small graphs here take the incremental visit)
+MODES = {"tree": dict(csr_lean=0), "lean": dict(csr_lean=1, csr_incremental=0),
+         "inc": dict(csr_lean=1, csr_incremental=1)}
+
+
+@pytest.mark.parametrize("lean", list(MODES))
 @pytest.mark.parametrize("worklist", [1, 2])
 @pytest.mark.parametrize("case", CASES)
 def test_csr_rounds(case, worklist, lean):
-    """default schedule (worklists when under half the pairs are active) and always-worklist;
-    the tree fold inside the rounds (lean 0) and the lean rounds + a walk per pair (lean 1)"""
+    """default schedule (worklists when under half the pairs are active) and always-worklist,
+    in every round-state mode"""
     g = _case(case)
-    st = compare(g, layout="csr", worklist=worklist, csr_lean=lean)
+    st = compare(g, layout="csr", worklist=worklist, **MODES[lean])
     assert st["dense"] == 0
-    assert (st["lean_groups"] > 0) == (lean == 1)
+    assert (st["lean_groups"] > 0) == (lean != "tree")
 
 
 def test_csr_removed_variants_rejected():
@@ -73,7 +80,7 @@ def test_csr_full_grid_without_worklists(case):
     compare(g, layout="csr", worklist=1, batches_in_flight=2)
 
 
-@pytest.mark.parametrize("lean", [0, 1])
+@pytest.mark.parametrize("lean", list(MODES))
 @pytest.mark.parametrize("worklist", [0, 1, 2])
 def test_csr_two_dimensional_grids(worklist, lean):
     """grids past 2^24 blocks (C5: 102 batches x 868k vertices = 22M blocks of 256) go 2-D
@@ -81,14 +88,14 @@ def test_csr_two_dimensional_grids(worklist, lean):
     blocks, and a round that dropped a batch could end the iteration early); forcing the
     2-D form on every launch of a small graph must give the same matrices"""
     g = synth.random_sparse(V=400, avg_deg=5, seed=38)
-    compare(g, layout="csr", worklist=worklist, grid_x=64, csr_lean=lean)
+    compare(g, layout="csr", worklist=worklist, grid_x=64, **MODES[lean])
 
 
-@pytest.mark.parametrize("lean", [0, 1])
+@pytest.mark.parametrize("lean", list(MODES))
 @pytest.mark.parametrize("worklist", [0, 1])
 def test_csr_several_groups(worklist, lean):
     g = synth.random_sparse(V=500, avg_deg=4, seed=37)
-    compare(g, layout="csr", batches_in_flight=3, worklist=worklist, csr_lean=lean)  # 8 batches -> 3 groups
+    compare(g, layout="csr", batches_in_flight=3, worklist=worklist, **MODES[lean])  # 8 batches -> 3 groups
 
 
 @pytest.mark.parametrize("case", ["sparse", "ties", "vloss_prefer", "multigraph", "directed"])
@@ -109,6 +116,33 @@ def test_lean_rounds_long_paths_and_auto(case):
                           rng.uniform(0, 0.05, keep.sum()), np.arange(0, V, 7, dtype=np.int32))
     chain.vertex_packetloss = np.where(rng.random(V) < 0.5, rng.uniform(0, 0.05, V), np.nan)
     compare(chain, layout="csr", csr_lean=1)
+    compare(chain, layout="csr", csr_lean=1, csr_incremental=1)
+
+
+def _long_chain(V, seed, chords=2):
+    """a path with a few chords: the rounds run about as many rounds as the path is long"""
+    rng = np.random.default_rng(seed)
+    src = np.concatenate([np.arange(V - 1), rng.integers(0, V, chords)]).astype(np.int32)
+    dst = np.concatenate([np.arange(1, V), rng.integers(0, V, chords)]).astype(np.int32)
+    keep = src != dst
+    lat = rng.uniform(1, 5, keep.sum())
+    lat[: V // 3] = np.round(lat[: V // 3])  # integer latencies on a stretch: ties through the chords
+    return synth._finish("chain", V, src[keep], dst[keep], lat, rng.uniform(0, 0.05, keep.sum()),
+                         np.arange(0, V, 7, dtype=np.int32))
+
+
+@pytest.mark.parametrize("sched", ["grid", "worklist", "device"])
+def test_incremental_rounds_past_stamp_wrap(sched):
+    """incremental lean rounds (OPT_CSR_INCREMENTAL) stamp each change with the round mod 256:
+    on a 1200-vertex chain the rounds run past the wrap (a stale stamp that matches again
+    only costs a re-read), over every schedule and several batch groups, bit-exact against
+    the oracle and the non-incremental lean rounds"""
+    g = _long_chain(1200, seed=12)
+    opts = {"grid": dict(worklist=0), "worklist": dict(worklist=1, device_rounds=0),
+            "device": dict(worklist=1, device_rounds=2)}[sched]
+    st = compare(g, layout="csr", csr_lean=1, csr_incremental=1, batches_in_flight=1, **opts)
+    assert st["rounds"] > 300 and st["lean_groups"] > 1, (st["rounds"], st["lean_groups"])
+    compare(g, layout="csr", csr_lean=1, csr_incremental=0, batches_in_flight=1, **opts)
 
 
 @pytest.mark.parametrize("case", ["ties", "sparse", "int_random", "directed"])

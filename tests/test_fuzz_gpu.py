@@ -45,8 +45,10 @@ def _case(seed):
     if rng.random() < 0.4:
         opts["batches_in_flight"] = int(rng.integers(1, 3))
     lean = int(rng.integers(0, 3))  # drawn last: the draws above are the r04 sweep's
+    inc = int(rng.choice([0, 1, 8]))  # incremental lean visits (r05), drawn after everything else
     if layout != "dense" and opts.get("csr_variant") != 2:
         opts["csr_lean"] = lean
+        opts["csr_incremental"] = inc
     return g, layout, opts
 
 
@@ -77,6 +79,7 @@ def _big_case(seed):
         g = synth.integer_grid(rows=int(rng.integers(10, 30)), cols=int(rng.integers(10, 30)), seed=int(rng.integers(1 << 20)))
     opts = {"batches_in_flight": int(rng.integers(1, 4))} if rng.random() < 0.5 else {}
     opts["csr_lean"] = int(rng.integers(0, 3))  # (dense graphs ignore it)
+    opts["csr_incremental"] = int(rng.choice([0, 1, 8]))
     return g, opts
 
 
