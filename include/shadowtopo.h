@@ -148,6 +148,10 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               re-reads only the in-arcs whose tail's distance changed in the last two
                                               rounds (a per-(vertex, batch) change stamp), starting from the stored
                                               state (default 32); 0 = every in-arc. Results are identical. */
+#define SHADOWTOPO_OPT_SPEC_COMPOSE 33      /* dense rounds: 1 (default) = the pair compose is enqueued behind each delta
+                                              round, before its read-back, and kept when that round changed nothing
+                                              (one host round trip fewer per computation); 0 = after convergence.
+                                              Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
@@ -239,6 +243,8 @@ typedef struct shadowtopo_stats {
     double attach_prep_ms;   /* host wall time in compute calls of the work a new attached set needs first: the
                                 relaxation view, the walk list and arc table, the pools, the source order */
     int64_t lean_groups;     /* batch groups computed with lean sparse rounds (OPT_CSR_LEAN) */
+    int64_t spec_composes;   /* dense: composes enqueued behind the round that found convergence (OPT_SPEC_COMPOSE) */
+    int64_t spec_composes_lost; /* dense: such composes redone because that round still changed pairs */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

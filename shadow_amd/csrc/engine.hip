@@ -3488,6 +3488,9 @@ struct shadowtopo_engine {
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
+    int32_t opt_spec_compose = 1;     // OPT_SPEC_COMPOSE: dense compose enqueued behind a delta round (1)
+    unsigned long long* h_masks = nullptr;  // pinned: the compose's error word and tie masks, read back
+    size_t h_masks_n = 0;
     int32_t opt_csr_incremental = 32; // OPT_CSR_INCREMENTAL: lean visits of vertices with more in-arcs than this
                                       // read only the tails changed since (0 = off)
     int32_t opt_walk_tpw = 1;         // k_walk shape (OPT_WALK_TPW): 1 target / 1 chain, or 2 / 2
@@ -4060,8 +4063,14 @@ int run_push_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
     return SHADOWTOPO_OK;
 }
 
-// relax rounds for the batch slots [0, nbg) until no vertex changes
-int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
+// relax rounds for the batch slots [0, nbg) until no vertex changes.  spec_compose (dense
+// rounds): enqueued behind a delta round, before that round's read-back, so that the round
+// that finds convergence (C2: the third) needs no second host round trip for the compose;
+// *composed tells the caller whether the last enqueued compose saw the converged state (a
+// compose behind a round that still changed pairs is redone, its masks and error word reset)
+int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s, const std::function<int()>* spec_compose = nullptr,
+               bool* composed = nullptr) {
+    if (composed) *composed = false;
     const GraphDev& g = eng->rg ? *eng->rg : eng->g;
     const int32_t V = g.V;
     // incremental lean rounds (OPT_CSR_INCREMENTAL): k_init / k_seed set the change stamps the
@@ -4454,6 +4463,11 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipMemcpyAsync(eng->h_wlcnt, eng->d_wlcnt, sizeof(uint32_t) * nbg, hipMemcpyDeviceToHost, s));
         }
+        // a dense delta round is usually the last: the compose goes behind it, read back with it
+        const bool spec_c = spec_compose && eng->dense && !round_full && round >= 1;
+        if (spec_c) {
+            if (int rc2 = (*spec_compose)()) return rc2;
+        }
         if (eng->dense && round == spec_rounds && spec_rounds > 0) {
             // the counts of every round since the seed, rows 1 .. spec_rounds + 1, in one copy
             HIP_TRY(hipMemcpyAsync(eng->h_cnt_spec, cnt_row(0), sizeof(int32_t) * eng->nb_cap * (spec_rounds + 1),
@@ -4538,7 +4552,11 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s) {
                     (long long)changed, ms);
         }
         if (eng->dense && eng->opt_profile) eng->st.changes += changed;  // changed (vertex, source) pairs
-        if (changed == 0) break;
+        if (changed == 0) {
+            if (spec_c && composed) *composed = true;
+            break;
+        }
+        if (spec_c) eng->st.spec_composes_lost++;
     }
     }  // host-driven rounds
     if (eng->d_prof) {
@@ -5222,10 +5240,41 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                                hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(eng->pools.row, eng->h_row.data(), sizeof(int32_t) * KL * nbg,
                                hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemsetAsync(eng->pools.err, 0, sizeof(unsigned long long) * (nbg + 1), s));
+        // the pair compose (+ path walks) and the read-back of the tie-tainted sources (masks[1 + b])
+        // and the walks' error word (masks[0]), into pinned host memory
+        if (eng->h_masks_n < (size_t)nbg + 1) {
+            if (eng->h_masks) (void)hipHostFree(eng->h_masks);
+            eng->h_masks = nullptr;
+            eng->h_masks_n = 0;
+            HIP_TRY(hipHostMalloc((void**)&eng->h_masks, sizeof(unsigned long long) * (nb + 1), hipHostMallocDefault));
+            eng->h_masks_n = (size_t)nb + 1;
+        }
+        const std::function<int()> enqueue_compose = [&]() -> int {
+            HIP_TRY(hipMemsetAsync(eng->pools.err, 0, sizeof(unsigned long long) * (nbg + 1), s));
+            if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[0], s));
+            if (A > 0) {
+                hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(COMPOSE_T), 0, s, *eng->rg, eng->pools,
+                                   d_att_r, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
+                                   eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
+                HIP_TRY(hipGetLastError());
+                if (eng->pools.P32) {  // lean rounds: every shortest-path pair's hops, rel and taint
+                    HIP_TRY(launch_walk_lean(eng, nbg, d_att_r, A, dl, dr, dh, row_base, ls, s));
+                } else if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
+                    HIP_TRY(launch_walk(eng, nbg, d_att_r, A, dl, dr, row_base, ls, s));
+                }
+            }
+            if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[1], s));
+            HIP_TRY(hipMemcpyAsync(eng->h_masks, eng->pools.err, sizeof(unsigned long long) * (nbg + 1),
+                                   hipMemcpyDeviceToHost, s));
+            return SHADOWTOPO_OK;
+        };
+        bool composed = false;
         if (!complete) {
             eng->unconverged = false;
-            if ((rc = run_rounds(eng, nbg, s))) return rc;
+            // speculative compose behind the dense delta rounds (not with the testing options
+            // that act between the rounds and the compose)
+            const bool spec = eng->opt_spec_compose && !eng->opt_test_scramble && !eng->opt_test_unconverged;
+            if ((rc = run_rounds(eng, nbg, s, spec ? &enqueue_compose : nullptr, &composed))) return rc;
             // testing options: compose the state an iteration guard stopped at (every stream of
             // the device drained first: the rounds may have left work on the part streams), or
             // a scrambled tree
@@ -5237,24 +5286,13 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             }
         }
         auto t0 = std::chrono::steady_clock::now();
-        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[0], s));
-        if (A > 0) {
-            hipLaunchKernelGGL(k_compose, dim3((A + 63) / 64, nbg), dim3(COMPOSE_T), 0, s, *eng->rg, eng->pools,
-                               d_att_r, A, eng->d_self_lat, eng->d_self_rel, eng->d_self_hops,
-                               eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
-            HIP_TRY(hipGetLastError());
-            if (eng->pools.P32) {  // lean rounds: every shortest-path pair's hops, rel and taint
-                HIP_TRY(launch_walk_lean(eng, nbg, d_att_r, A, dl, dr, dh, row_base, ls, s));
-            } else if (eng->n_walk > 0) {  // the reference's full fold where the tree's is not it
-                HIP_TRY(launch_walk(eng, nbg, d_att_r, A, dl, dr, row_base, ls, s));
-            }
+        if (!composed) {
+            if ((rc = enqueue_compose())) return rc;
+            HIP_TRY(round_sync(eng, s));
+        } else {
+            eng->st.spec_composes++;
         }
-        if (eng->opt_timing) HIP_TRY(hipEventRecord(eng->ev_cmp[1], s));
-        // collect tie-tainted sources (masks[1 + b]) and the path walks' error word (masks[0])
-        std::vector<unsigned long long> masks((size_t)nbg + 1);
-        HIP_TRY(hipMemcpyAsync(masks.data(), eng->pools.err, sizeof(unsigned long long) * (nbg + 1),
-                               hipMemcpyDeviceToHost, s));
-        HIP_TRY(round_sync(eng, s));
+        const unsigned long long* masks = eng->h_masks;
         eng->st.compose_ms +=
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (eng->opt_timing) {
@@ -5885,6 +5923,7 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
         if (e) (void)hipEventDestroy(e);
     for (auto e : eng->ev_cmp)
         if (e) (void)hipEventDestroy(e);
+    if (eng->h_masks) (void)hipHostFree(eng->h_masks);
     if (eng->copy_stream) (void)hipStreamSynchronize(eng->copy_stream);
     for (int k = 0; k < 2; ++k) {
         if (eng->ev_comp[k]) (void)hipEventDestroy(eng->ev_comp[k]);
@@ -6045,6 +6084,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_CSR_LEAN:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "CSR lean must be 0, 1 or 2");
             eng->opt_csr_lean = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SPEC_COMPOSE:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "speculative compose must be 0 or 1");
+            eng->opt_spec_compose = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_CSR_INCREMENTAL:
             if (value < 0 || value > (1 << 20)) return fail(SHADOWTOPO_EINVAL, "CSR incremental must be in [0, 2^20]");

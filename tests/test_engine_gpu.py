@@ -564,6 +564,37 @@ def test_dense_rounds_without_read_back(case, spec):
     assert st0["delta_sweeps"] == 0
 
 
+@pytest.mark.parametrize("on", [0, 1])
+@pytest.mark.parametrize("spec", [0, 2])
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_multigraph", "several_groups"])
+def test_dense_speculative_compose(case, spec, on):
+    """OPT_SPEC_COMPOSE: the compose enqueued behind every dense delta round before its
+    read-back, kept when that round changed nothing and redone (masks and error word reset)
+    when it did -- including path walks over a state that had not converged yet (vertex loss,
+    a multigraph), whose error word must not survive -- bit-exact against the oracle"""
+    if case == "geometric":
+        g = synth.geometric_complete_ish(V=900, A=200)
+    elif case == "ties":
+        g = synth.integer_grid(rows=11, cols=12, seed=6)
+    elif case == "several_groups":
+        g = synth.geometric_complete_ish(V=700, A=300, drop=0.2)
+    else:
+        g = synth.random_sparse(V=220, avg_deg=8, seed=17, vloss=np.where(np.arange(220) % 3 == 0, 0.03, np.nan))
+        rng = np.random.default_rng(4)
+        pick = rng.choice(np.nonzero(g.src != g.dst)[0], 30, replace=False)
+        g.src = np.concatenate([g.src, g.dst[pick]])
+        g.dst = np.concatenate([g.dst, g.src[pick]])
+        g.latency = np.concatenate([g.latency, g.latency[pick] * rng.uniform(0.5, 1.5, 30)])
+        g.packetloss = np.concatenate([g.packetloss, rng.uniform(0, 0.05, 30)])
+    opts = dict(batches_in_flight=2) if case == "several_groups" else {}
+    st = compare(g, layout="dense", dense_spec=spec, spec_compose=on, **opts)
+    assert st["dense"] == 1
+    if not on:
+        assert st["spec_composes"] == 0 and st["spec_composes_lost"] == 0
+    elif case != "ties":
+        assert st["spec_composes"] > 0, st
+
+
 @pytest.mark.parametrize("tb", [1, 2, 4])
 @pytest.mark.parametrize("case", ["geometric", "geometric_odd", "ties"])
 def test_dense_batches_per_wave(case, tb):
