@@ -152,6 +152,8 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               round, before its read-back, and kept when that round changed nothing
                                               (one host round trip fewer per computation); 0 = after convergence.
                                               Results are identical. */
+#define SHADOWTOPO_OPT_SPIN_US 35           /* host waits on the device (between rounds, for the compose) poll for up to this
+                                              many microseconds before a blocking wait (default 20000) */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL

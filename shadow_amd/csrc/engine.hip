@@ -3488,6 +3488,8 @@ struct shadowtopo_engine {
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
+    int32_t opt_spin_us = 20000;      // OPT_SPIN_US: host waits poll this long before a blocking wait (a blocking
+                                      // wait's wake-up cost C3's host-delivered build 13 ms of 31, r05c3t)
     int32_t opt_spec_compose = 1;     // OPT_SPEC_COMPOSE: dense compose enqueued behind a delta round (1)
     unsigned long long* h_masks = nullptr;  // pinned: the compose's error word and tie masks, read back
     size_t h_masks_n = 0;
@@ -3668,17 +3670,23 @@ int ensure_replay(shadowtopo_engine* eng) {
 // total; the budget is 55 % of the free HBM (MI355X: 288 GB) beside the resident graph, never
 // under 24 GB (times the share) -- a floor that holds every requested batch skips the query
 // only when it is itself within the device's capacity.
-// The host's wait between rounds (a round's counts decide the next launch): polls an event
-// for up to 200 us before falling back to a blocking wait.  A blocking synchronisation
-// sleeps, and its wake-up added tens of microseconds to each of a C2 step's 4 waits.
+// The host's waits on the device (a round's counts decide the next launch; the copy stream's
+// last rows): poll an event for up to opt_spin_us (default 20 ms) before falling back to a
+// blocking wait.  A blocking synchronisation sleeps, and its wake-up added tens of
+// microseconds to each of a C2 step's waits and ~0.4 ms to each of C3's host-delivered
+// build's ~30 waits beside the row copies (31 -> 18 ms with a 5 ms budget, r05c3t).
+hipError_t spin_event(const shadowtopo_engine* eng, hipEvent_t ev) {
+    hipError_t e;
+    const auto t0 = std::chrono::steady_clock::now();
+    while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(eng->opt_spin_us)) return hipEventSynchronize(ev);
+    }
+    return e;
+}
 hipError_t round_sync(shadowtopo_engine* eng, hipStream_t s) {
     hipError_t e = hipEventRecord(eng->ev_spin, s);
     if (e != hipSuccess) return e;
-    const auto t0 = std::chrono::steady_clock::now();
-    while ((e = hipEventQuery(eng->ev_spin)) == hipErrorNotReady) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) return hipEventSynchronize(eng->ev_spin);
-    }
-    return e;
+    return spin_event(eng, eng->ev_spin);
 }
 
 int32_t default_nb(shadowtopo_engine* eng, int32_t rows) {
@@ -5369,7 +5377,10 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         eng->st.groups++;
         eng->st.group_batches = std::max<int64_t>(gidx == 0 ? 0 : eng->st.group_batches, nbg);
     }
-    if (pinned_out) HIP_TRY(hipStreamSynchronize(eng->copy_stream));
+    if (pinned_out) {  // the last group's rows have left
+        HIP_TRY(hipEventRecord(eng->ev_spin, eng->copy_stream));
+        HIP_TRY(spin_event(eng, eng->ev_spin));
+    }
     return SHADOWTOPO_OK;
 }
 
@@ -6084,6 +6095,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_CSR_LEAN:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "CSR lean must be 0, 1 or 2");
             eng->opt_csr_lean = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SPIN_US:
+            if (value < 0 || value > 10000000) return fail(SHADOWTOPO_EINVAL, "spin must be in [0, 1e7] us");
+            eng->opt_spin_us = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SPEC_COMPOSE:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "speculative compose must be 0 or 1");
