@@ -5345,7 +5345,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                                    eng->d_self_kind, dl, dr, dh, dk, row_base, ls);
                 HIP_TRY(hipGetLastError());
             }
-            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(round_sync(eng, s));
             eng->st.replayed_sources += (int64_t)jobs.size();
             eng->st.replay_ms +=
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
@@ -5369,7 +5369,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
             if (pinned_out)
                 HIP_TRY(hipEventRecord(eng->ev_copy[slot], cs));
             else
-                HIP_TRY(hipStreamSynchronize(s));
+                HIP_TRY(hipStreamSynchronize(s));  // pageable rows: the whole staged copy, host part included
         }
         eng->st.sources += r1 - r0;
         eng->st.batches += nbg;
