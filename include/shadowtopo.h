@@ -154,6 +154,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               Results are identical. */
 #define SHADOWTOPO_OPT_SPIN_US 35           /* host waits on the device (between rounds, for the compose) poll for up to this
                                               many microseconds before a blocking wait (default 20000) */
+#define SHADOWTOPO_OPT_HOST_GROUPS 36       /* rows into page-locked host memory: computed in this many batch groups, each
+                                              group's copy behind the next group's rounds; 0 (default) = automatic (one
+                                              group unless the rows outweigh the rounds). Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL

@@ -3488,6 +3488,7 @@ struct shadowtopo_engine {
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
+    int32_t opt_host_groups = 0;      // OPT_HOST_GROUPS: page-locked host rows in this many groups (0: automatic)
     int32_t opt_spin_us = 20000;      // OPT_SPIN_US: host waits poll this long before a blocking wait (a blocking
                                       // wait's wake-up cost C3's host-delivered build 13 ms of 31, r05c3t)
     int32_t opt_spec_compose = 1;     // OPT_SPEC_COMPOSE: dense compose enqueued behind a delta round (1)
@@ -5141,18 +5142,19 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
                             (!hops || is_pinned(hops)) && (!kind || is_pinned(kind));
     int32_t nb = default_nb(eng, row_end - row_begin);
     {
-        // a computation that fits one group would copy all its rows after its last round.
-        // Where the copy outweighs the relaxation it is cut into opt_host_split groups, so
-        // every group's copy but the last runs behind the next group's rounds.  The test is a
-        // row's bytes against the graph's arcs (what a source's rounds walk), calibrated on one
-        // MI355X: C3 (7000 x 17 B per row, 139 k arcs: 0.86 B per arc; 833 MB, 15 ms of PCIe
-        // against 8 ms of rounds) 22.4 -> 19.5 ms in 4 groups (8: 26.4); C4 (0.21 B per arc)
-        // 186 -> 207 ms in 4 groups, its smaller groups' rounds cost more than the copy
+        // a computation that fits one group would copy all its rows after its last round.  Cut
+        // into opt_host_split groups, every group's copy but the last runs behind the next
+        // group's rounds: sparse graphs whose rows are >= 64 MB (r05, with the host waits
+        // polling: C3 25.0 -> 21.4 ms, C4 168 -> 141 ms in 4 groups, 6 / 8 no better; r04's
+        // C4 loss to 4 groups was the blocking waits); dense graphs only when the rows outweigh
+        // the arcs (C2's one sweep of 16 batches: 4.3 ms in one group, 5.4 in two)
         const int32_t need = (row_end - row_begin + KL - 1) / KL;
         const double row_bytes = (double)A * (16 + (hops ? 4 : 0) + (kind ? 1 : 0));
         const double bytes = row_bytes * (row_end - row_begin);
-        if (pinned_out && eng->opt_host_split > 1 && nb >= need && bytes >= 64.0e6 &&
-            row_bytes >= 0.5 * (double)eng->n_arcs)
+        if (pinned_out && eng->opt_host_groups > 0 && nb >= need)  // OPT_HOST_GROUPS: forced
+            nb = std::max(1, (need + eng->opt_host_groups - 1) / eng->opt_host_groups);
+        else if (pinned_out && eng->opt_host_split > 1 && nb >= need && bytes >= 64.0e6 &&
+                 (!eng->dense || row_bytes >= 0.5 * (double)eng->n_arcs))
             nb = std::max(1, (need + eng->opt_host_split - 1) / eng->opt_host_split);
     }
     {
@@ -6095,6 +6097,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_CSR_LEAN:
             if (value < 0 || value > 2) return fail(SHADOWTOPO_EINVAL, "CSR lean must be 0, 1 or 2");
             eng->opt_csr_lean = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_HOST_GROUPS:
+            if (value < 0 || value > 1024) return fail(SHADOWTOPO_EINVAL, "host groups must be in [0, 1024]");
+            eng->opt_host_groups = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SPIN_US:
             if (value < 0 || value > 10000000) return fail(SHADOWTOPO_EINVAL, "spin must be in [0, 1e7] us");

@@ -59,6 +59,7 @@ OPT_CSR_LEAN = 30  # sparse rounds: lean D + predecessor state and a walk per pa
 OPT_CSR_INCREMENTAL = 31  # lean rounds: visits of vertices with more than n in-arcs re-read only fresh tails (default 32, 0 = off)
 OPT_SPEC_COMPOSE = 33  # dense: compose enqueued behind each delta round, kept at convergence (1, default)
 OPT_SPIN_US = 35  # host waits poll this many microseconds before blocking (default 20000)
+OPT_HOST_GROUPS = 36  # page-locked host rows: batch groups (0 = automatic)
 OPT_PART0_PERMILLE = 29  # two sweep parts: part 0's share of the batches, per mille (default 562)
 OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order
 # testing: the failure paths a convergence bug or a full device would take (SHADOWTOPO_EINTERNAL /
