@@ -356,11 +356,10 @@ def test_pinned_host_rows_pipelined(layout):
 
 
 def test_pinned_host_rows_split_into_groups():
-    """A computation that fits one batch group but whose rows outweigh its relaxation (row
-    bytes >= half the graph's arcs, past 64 MB) is cut into host groups
-    (opt_host_split = 4), so its copies overlap the later groups' rounds: 2200 sources of a
-    k-NN graph (82 MB of rows, 35 batches -> 4 groups).  Bit-identical to the pageable path,
-    which computes in one group (fewer rounds)."""
+    """A sparse computation that fits one batch group but whose rows pass 64 MB is cut into
+    host groups (opt_host_split = 4), so its copies overlap the later groups' rounds: 2200
+    sources of a k-NN graph (82 MB of rows, 35 batches -> 4 groups).  Bit-identical to the
+    pageable path, which computes in one group (fewer rounds)."""
     g = synth.knn_geographic(V=2200, k=8, seed=12)
     eng = E.Engine.from_synth(g, layout="csr")
     eng.set_attached(g.attached)
@@ -378,6 +377,26 @@ def test_pinned_host_rows_split_into_groups():
     assert_bitexact("latency", lat, pl)
     assert_bitexact("reliability", rel, pr)
     assert_bitexact("kind", kind, pk)
+
+
+@pytest.mark.parametrize("layout", ["csr", "dense"])
+def test_host_groups_forced(layout):
+    """OPT_HOST_GROUPS: rows into page-locked memory in a forced number of batch groups (each
+    group's copy behind the next group's rounds), bit-identical to the pageable path"""
+    g = synth.random_sparse(V=600, avg_deg=5, seed=53, A=400)
+    eng = E.Engine.from_synth(g, layout=layout)
+    eng.set_option(E.OPT_HOST_GROUPS, 3)
+    eng.set_attached(g.attached)
+    A = len(g.attached)
+    outs = [E.pinned_empty((A, A), np.float64), E.pinned_empty((A, A), np.float64),
+            E.pinned_empty((A, A), np.uint32), E.pinned_empty((A, A), np.uint8)]
+    eng.reset_stats()
+    eng.compute_rows_into(0, A, *outs)
+    assert eng.stats()["groups"] == 3
+    want = eng.compute_rows(0, A, want_kind=True)
+    eng.close()
+    for name, got, w in zip(("latency", "reliability", "hops", "kind"), outs, want):
+        assert_bitexact(name, got, w)
 
 
 def test_row_exchange_with_engine_device_rows():
