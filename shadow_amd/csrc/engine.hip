@@ -5154,8 +5154,12 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         if (pinned_out && eng->opt_host_groups > 0 && nb >= need)  // OPT_HOST_GROUPS: forced
             nb = std::max(1, (need + eng->opt_host_groups - 1) / eng->opt_host_groups);
         else if (pinned_out && eng->opt_host_split > 1 && nb >= need && bytes >= 64.0e6 &&
-                 (!eng->dense || row_bytes >= 0.5 * (double)eng->n_arcs))
-            nb = std::max(1, (need + eng->opt_host_split - 1) / eng->opt_host_split);
+                 (!eng->dense || row_bytes >= 0.5 * (double)eng->n_arcs)) {
+            // groups of at least 24 batches: smaller groups' rounds are latency-bound (C4's
+            // 8-rank share, 20 batches: 23.1 ms in one group, 27.0 in four)
+            const int32_t ng = std::min(eng->opt_host_split, need / 24);
+            if (ng >= 2) nb = (need + ng - 1) / ng;
+        }
     }
     {
         // groups of equal size: C5's 782 batches at 260 per group ran as 260 / 260 / 260 / 2,

@@ -357,10 +357,10 @@ def test_pinned_host_rows_pipelined(layout):
 
 def test_pinned_host_rows_split_into_groups():
     """A sparse computation that fits one batch group but whose rows pass 64 MB is cut into
-    host groups (opt_host_split = 4), so its copies overlap the later groups' rounds: 2200
-    sources of a k-NN graph (82 MB of rows, 35 batches -> 4 groups).  Bit-identical to the
-    pageable path, which computes in one group (fewer rounds)."""
-    g = synth.knn_geographic(V=2200, k=8, seed=12)
+    host groups of at least 24 batches (up to opt_host_split = 4), so its copies overlap the
+    later groups' rounds: 3200 sources of a k-NN graph (174 MB of rows, 50 batches -> 2
+    groups).  Bit-identical to the pageable path, which computes in one group (fewer rounds)."""
+    g = synth.knn_geographic(V=3200, k=8, seed=12)
     eng = E.Engine.from_synth(g, layout="csr")
     eng.set_attached(g.attached)
     A = len(g.attached)
