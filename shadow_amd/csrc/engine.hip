@@ -4579,6 +4579,16 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s, const std::fu
     return SHADOWTOPO_OK;
 }
 
+// landmark distances to a set of vertices: out[r][i] = dist[rows[r]][cols[i]] (rows of V)
+__global__ __launch_bounds__(256) void k_gather_dist(const double* __restrict__ dist, size_t V,
+                                                     const int32_t* __restrict__ rows,
+                                                     const int32_t* __restrict__ cols, int32_t nc,
+                                                     double* __restrict__ out) {
+    const int32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nc) return;
+    out[(size_t)blockIdx.y * nc + i] = dist[(size_t)rows[blockIdx.y] * V + cols[i]];
+}
+
 // Source order for the label-correcting (CSR) rounds.  A batch's wave is active at a vertex
 // when ANY of its 64 sources has a changed in-neighbour there, so 64 scattered sources make
 // every vertex busy in almost every round (C3: 24 visits per vertex and batch).  Sources
@@ -4607,17 +4617,25 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
     int rc;
     if ((rc = ensure_batches(eng, std::max(1, eng->nb_cap)))) return rc;
     const shadowtopo_stats keep = eng->st;
+    // dl[k][i]: the distance from landmark k to cand[i]
     std::vector<std::vector<double>> dl;
     // One batch of up to 64 sampled candidates (cand[0] first, then every (A/64)-th), and
     // farthest-point selection of the NL landmarks among them: each next landmark is the
     // sample farthest (finite) from those chosen so far.  One SSSP batch instead of NL
     // single-source runs one after another (C2 order 15.5 -> ~4 ms); any landmarks give a
-    // valid order, spread ones a local one.
+    // valid order, spread ones a local one.  Two gathers leave the device: the samples'
+    // distances among themselves (the selection), then the chosen landmarks' distances to the
+    // candidates -- not NL whole rows of V distances (C5: 8 x 5 MB, 50 ms of the attach).
     const int32_t S = std::min<int32_t>(KL, A);
-    std::vector<int32_t> samp((size_t)S);
+    std::vector<int32_t> samp((size_t)S), cols((size_t)std::max(A, S));
     for (int32_t i = 0; i < S; ++i) samp[i] = cand[(size_t)((int64_t)i * A / S)];
     double* d_dist = nullptr;
+    double* d_out = nullptr;
+    int32_t *d_rows = nullptr, *d_cols = nullptr;
     HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V * S));
+    HIP_TRY(hipMalloc((void**)&d_out, sizeof(double) * (size_t)std::max(A, S) * std::max(S, NL)));
+    HIP_TRY(hipMalloc((void**)&d_rows, sizeof(int32_t) * (size_t)KL));
+    HIP_TRY(hipMalloc((void**)&d_cols, sizeof(int32_t) * (size_t)std::max(A, S)));
     for (int j = 0; j < KL; ++j) {
         eng->h_srcv[j] = j < S ? vid(samp[j]) : -1;
         eng->h_row[j] = -1;
@@ -4631,25 +4649,54 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
                            nullptr, nullptr, nullptr);
         if (hipGetLastError() != hipSuccess) rc = fail(SHADOWTOPO_EDEVICE, "landmark distances");
     }
-    std::vector<double> mind((size_t)S, HINF);  // each sample's distance from the landmarks so far
-    std::vector<char> taken((size_t)S, 0);
-    for (int32_t li = 0, k = 0; k < NL && li >= 0 && rc == 0; ++k) {
-        dl.emplace_back((size_t)V);
-        if (hipMemcpyAsync(dl.back().data(), d_dist + (size_t)li * V, sizeof(double) * (size_t)V,
-                           hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            rc = fail(SHADOWTOPO_EDEVICE, "landmark distances");
-            break;
-        }
-        taken[li] = 1;
-        double best = -1.0;
-        li = -1;
-        for (int32_t i = 0; i < S; ++i) {
-            mind[i] = std::min(mind[i], dl.back()[vid(samp[i])]);
-            if (!taken[i] && mind[i] < HINF && mind[i] > best) best = mind[i], li = i;
+    // out[r][i] = dist[rows[r]][cols[i]]
+    std::vector<double> G;
+    const auto gather = [&](const std::vector<int32_t>& rows, int32_t nc, std::vector<double>& out) -> int {
+        const int32_t nr = (int32_t)rows.size();
+        out.resize((size_t)nr * nc);
+        if (hipMemcpyAsync(d_rows, rows.data(), sizeof(int32_t) * nr, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(d_cols, cols.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, s) != hipSuccess)
+            return fail(SHADOWTOPO_EDEVICE, "landmark gather");
+        hipLaunchKernelGGL(k_gather_dist, dim3((uint32_t)((nc + 255) / 256), (uint32_t)nr), dim3(256), 0, s, d_dist,
+                           (size_t)V, d_rows, d_cols, nc, d_out);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(out.data(), d_out, sizeof(double) * out.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            round_sync(eng, s) != hipSuccess)
+            return fail(SHADOWTOPO_EDEVICE, "landmark gather");
+        return SHADOWTOPO_OK;
+    };
+    if (rc == 0) {
+        std::vector<int32_t> all((size_t)S);
+        for (int32_t j = 0; j < S; ++j) all[j] = j, cols[j] = vid(samp[j]);
+        rc = gather(all, S, G);  // G[j][i]: sample j to sample i
+    }
+    std::vector<int32_t> land;
+    {
+        std::vector<double> mind((size_t)S, HINF);  // each sample's distance from the landmarks so far
+        std::vector<char> taken((size_t)S, 0);
+        for (int32_t li = 0, k = 0; k < NL && li >= 0 && rc == 0; ++k) {
+            land.push_back(li);
+            taken[li] = 1;
+            double best = -1.0;
+            const int32_t cur = li;
+            li = -1;
+            for (int32_t i = 0; i < S; ++i) {
+                mind[i] = std::min(mind[i], G[(size_t)cur * S + i]);
+                if (!taken[i] && mind[i] < HINF && mind[i] > best) best = mind[i], li = i;
+            }
         }
     }
+    if (rc == 0) {
+        for (int32_t i = 0; i < A; ++i) cols[i] = vid(cand[i]);
+        std::vector<double> H;
+        rc = gather(land, A, H);  // H[k][i]: landmark k to cand[i]
+        for (size_t k = 0; k < land.size() && rc == 0; ++k)
+            dl.emplace_back(H.begin() + (ptrdiff_t)(k * A), H.begin() + (ptrdiff_t)((k + 1) * A));
+    }
     (void)hipFree(d_dist);
+    (void)hipFree(d_out);
+    (void)hipFree(d_rows);
+    (void)hipFree(d_cols);
     eng->st = keep;
     if (rc) return rc;
     if (embed2 && dl.size() >= 3) {
@@ -4659,10 +4706,10 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
             double sum = 0.0;
             int64_t n = 0;
             for (int32_t i = 0; i < A; ++i)
-                if (dl[k][vid(cand[i])] < HINF) sum += dl[k][vid(cand[i])], ++n;
+                if (dl[k][i] < HINF) sum += dl[k][i], ++n;
             const double m = n ? sum / (double)n : 0.0;
             for (int32_t i = 0; i < A; ++i) {
-                const double d = dl[k][vid(cand[i])];
+                const double d = dl[k][i];
                 X[(size_t)i * L + k] = (d < HINF ? d : m) - m;
             }
         }
@@ -4727,12 +4774,12 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
     for (size_t k = 0; k < std::min<size_t>(dl.size(), 3); ++k) {
         double lo = HINF, hi = -HINF;
         for (int32_t i = 0; i < A; ++i) {
-            const double d = dl[k][vid(cand[i])];
+            const double d = dl[k][i];
             if (d < HINF) lo = std::min(lo, d), hi = std::max(hi, d);
         }
         const double span = hi > lo ? hi - lo : 1.0;
         for (int32_t i = 0; i < A; ++i) {
-            const double d = dl[k][vid(cand[i])];
+            const double d = dl[k][i];
             const uint64_t q = d < HINF ? std::min<uint64_t>(qmax, (uint64_t)((d - lo) / span * (double)qmax)) : qmax;
             for (int b = 0; b < QB; ++b) key[i] |= ((q >> b) & 1ull) << (b * 3 + k);
         }
@@ -5080,7 +5127,18 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         eng->st.self_paths += row_end - row_begin;
     }
     const auto t_att = std::chrono::steady_clock::now();
+    // SHADOWTOPO_TRACE_PREP=1: the attached-set preparation's phases on stderr (diagnostics)
+    static const bool trace_prep = getenv("SHADOWTOPO_TRACE_PREP") != nullptr;
+    auto t_ph = t_att;
+    const auto phase = [&](const char* what) {
+        if (!trace_prep) return;
+        const auto t = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(t - t_ph).count();
+        if (ms > 0.05) fprintf(stderr, "[prep] %s %.2f ms\n", what, ms);
+        t_ph = t;
+    };
     if ((rc = ensure_pruned(eng, s))) return rc;
+    phase("pendant view");
     eng->rg = eng->prune_ready ? &eng->gp : &eng->g;  // back to g for sssp (shadowtopo_sssp)
     // lean sparse rounds (D + the predecessor arc, 12 B per pair instead of 24; no predecessor
     // gathers in the rounds; hops, reliability and the taint come from a walk per pair after
@@ -5113,6 +5171,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         eng->walk_ready = true;
     }
     eng->st.walk_targets = eng->n_walk;
+    phase("walk list");
     if ((eng->n_walk > 0 || eng->lean_next) &&
         (eng->arcinfo_of != eng->rg->in_src || eng->arcinfo_gen != eng->view_gen)) {
         // the walks' per-arc table, for the graph the rounds run on (rebuilt with the view)
@@ -5134,6 +5193,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         eng->arcinfo_of = eng->rg->in_src;
         eng->arcinfo_gen = eng->view_gen;
     }
+    phase("arc table");
     // host destinations: rows are composed into device staging and copied out per group;
     // into pinned (page-locked) host memory -- shadowtopo_host_alloc, as the topology shim
     // allocates its matrix -- the copy of group g runs on the copy stream behind group
@@ -5181,6 +5241,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         rc = ensure_batches(eng, nb);
     }
     if (rc) return rc;
+    phase("pools");
     const int32_t group = nb * KL;
     if ((rc = ensure_vperm(eng, s))) return rc;
     // rows of a group go to batch lanes in locality order (CSR rounds, and the pruned dense
@@ -5189,6 +5250,7 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
     const bool order = eng->opt_source_order && (!eng->dense || eng->vperm_ready) && !complete &&
                        row_end - row_begin > KL;
     if (order && (rc = ensure_locality(eng, s))) return rc;
+    phase("source order");
     // host wall time of what depends on the attached set (zero when the set is unchanged)
     eng->st.attach_prep_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_att).count();
     std::vector<int32_t> lane_row;
