@@ -155,6 +155,14 @@ struct Pools {
     int32_t inc;        // incremental lean rounds (OPT_CSR_INCREMENTAL): 0 = off, else the in-degree
                         // above which a visit reads only the fresh tails
 };
+// the pendant-pruned relaxation view's device arrays (ensure_pruned), allocated at the graph's
+// sizes once and refilled per attached set
+struct ViewBufs {
+    int32_t *nid = nullptr, *cnt = nullptr, *loop = nullptr, *att = nullptr, *src = nullptr, *eid = nullptr;
+    int64_t* ptr = nullptr;
+    double *vf = nullptr, *w = nullptr, *r = nullptr;
+    float* w32 = nullptr;
+};
 constexpr int32_t LT_BIT = (int32_t)0x80000000u;  // P32: the predecessor choice here is a heap-order tie
 constexpr int32_t P_MASK = 0x7fffffff;
 constexpr uint8_t STAMP_NONE = 0x80;  // stamp of a vertex no round has changed (a stale match only costs a re-read)
@@ -3374,8 +3382,6 @@ struct shadowtopo_engine {
     int mirrors_rc = 0;
     std::vector<int64_t> h_in_ptr;
     std::vector<int32_t> h_in_src, h_in_eid, h_loop_eid;
-    std::vector<double> h_in_w, h_in_r;  // ensure_pruned's mirrors of the arc weights (sparse graphs)
-    std::vector<float> h_in_w32;
     hipStream_t own_stream = nullptr;
     // attached
     int32_t A = 0;
@@ -3488,6 +3494,8 @@ struct shadowtopo_engine {
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
+    ViewBufs vb;                      // the pendant-pruned view's device buffers (kept across attached sets)
+    size_t view_cap_a = 0;            // attached rows vb.att holds (0: not allocated)
     int32_t opt_host_groups = 0;      // OPT_HOST_GROUPS: page-locked host rows in this many groups (0: automatic)
     int32_t opt_spin_us = 20000;      // OPT_SPIN_US: host waits poll this long before a blocking wait (a blocking
                                       // wait's wake-up cost C3's host-delivered build 13 ms of 31, r05c3t)
@@ -4894,12 +4902,124 @@ bool is_pinned(const void* p) {
 // full graph.  C5: 24 % of the vertices, 11 % of the arcs.
 int ensure_mirrors(shadowtopo_engine* eng);
 
+// the pendant-pruned view on the device.  nid[v]: v's id in the view (-1: peeled).  One wave
+// per vertex: cnt[nid v] = its in-arcs from kept tails
+__global__ __launch_bounds__(256) void k_view_count(const int64_t* __restrict__ in_ptr,
+                                                    const int32_t* __restrict__ in_src,
+                                                    const int32_t* __restrict__ nid, int32_t V,
+                                                    int32_t* __restrict__ cnt) {
+    const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (v >= V) return;
+    const int32_t n = nid[v];
+    if (n < 0) return;
+    int32_t c = 0;
+    for (int64_t e = in_ptr[v] + lane; e < in_ptr[v + 1]; e += 64) c += nid[in_src[e]] >= 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) cnt[n] = c;
+}
+
+// ptr[0] = 0, ptr[i + 1] = cnt[0] + .. + cnt[i] for i < n: one block, a contiguous segment per
+// thread, the segment sums scanned in LDS
+__global__ __launch_bounds__(1024) void k_view_scan(const int32_t* __restrict__ cnt, int32_t n,
+                                                    int64_t* __restrict__ ptr) {
+    __shared__ int64_t sc[1024];
+    const int32_t per = (n + 1023) / 1024;
+    const int32_t b = threadIdx.x * per, e = min(n, b + per);
+    int64_t sum = 0;
+    for (int32_t i = b; i < e; ++i) sum += cnt[i];
+    sc[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int64_t add = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0;
+        __syncthreads();
+        sc[threadIdx.x] += add;
+        __syncthreads();
+    }
+    int64_t run = sc[threadIdx.x] - sum;
+    if (threadIdx.x == 0) ptr[0] = 0;
+    for (int32_t i = b; i < e; ++i) {
+        run += cnt[i];
+        ptr[i + 1] = run;
+    }
+}
+
+// the kept arcs of each kept vertex, in row order (wave per vertex: a ballot prefix per 64 arcs)
+__global__ __launch_bounds__(256) void k_view_fill(const int64_t* __restrict__ in_ptr,
+                                                   const int32_t* __restrict__ in_src,
+                                                   const int32_t* __restrict__ in_eid,
+                                                   const double* __restrict__ in_w,
+                                                   const float* __restrict__ in_w32,
+                                                   const double* __restrict__ in_r,
+                                                   const int32_t* __restrict__ nid, int32_t V,
+                                                   const int64_t* __restrict__ ptr, int32_t* __restrict__ src,
+                                                   int32_t* __restrict__ eid, double* __restrict__ w,
+                                                   float* __restrict__ w32, double* __restrict__ r) {
+    const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (v >= V) return;
+    const int32_t n = nid[v];
+    if (n < 0) return;
+    int64_t o = ptr[n];
+    for (int64_t e0 = in_ptr[v]; e0 < in_ptr[v + 1]; e0 += 64) {
+        const int64_t e = e0 + lane;
+        const int32_t t = e < in_ptr[v + 1] ? nid[in_src[e]] : -1;
+        const unsigned long long m = __ballot(t >= 0);
+        if (t >= 0) {
+            const int64_t q = o + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            src[q] = t;
+            eid[q] = in_eid[e];
+            w[q] = in_w[e];
+            w32[q] = in_w32[e];
+            r[q] = in_r[e];
+        }
+        o += __popcll(m);
+    }
+}
+
+// per-vertex tables in the view's ids, the attached list in them, and the builder's padding
+// arcs after the na0 kept arcs (u = 0, w = +inf)
+__global__ __launch_bounds__(256) void k_view_tables(const double* __restrict__ vfac,
+                                                     const int32_t* __restrict__ loop_eid,
+                                                     const int32_t* __restrict__ nid, int32_t V,
+                                                     const int32_t* __restrict__ attached, int32_t A, int64_t na0,
+                                                     double* __restrict__ vf, int32_t* __restrict__ loop,
+                                                     int32_t* __restrict__ att, int32_t* __restrict__ src,
+                                                     int32_t* __restrict__ eid, double* __restrict__ w,
+                                                     float* __restrict__ w32, double* __restrict__ r) {
+    const int32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < V) {
+        const int32_t n = nid[i];
+        if (n >= 0) {
+            vf[n] = vfac[i];
+            loop[n] = loop_eid[i];
+        }
+    }
+    if (i < A) att[i] = nid[attached[i]];
+    if (i < CSR_PAD) {
+        src[na0 + i] = 0;
+        eid[na0 + i] = -1;
+        w[na0 + i] = dinf();
+        w32[na0 + i] = __int_as_float(0x7f800000);
+        r[na0 + i] = 0.0;
+    }
+}
+
 int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->prune_ready || !eng->opt_prune || eng->dense || (eng->flags & SHADOWTOPO_F_DIRECTED) ||
         (eng->flags & SHADOWTOPO_F_COMPLETE) || eng->n_arcs == 0)
         return SHADOWTOPO_OK;
     int rc;
+    static const bool trace_prep = getenv("SHADOWTOPO_TRACE_PREP") != nullptr;
+    auto t_ph = std::chrono::steady_clock::now();
+    const auto phase = [&](const char* what) {
+        if (!trace_prep) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[prep]   view: %s %.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_ph).count());
+        t_ph = t;
+    };
     if ((rc = ensure_mirrors(eng))) return rc;
+    phase("mirrors");
     const int32_t V = eng->V;
     const int64_t M = eng->n_arcs;
     const std::vector<int64_t>& ptr = eng->h_in_ptr;
@@ -4912,21 +5032,21 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
         deg[v] = (int32_t)(ptr[v + 1] - ptr[v]);
         if (deg[v] <= 1 && !att[v]) stack.push_back(v);
     }
-    int64_t peeled = 0;
+    int64_t peeled = 0, cut = 0;  // cut: edges to kept neighbours the peeled vertices took along
     while (!stack.empty()) {
         const int32_t x = stack.back();
         stack.pop_back();
         if (!keep[x]) continue;
         keep[x] = 0;
         ++peeled;
+        cut += deg[x];  // its kept neighbours now (0 or 1): every other arc left with an earlier peel
         for (int64_t e = ptr[x]; e < ptr[x + 1]; ++e) {
             const int32_t y = src[e];
             if (keep[y] && --deg[y] <= 1 && !att[y]) stack.push_back(y);
         }
     }
     eng->pruned_vertices = peeled;
-    for (void* p : eng->prune_allocs) (void)hipFree(p);
-    eng->prune_allocs.clear();
+    phase("peel");
     eng->h_view_of.clear();
     eng->d_att_view = nullptr;
     eng->view_gen++;
@@ -4943,82 +5063,56 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     int32_t Vc = 0;
     for (int32_t v = 0; v < V; ++v)
         if (keep[v]) nid[v] = Vc++;
-    // the filtered arrays, row order kept, with the builder's padding arcs at the end (the
-    // arc weights come from host mirrors copied once per engine: every attach epoch peels)
-    if (eng->h_in_w.size() != (size_t)M) {
-        eng->h_in_w.resize((size_t)M);
-        eng->h_in_w32.resize((size_t)M);
-        eng->h_in_r.resize((size_t)M);
-        HIP_TRY(hipMemcpy(eng->h_in_w.data(), eng->g.in_w, 8 * (size_t)M, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(eng->h_in_w32.data(), eng->g.in_w32, 4 * (size_t)M, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(eng->h_in_r.data(), eng->g.in_r, 8 * (size_t)M, hipMemcpyDeviceToHost));
+    // the filtered arrays, row order kept, with the builder's padding arcs at the end, built on
+    // the device from the resident in-CSR (k_view_*: 2 ms on C5 where the host built and
+    // uploaded them in 45 ms); the buffers are kept across attached sets at the graph's sizes
+    const int64_t na0 = M - 2 * cut;  // kept arcs: every cut edge was two arcs
+    const size_t na = (size_t)na0 + CSR_PAD;
+    const int32_t A = eng->A;
+    if (eng->view_cap_a < (size_t)std::max(A, 1)) {
+        for (void* p : eng->prune_allocs) (void)hipFree(p);
+        eng->prune_allocs.clear();
+        eng->view_cap_a = 0;
+        ViewBufs& vb = eng->vb;
+        const size_t Mc = (size_t)M + CSR_PAD, Ac = (size_t)std::max(A, 1);
+        if ((rc = dev_alloc(eng->prune_allocs, (void**)&vb.nid, 4 * (size_t)V)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.cnt, 4 * (size_t)V)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.vf, 8 * (size_t)V)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.loop, 4 * (size_t)V)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.att, 4 * Ac)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.ptr, 8 * ((size_t)V + 1))) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.src, 4 * Mc)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.eid, 4 * Mc)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.w, 8 * Mc)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.r, 8 * Mc)) ||
+            (rc = dev_alloc(eng->prune_allocs, (void**)&vb.w32, 4 * Mc)))
+            return rc;
+        eng->view_cap_a = Ac;
     }
-    const std::vector<double>& w = eng->h_in_w;
-    const std::vector<double>& r = eng->h_in_r;
-    const std::vector<float>& w32 = eng->h_in_w32;
-    std::vector<int64_t> nptr((size_t)Vc + 1, 0);
-    std::vector<int32_t> nsrc, neid;
-    std::vector<double> nw, nr;
-    std::vector<float> nw32;
-    nsrc.reserve((size_t)M + CSR_PAD);
-    neid.reserve((size_t)M + CSR_PAD);
-    nw.reserve((size_t)M + CSR_PAD);
-    nr.reserve((size_t)M + CSR_PAD);
-    nw32.reserve((size_t)M + CSR_PAD);
-    for (int32_t v = 0; v < V; ++v) {
-        if (!keep[v]) continue;
-        for (int64_t e = ptr[v]; e < ptr[v + 1]; ++e)
-            if (keep[src[e]]) {  // rows stay sorted by tail: the renumbering keeps the order
-                nsrc.push_back(nid[src[e]]);
-                nw.push_back(w[e]);
-                nw32.push_back(w32[e]);
-                nr.push_back(r[e]);
-                neid.push_back(eng->h_in_eid[e]);
-            }
-        nptr[(size_t)nid[v] + 1] = (int64_t)nsrc.size();
-    }
-    // per-vertex tables the rounds and the pair dispatch read, in the view's ids
-    const std::vector<double>& vf = eng->h_vfac;
-    std::vector<double> nvf((size_t)Vc);
-    std::vector<int32_t> nloop((size_t)Vc), natt((size_t)std::max<int32_t>(1, eng->A));
-    for (int32_t v = 0; v < V; ++v)
-        if (nid[v] >= 0) {
-            nvf[(size_t)nid[v]] = vf[v];
-            nloop[(size_t)nid[v]] = eng->h_loop_eid[v];
-        }
-    for (int32_t i = 0; i < eng->A; ++i) natt[(size_t)i] = nid[eng->h_attached[i]];
-    for (int k = 0; k < CSR_PAD; ++k) {  // graph_build's k_pad
-        nsrc.push_back(0);
-        nw.push_back(std::numeric_limits<double>::infinity());
-        nw32.push_back(std::numeric_limits<float>::infinity());
-        nr.push_back(0.0);
-        neid.push_back(-1);
-    }
+    const ViewBufs& vb = eng->vb;
+    HIP_TRY(hipMemcpyAsync(vb.nid, nid.data(), 4 * (size_t)V, hipMemcpyHostToDevice, s));
+    const GraphDev& g0 = eng->g;
+    const uint32_t wv = (uint32_t)(((int64_t)V + 3) / 4);  // one wave per vertex
+    hipLaunchKernelGGL(k_view_count, dim3(wv), dim3(256), 0, s, g0.in_ptr, g0.in_src, vb.nid, V, vb.cnt);
+    hipLaunchKernelGGL(k_view_scan, dim3(1), dim3(1024), 0, s, vb.cnt, Vc, vb.ptr);
+    hipLaunchKernelGGL(k_view_fill, dim3(wv), dim3(256), 0, s, g0.in_ptr, g0.in_src, g0.in_eid, g0.in_w, g0.in_w32,
+                       g0.in_r, vb.nid, V, (const int64_t*)vb.ptr, vb.src, vb.eid, vb.w, vb.w32, vb.r);
+    hipLaunchKernelGGL(k_view_tables, dim3((uint32_t)((std::max(V, A) + 255) / 256)), dim3(256), 0, s, g0.vfac,
+                       g0.loop_eid, vb.nid, V, eng->d_attached, A, na0, vb.vf, vb.loop, vb.att, vb.src, vb.eid, vb.w,
+                       vb.w32, vb.r);
+    HIP_TRY(hipGetLastError());
+    // the view's arc count was derived from the peel; the scan's total must agree
+    int64_t tot = -1;
+    HIP_TRY(hipMemcpyAsync(&tot, vb.ptr + Vc, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));  // a pageable destination: the whole copy
+    if (tot != na0) return fail(SHADOWTOPO_EINTERNAL, "pendant view: %lld arcs kept, %lld expected", (long long)tot,
+                                (long long)na0);
+    phase("device build");
     GraphDev gp = eng->g;
-    int64_t* d_ptr = nullptr;
-    int32_t *d_src = nullptr, *d_eid = nullptr, *d_loop = nullptr, *d_att = nullptr;
-    double *d_w = nullptr, *d_r = nullptr, *d_vf = nullptr;
-    float* d_w32 = nullptr;
-    const size_t na = nsrc.size();
-    if ((rc = dev_alloc(eng->prune_allocs, (void**)&d_vf, 8 * (size_t)Vc)) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_loop, 4 * (size_t)Vc)) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_att, 4 * natt.size())) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_ptr, 8 * ((size_t)Vc + 1))) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_src, 4 * na)) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_eid, 4 * na)) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_w, 8 * na)) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_r, 8 * na)) ||
-        (rc = dev_alloc(eng->prune_allocs, (void**)&d_w32, 4 * na)))
-        return rc;
-    HIP_TRY(hipMemcpy(d_vf, nvf.data(), 8 * (size_t)Vc, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_loop, nloop.data(), 4 * (size_t)Vc, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_att, natt.data(), 4 * natt.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_ptr, nptr.data(), 8 * ((size_t)Vc + 1), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_src, nsrc.data(), 4 * na, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_eid, neid.data(), 4 * na, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_w, nw.data(), 8 * na, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_r, nr.data(), 8 * na, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_w32, nw32.data(), 4 * na, hipMemcpyHostToDevice));
+    int64_t* d_ptr = vb.ptr;
+    int32_t *d_src = vb.src, *d_eid = vb.eid, *d_loop = vb.loop, *d_att = vb.att;
+    double *d_w = vb.w, *d_r = vb.r, *d_vf = vb.vf;
+    float* d_w32 = vb.w32;
     gp.in_ptr = d_ptr;
     gp.in_src = d_src;
     gp.in_eid = d_eid;
@@ -5037,6 +5131,7 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     eng->gp = gp;
     eng->gp_arcs = (int64_t)na - CSR_PAD;
     eng->h_view_of = std::move(nid);
+    (void)phase;
     eng->d_att_view = d_att;
     eng->prune_ready = true;
     (void)s;
