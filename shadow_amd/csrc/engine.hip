@@ -5131,10 +5131,8 @@ int ensure_pruned(shadowtopo_engine* eng, hipStream_t s) {
     eng->gp = gp;
     eng->gp_arcs = (int64_t)na - CSR_PAD;
     eng->h_view_of = std::move(nid);
-    (void)phase;
     eng->d_att_view = d_att;
     eng->prune_ready = true;
-    (void)s;
     return SHADOWTOPO_OK;
 }
 
