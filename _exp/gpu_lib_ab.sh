@@ -1,4 +1,5 @@
 # A/B of two builds of the engine (_exp/ablib/old.so vs new.so) on one config, interleaved
+# (the libraries travel with the tree: delete _exp/ablib after the A/B)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:?tag}
