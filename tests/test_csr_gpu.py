@@ -60,6 +60,26 @@ def test_csr_rounds(case, worklist, lean):
     assert (st["lean_groups"] > 0) == (lean != "tree")
 
 
+def test_option_ranges():
+    """the r05 options take their documented values and reject the rest (SHADOWTOPO_EINVAL)"""
+    g = _case("sparse")
+    eng = E.Engine.from_synth(g, layout="csr")
+    good = {E.OPT_CSR_INCREMENTAL: (0, 1, 32, 1 << 20), E.OPT_SPEC_COMPOSE: (0, 1), E.OPT_SPIN_US: (0, 200, 20000),
+            E.OPT_HOST_GROUPS: (0, 1, 4), E.OPT_CSR_LEAN: (0, 1, 2), E.OPT_HEAVY_FIRST: (0, 1),
+            E.OPT_WALK_TPW: (1, 2, 4), E.OPT_PART0_PERMILLE: (1, 562, 999)}
+    bad = {E.OPT_CSR_INCREMENTAL: (-1, (1 << 20) + 1), E.OPT_SPEC_COMPOSE: (2, -1), E.OPT_SPIN_US: (-1, 10_000_001),
+           E.OPT_HOST_GROUPS: (-1, 1025), E.OPT_CSR_LEAN: (3,), E.OPT_HEAVY_FIRST: (2,), E.OPT_WALK_TPW: (0, 5),
+           E.OPT_PART0_PERMILLE: (0, 1000)}
+    for k, vals in good.items():
+        for v in vals:
+            eng.set_option(k, v)
+    for k, vals in bad.items():
+        for v in vals:
+            with pytest.raises(E.ShadowTopoError):
+                eng.set_option(k, v)
+    eng.close()
+
+
 def test_csr_removed_variants_rejected():
     g = _case("sparse")
     eng = E.Engine.from_synth(g, layout="csr")
