@@ -75,6 +75,8 @@ Random* shadowtopo_random_new(uint32_t seed);
 void shadowtopo_random_free(Random* r);
 /* last value the standalone worker_updateMinTimeJump received (-1 if never called) */
 double shadowtopo_last_min_time_jump(void);
+/* how many times the standalone worker_updateMinTimeJump was called */
+long shadowtopo_min_time_jump_calls(void);
 /* log verbosity of the standalone logger: 0 error .. 5 debug (default 3 = message) */
 void shadowtopo_set_log_level(int level);
 

@@ -37,6 +37,7 @@ struct _Random {
 /* the last upcall's value; worker threads upcall concurrently (Shadow's master takes a lock,
  * master.c:148-159), so the stand-in keeps it in one atomic word */
 static _Atomic double g_last_min_jump = -1.0;
+static _Atomic long g_min_jump_calls = 0;
 static int g_log_level = -1;
 
 __attribute__((weak)) uint32_t address_toNetworkIP(Address* address) { return address->ip; }
@@ -59,6 +60,7 @@ __attribute__((weak)) double random_nextDouble(Random* random) {
 
 __attribute__((weak)) void worker_updateMinTimeJump(double minPathLatency) {
     atomic_store_explicit(&g_last_min_jump, minPathLatency, memory_order_relaxed);
+    atomic_fetch_add_explicit(&g_min_jump_calls, 1, memory_order_relaxed);
 }
 
 Address* shadowtopo_address_new(const char* ipString, const char* name) {
@@ -89,6 +91,9 @@ Random* shadowtopo_random_new(uint32_t seed) {
 void shadowtopo_random_free(Random* r) { free(r); }
 
 double shadowtopo_last_min_time_jump(void) { return atomic_load_explicit(&g_last_min_jump, memory_order_relaxed); }
+
+/* the stand-in's upcall count (the tests compare it with the reference model's upcalls) */
+long shadowtopo_min_time_jump_calls(void) { return atomic_load_explicit(&g_min_jump_calls, memory_order_relaxed); }
 
 void shadowtopo_set_log_level(int level) { g_log_level = level; }
 

@@ -1740,6 +1740,7 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
         const uint8_t k = cell_k(&m->kind[(size_t)i * A + j]);
         double mn = 0.0;
         int64_t stored = 0;
+        int noted = 0;   /* the Dijkstra branch hands each lowering store to the upcall itself */
         int success = 1; /* the reference's `success` (:2009-2031) */
         if (k == SHADOWTOPO_KIND_DIRECT || top->complete) {
             /* a complete graph without the edge: get_eid fails, nothing is stored */
@@ -1770,6 +1771,14 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
             }
             const uint8_t* kr = m->kind + (size_t)i * A;
             const int32_t t0 = mine ? 0 : j, t1 = mine ? A : j + 1;
+            /* the running minimum at the loop's start (0: none yet); a store at or above what
+             * this loop has seen cannot lower the minimum, which only falls (other threads'
+             * stores included), so only the others take the lock -- each lowering store makes
+             * its own upcall, in store order, as _topology_storePathInCache does (:1374-1385) */
+            pthread_mutex_lock(&top->min_lock);
+            double seen = top->min_latency == 0 ? INFINITY : top->min_latency;
+            pthread_mutex_unlock(&top->min_lock);
+            noted = 1;
             for (int32_t t = t0; t < t1; t++) {
                 /* the source itself: the igraph that returns [] for it stores nothing
                  * (topology.c:1815, the default rule); the one that returns [s] stores its
@@ -1781,7 +1790,10 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
                 if (kt == SHADOWTOPO_KIND_NONE || kt == SHADOWTOPO_KIND_DIRECT) continue;
                 if (!cache_claim(top, i, t)) continue;
                 const double l = cell_d(&m->lr[2 * ((size_t)i * A + t)]);
-                if (!stored || l < mn) mn = l;
+                if (l < seen) {
+                    note_min_latency(top, l);
+                    seen = l;
+                }
                 stored++;
             }
             /* [s] without a self-loop: _topology_computePathProperties fails for the source's
@@ -1791,7 +1803,7 @@ static int cache_resolve(Topology* top, matrix** mp, int32_t i, int32_t j, int32
         }
         if (stored) {
             atomic_fetch_add_explicit(&top->cached_paths, stored, memory_order_relaxed);
-            note_min_latency(top, mn);
+            if (!noted) note_min_latency(top, mn);
         }
         if (!success) return -1;
         d = cached_dir(top, i, j); /* (s, t), else (t, s), directed or not (:2033-2038) */

@@ -24,7 +24,8 @@ EXT_SYMBOLS = (
     "topology_hip_set_device", "topology_hip_set_devices", "topology_hip_set_self_rule", "topology_hip_prepare", "topology_hip_get_info",
     "topology_hip_attached", "topology_hip_vertex_of_ip", "topology_hip_vertex_of_id", "topology_hip_packet_count",
     "topology_hip_cached_cell", "topology_hip_edges", "shadowtopo_address_new", "shadowtopo_address_free", "shadowtopo_random_new",
-    "shadowtopo_random_free", "shadowtopo_last_min_time_jump", "shadowtopo_set_log_level",
+    "shadowtopo_random_free", "shadowtopo_last_min_time_jump", "shadowtopo_min_time_jump_calls",
+    "shadowtopo_set_log_level",
 )
 
 
@@ -89,6 +90,7 @@ def lib():
         L.shadowtopo_random_new.argtypes = [ctypes.c_uint32]
         L.shadowtopo_random_free.argtypes = [vp]
         L.shadowtopo_last_min_time_jump.restype = ctypes.c_double
+        L.shadowtopo_min_time_jump_calls.restype = ctypes.c_long
         L.shadowtopo_set_log_level.argtypes = [ctypes.c_int]
         _configured = True
     return L
@@ -137,6 +139,11 @@ def set_log_level(level: int):
 
 def last_min_time_jump() -> float:
     return float(lib().shadowtopo_last_min_time_jump())
+
+
+def min_time_jump_calls() -> int:
+    """how many upcalls the standalone worker_updateMinTimeJump has received (process-wide)"""
+    return int(lib().shadowtopo_min_time_jump_calls())
 
 
 class Topology:

@@ -48,8 +48,10 @@ def attach_all(top, ips, vertices, base=0):
 def ref_cache(g, lat_o, kind_o, complete=False):
     # directed graphs as the reference: (s, t) is refused once (t, s) is cached, and the query
     # (s, t) is then answered with the (t, s) Path (topology.c:1311-1317, :2033-2038)
-    return RefPathCache(lat_o, kind_o, directed=g.directed, complete=complete, prefer_direct=bool(g.prefer_direct),
-                        adjacent=adjacency_of(g))
+    model = RefPathCache(lat_o, kind_o, directed=g.directed, complete=complete, prefer_direct=bool(g.prefer_direct),
+                         adjacent=adjacency_of(g))
+    model.calls0 = T.min_time_jump_calls()  # the stand-in's upcall count before the first query
+    return model
 
 
 def check_cache_state(top, model):
@@ -62,6 +64,10 @@ def check_cache_state(top, model):
     assert inf["min_path_latency"] == model.min_latency
     if model.upcalls:
         assert T.last_min_time_jump() == model.upcalls[-1]
+    # one upcall per store that lowered the minimum, as _topology_storePathInCache makes them
+    # (topology.c:1374-1385), not one per miss
+    assert T.min_time_jump_calls() - model.calls0 == len(model.upcalls), (T.min_time_jump_calls() - model.calls0,
+                                                                             model.upcalls)
 
 
 def check_against_oracle(tmp_path, g, n_hosts=None):
