@@ -1599,9 +1599,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
             out[0] = f4{f[0], f[1], f[2], f[3]};
             out[1] = f4{f[4], f[5], f[6], f[7]};
         };
+        // RP: the W32 slab's row base in a VGPR kept live across the chunk (rows are immediate
+        // offsets from it; without the pin the compiler re-materialises it from an SGPR per row)
+        typedef __attribute__((address_space(3))) const f4 lf4;
+        uint32_t wbase = (uint32_t)(uintptr_t)(lf4*)&sW[cur][wave * TDT];
+        if constexpr (RP) asm volatile("" : "+v"(wbase));
         auto lds_row = [&](int r) {
             if constexpr (H16) {
                 w16_row(r, wn);
+            } else if constexpr (RP) {
+#pragma unroll
+            for (int j = 0; j < TDT / 4; ++j) wn[j] = *(lf4*)(uintptr_t)(wbase + (uint32_t)(r * BW + 4 * j) * 4u);
             } else {
             const f4* wr = (const f4*)&sW[cur][r * BW + wave * TDT];
 #pragma unroll
