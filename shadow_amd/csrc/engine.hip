@@ -1717,7 +1717,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         if (!live[k]) continue;
         const uint32_t* hl = hitlog + hl_at(k);
         const gdouble* Dl = B[k].D + lane;
-        const int32_t vl = v0 + (lane & (TDT - 1));  // PR: a position (W is permuted), else the vertex
         for (int32_t c0 = 0; c0 < nchunks; c0 += 64) {
             const uint32_t e = (c0 + lane < nchunks) ? hl[c0 + lane] : 0u;
             unsigned long long cm = __ballot(e != 0u);
@@ -1740,11 +1739,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                         }
                         ur[x] = PR ? perm[rp[x]] : rp[x];  // row position -> vertex
                     }
-                    double d64[XR], wl[XR];
+                    // the row's TDT weights are wave-uniform (rp is): scalar loads into SGPRs
+                    // instead of a vector load and 2 * TDT readlanes
+                    double d64[XR], ws[XR][TDT];
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
                         d64[x] = Dl[(size_t)ur[x] * KL];
-                        wl[x] = W[(size_t)rp[x] * Vp + vl];
+#pragma unroll
+                        for (int t = 0; t < TDT; ++t) ws[x][t] = W[(size_t)rp[x] * Vp + v0 + t];
                     }
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
@@ -1753,7 +1755,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                         const bool own = (u == sv[k]);
 #pragma unroll
                         for (int t = 0; t < TDT; ++t) {
-                            const double c = d64[x] + readlane_d(wl[x], t);
+                            const double c = d64[x] + ws[x][t];
                             if (__ballot((c <= bc[k][t]) & !own)) {
                                 if (!own) lex_update(c, d64[x], u, bc[k][t], bdu[k][t], bu[k][t], tie[k], 1u << t);
                             }
