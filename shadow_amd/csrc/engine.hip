@@ -1483,7 +1483,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         return 1 + (wi - 1) * 64;
     };
     auto win_size = [&](int32_t wi) { return wi == 0 ? 1 : (w1 && wi == 1 ? w1 : 64); };
-    constexpr int WG = 8;  // chunks whose bounds are in flight at once in a window evaluation (4: +1 %)
+    constexpr int WG = 4;  // chunks whose bounds are in flight at once in a window evaluation (8: 64 SGPRs of
+                           // minW, 149 SGPR spills reloaded by readlane in the chunk loop, sweep +6 %)
     auto eval_window = [&](int32_t wi) -> unsigned long long {
         const int32_t base = win_base(wi);
         const int32_t nw = nchunks - base < win_size(wi) ? nchunks - base : win_size(wi);
