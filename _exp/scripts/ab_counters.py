@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """HBM traffic per step of each relax-family kernel from separate rocprofv3 FETCH_SIZE and
-WRITE_SIZE passes over one bench command (scripts/ab_counters.sh): every dispatch of a kernel
+WRITE_SIZE passes over one bench command (_exp/scripts/ab_counters.sh): every dispatch of a kernel
 whose name matches the regex is summed and divided by the bench's warmup + timed steps (the
 engine's one-batch landmark rounds, run once before them, are included: ~1/157 of a C4 step).
 FETCH_SIZE is doubled (gfx950 counts half of wide reads, MI355X_MICROARCH.md), WRITE_SIZE taken

@@ -5,7 +5,7 @@
 set -o pipefail
 O=gpurun_out/${1:?tag}
 mkdir -p $O
-timeout -k 10 900 python -u scripts/shim_ab.py ${2:-4} > $O/shim_ab.jsonl 2> $O/shim_ab.err || { tail $O/shim_ab.err; exit 1; }
+timeout -k 10 900 python -u _exp/scripts/shim_ab.py ${2:-4} > $O/shim_ab.jsonl 2> $O/shim_ab.err || { tail $O/shim_ab.err; exit 1; }
 python3 - $O <<'PY'
 import json, statistics as S, collections, sys
 r = collections.defaultdict(list); x = {}; pr = collections.defaultdict(list)

@@ -3613,6 +3613,12 @@ int ensure_batches(shadowtopo_engine* eng, int32_t nb) {
     const int rc = ensure_batches_impl(eng, nb);
     eng->st.pool_allocs++;
     eng->st.pool_alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    // exactly one predecessor state: the kernels pick the tree fold or the lean form by which
+    // pool pointer is set (batch_view passes an absent pool on as NULL, never as NULL + offset:
+    // r05r's fault was k_seed storing a source record through such a pointer in batch >= 1)
+    if (rc == SHADOWTOPO_OK && ((eng->pools.Q != nullptr) == (eng->pools.P32 != nullptr) ||
+                                (eng->pools.P32 != nullptr) != eng->lean_next))
+        return fail(SHADOWTOPO_EINTERNAL, "batch pools: tree records and lean predecessor state both or neither present");
     return rc;
 }
 int ensure_batches_impl(shadowtopo_engine* eng, int32_t nb) {
@@ -3695,11 +3701,18 @@ int ensure_replay(shadowtopo_engine* eng) {
 // blocking wait.  A blocking synchronisation sleeps, and its wake-up added tens of
 // microseconds to each of a C2 step's waits and ~0.4 ms to each of C3's host-delivered
 // build's ~30 waits beside the row copies (31 -> 18 ms with a 5 ms budget, r05c3t).
+// Past the first 200 us the poll yields the core between queries (r06 advisor: a multi-second
+// C5 build, or 8 ranks on one host, kept a core busy that Shadow's worker threads could use);
+// sched_yield returns at once when no other thread is runnable, so an idle host loses nothing.
 hipError_t spin_event(const shadowtopo_engine* eng, hipEvent_t ev) {
     hipError_t e;
     const auto t0 = std::chrono::steady_clock::now();
+    const auto hot = std::chrono::microseconds(std::min(eng->opt_spin_us, 200));
+    const auto budget = std::chrono::microseconds(eng->opt_spin_us);
     while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(eng->opt_spin_us)) return hipEventSynchronize(ev);
+        const auto el = std::chrono::steady_clock::now() - t0;
+        if (el > budget) return hipEventSynchronize(ev);
+        if (el > hot) sched_yield();
     }
     return e;
 }
@@ -4651,15 +4664,17 @@ int locality_keys(shadowtopo_engine* eng, hipStream_t s, const std::vector<int32
     double* d_dist = nullptr;
     double* d_out = nullptr;
     int32_t *d_rows = nullptr, *d_cols = nullptr;
-    HIP_TRY(hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V * S));
-    HIP_TRY(hipMalloc((void**)&d_out, sizeof(double) * (size_t)std::max(A, S) * std::max(S, NL)));
-    HIP_TRY(hipMalloc((void**)&d_rows, sizeof(int32_t) * (size_t)KL));
-    HIP_TRY(hipMalloc((void**)&d_cols, sizeof(int32_t) * (size_t)std::max(A, S)));
+    // allocation failures fall through to the common free + stats restore below (r06 advisor)
+    if (hipMalloc((void**)&d_dist, sizeof(double) * (size_t)V * S) != hipSuccess ||
+        hipMalloc((void**)&d_out, sizeof(double) * (size_t)std::max(A, S) * std::max(S, NL)) != hipSuccess ||
+        hipMalloc((void**)&d_rows, sizeof(int32_t) * (size_t)KL) != hipSuccess ||
+        hipMalloc((void**)&d_cols, sizeof(int32_t) * (size_t)std::max(A, S)) != hipSuccess)
+        rc = fail(SHADOWTOPO_ENOMEM, "landmark buffers");
     for (int j = 0; j < KL; ++j) {
         eng->h_srcv[j] = j < S ? vid(samp[j]) : -1;
         eng->h_row[j] = -1;
     }
-    if (hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL, hipMemcpyHostToDevice, s) !=
+    if (rc == 0 && hipMemcpyAsync(eng->pools.srcv, eng->h_srcv.data(), sizeof(int32_t) * KL, hipMemcpyHostToDevice, s) !=
         hipSuccess)
         rc = fail(SHADOWTOPO_EDEVICE, "memcpy");
     if (rc == 0) rc = run_rounds(eng, 1, s);
@@ -5282,9 +5297,6 @@ int compute_rows_impl(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end
         const int64_t na = eng->rg == &eng->g ? eng->n_arcs : eng->gp_arcs;
         if (eng->arcinfo_cap < (size_t)std::max<int64_t>(na, 1)) {
             if (eng->d_arcinfo) (void)hipFree(eng->d_arcinfo);
-    for (int k = 0; k < 4; ++k)
-        for (void* q : {(void*)eng->d_bweight[k], (void*)eng->d_border[k][0], (void*)eng->d_border[k][1]})
-            if (q) (void)hipFree(q);
             eng->d_arcinfo = nullptr;
             eng->arcinfo_cap = 0;
             HIP_TRY(hipMalloc((void**)&eng->d_arcinfo, sizeof(ArcInfo) * (size_t)std::max<int64_t>(na, 1)));

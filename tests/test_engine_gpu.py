@@ -766,6 +766,34 @@ def test_scrambled_tree_reports_an_error(mode, layout):
         assert_bitexact(name, x, y)
 
 
+@pytest.mark.parametrize("worklist", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_scrambled_lean_state_reports_an_error(mode, worklist):
+    """the lean rounds' predecessor state (P32) scrambled before the walks, over several batches
+    (batch >= 1 is where r05r's fault was: a tree-record pointer formed from the absent pool):
+    k_walk_lean's range checks end the call in SHADOWTOPO_EINTERNAL, not a device fault, and
+    the same engine then computes the oracle's matrices"""
+    g = _vloss_graph(V=600, seed=41)
+    g.attached = np.arange(0, g.n, 3, dtype=np.int32)  # 200 sources: 4 batches
+    eng = E.Engine.from_synth(g, layout="csr")
+    eng.set_option(E.OPT_CSR_LEAN, 1)
+    eng.set_option(E.OPT_WORKLIST, worklist)
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_TEST_SCRAMBLE_TREE, mode)
+    with pytest.raises(E.ShadowTopoError, match="error -5"):
+        eng.compute_rows()
+    eng.set_option(E.OPT_TEST_SCRAMBLE_TREE, 0)
+    lat, rel, hops, kind = eng.compute_rows()
+    st = eng.stats()
+    eng.close()
+    assert st["lean_groups"] >= 1
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                       ("reliability", rel, orel)):
+        assert_bitexact(name, x, y)
+
+
 @pytest.mark.parametrize("layout", ["csr", "dense"])
 def test_unconverged_state_composes_without_fault(layout):
     """the iteration guard tripped after one round (OPT_MAX_ROUNDS 1) with the testing option
@@ -874,3 +902,33 @@ def test_heavy_first_sweep_order(case, parts):
     eng.close()
     assert_bitexact("new set latency", lat, olat[: len(sub), : len(sub)])
     assert_bitexact("new set hops", hops, ohops[: len(sub), : len(sub)])
+
+
+def test_late_walk_table_keeps_heavy_first_buffers():
+    """a dense engine runs parted heavy-first sweeps on a loss-free attached set (the chunk-count
+    and order buffers are allocated), then set_attached adds targets with vertex loss, so the
+    walk's per-arc table is allocated for the first time: the heavy-first buffers must survive
+    that allocation (r05 advisor: a pasted loop freed them there), every matrix is the oracle's
+    and close() frees each buffer once"""
+    g = synth.geometric_complete_ish(V=900, A=330)
+    rng = np.random.default_rng(12)
+    vl = np.full(g.n, np.nan)
+    lossy = np.setdiff1d(np.arange(g.n), g.attached)[:40]
+    vl[lossy] = rng.uniform(0.0, 0.05, len(lossy))
+    g.vertex_packetloss = vl
+    eng = E.Engine.from_synth(g, layout="dense")
+    eng.set_option(E.OPT_SWEEP_PARTS, 2)
+    eng.set_option(E.OPT_HEAVY_FIRST, 1)
+    sets = [g.attached, np.sort(np.concatenate([g.attached[:300], lossy[:30]])).astype(np.int32)]
+    for k, att in enumerate([sets[0], sets[0], sets[1], sets[1], sets[0]]):
+        eng.set_attached(att)
+        lat, rel, hops, kind = eng.compute_rows()
+        g.attached = att
+        olat, orel, ohops, okind, og = oracle_matrix(g)
+        og.close()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"set {k} {name}", x, y)
+    st = eng.stats()
+    eng.close()
+    assert st["walk_targets"] == 0  # the last set is loss-free again
