@@ -136,7 +136,7 @@ def cpu_baseline(g, n_sources, budget_s=20.0, all_cores=16):
     return out
 
 
-def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0):
+def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0, step_ms=None):
     """Roofline of the dominant kernel, timed with HIP events on the engine's stream around
     every launch: the f32 dense full sweep (k_relax_dense_f) on complete-ish graphs, the CSR
     relax rounds (k_relax, with the k_relax_wl worklist rounds) otherwise.  achieved = that
@@ -183,6 +183,23 @@ def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0):
                             "frac": ach / VALU_PEAK, "insts_per_launch": cnt["valu_insts_per_launch"],
                             "note": "SQ_INSTS_VALU of the same bench command (profiles/), scaled by known "
                                     "waves / SQ_WAVES; peak = one wave64 VALU issue per 2 cycles per SIMD-32 at 2.4 GHz"}
+    # the step-level fraction: the step's compulsory bytes (every launch of the dominant kernel)
+    # over the whole step, not only the kernel's own time
+    if step_ms:
+        roofline["frac_step"] = bytes_per_launch * launches / steps / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS
+    if st["dense"] and "valu" in roofline:
+        # the dense sweep is bound by VALU issue and the latency of its barrier-coupled chunk
+        # loop, not by HBM (DESIGN.md 9, r05 verdict): the headline fraction is the VALU one;
+        # the HBM compulsory-byte fraction and the measured traffic stay beside it
+        hbm = {k: roofline[k] for k in ("achieved", "peak", "unit", "frac", "frac_step", "traffic",
+                                         "compulsory_bytes_per_launch", "traffic_over_compulsory", "fabric_gbs",
+                                         "traffic_note") if k in roofline}
+        v = roofline["valu"]
+        roofline.update(bound="valu/latency", achieved=v["achieved"], peak=v["peak"], unit=v["unit"],
+                        frac=v["frac"], hbm=hbm,
+                        bound_note="VALU issue fraction of the chunk loop + exact pass (SQ_INSTS_VALU, profiles/); "
+                                   "the kernel is latency-bound on its barrier-coupled chunk loop, neither VALU "
+                                   "nor HBM saturated; roofline.hbm holds the compulsory-byte HBM fraction")
     if not st["dense"] and st["wl_launches"]:
         roofline["worklist_kernel"] = {"kernel": "k_relax_wl", "avg_launch_ms": st["wl_ms"] / st["wl_launches"],
                                        "launches_per_step": st["wl_launches"] / steps}
@@ -272,7 +289,7 @@ def sharded_report(dist, world, run, steps, relax_ms_per_step, rows):
 
 
 def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, on_timed_start=None,
-                on_timed_end=None, on_first_step=None, codec=None):
+                on_timed_end=None, on_first_step=None, codec=None, hops16=None):
     """One sharded attached-pair matrix build per step: this rank's contiguous
     row block computed by `compute(a, z, lat, rel, hops)` into packed row chunks, each chunk
     all-gathered (shard.RowExchange).  `warmup` untimed steps, then exactly `steps` bracketed
@@ -305,7 +322,7 @@ def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, 
             el = float(tt.item())
         return el
 
-    ex = shard.RowExchange(dist, A, world, rank, device, chunks, codec=codec)
+    ex = shard.RowExchange(dist, A, world, rank, device, chunks, codec=codec, hops16=hops16)
     for i in range(max(1, warmup)):
         ex.step(compute)
         if i == 0 and on_first_step:
@@ -336,7 +353,7 @@ def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, 
     return out
 
 
-def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=1, project=True):
+def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=1, project=True, hops16=True):
     """The north-star workload (BASELINE.json configs[3], SURVEY.md 8d C4: a 10^5-vertex
     Barabasi-Albert graph, 10^4 attached hosts) on every rank, timed like the headline
     (inputs resident, rows into HBM, barrier + synchronize around exactly `steps` matrix
@@ -370,8 +387,11 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
         def collect():
             eng_stats.update(eng.stats())
 
+        # sparse rows: hop counts exchanged as 16-bit halves (shard.EngineHopCodec, 18 B per pair)
+        hc = shard.EngineHopCodec(eng, stream_of=lambda: torch.cuda.current_stream(device).cuda_stream) \
+            if world > 1 and hops16 else None
         run = run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks,
-                          on_timed_start=reset, on_timed_end=collect)
+                          on_timed_start=reset, on_timed_end=collect, hops16=hc)
         ex, elapsed, st = run["exchange"], run["elapsed_s"], eng_stats
         timed = run["timed"]
         rec = {"workload": desc, "n_gpus": world, "n_vertices": g.n, "n_arcs": st["n_arcs"], "attached": A,
@@ -393,6 +413,8 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
         if world > 1:
             rec["allgather_ms"] = run["allgather_s"] / steps * 1e3
             rec["allgather_bytes_per_rank"] = run["allgather_bytes"]
+            rec["exchange_mode"] = "hops16" if hc is not None else "raw"
+            rec["hop_overflow_steps"] = ex.overflowed
             rec["allgather_GBps_per_rank"] = run["allgather_bytes"] * (world - 1) / world / (run["allgather_s"] / steps) / 1e9
         target = {"matrix_build_ms_under": 1000.0, "hbm_frac_at_least": 0.5, "on_gpus": 8,
                   "time_met": rec["matrix_build_ms"] < 1000.0,
@@ -420,6 +442,8 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
                 proj[str(W)] = {"per_gpu_ms": slow["ms"], "per_gpu_host_ms": max(x["host_ms"] for x in shares),
                                 "ranks_timed": shares,
                                 "allgather_bytes_per_gpu": 20 * A * A * (W - 1) // W,
+                                "allgather_bytes_per_gpu_hops16": (shard.packed_bytes(-(-A // W), A, 2) * (W - 1)
+                                                                   if hops16 else None),
                                 "note": "one rank's row share computed on this GPU; the all-gather over xGMI "
                                         "is not included (measured only by an N-GPU run)"}
             rec["projection"] = proj
@@ -573,7 +597,8 @@ def main():
     ap.add_argument("--sweep-parts", type=int, default=0, help="pruned dense sweep: batches in 1 .. 4 parts on their own streams (0 = engine default)")
     ap.add_argument("--chain-parts", type=int, default=-1, help="read-back-free delta rounds on each sweep part's stream (1) or after the join (0); -1 = engine default")
     ap.add_argument("--exchange", choices=["packed", "raw"], default="packed",
-                    help="N > 1, dense graphs: exchange rows packed (EngineRowCodec, default) or raw")
+                    help="N > 1: exchange rows packed (dense graphs: EngineRowCodec; sparse graphs: 16-bit hop "
+                         "counts, EngineHopCodec; the default) or raw")
     ap.add_argument("--dense-tb", type=int, default=0, help="batches per wave in the f32 dense sweep (0 = engine default)")
     ap.add_argument("--source-order", type=int, default=1, help="1 = locality-ordered source batches (default), 0 = attach order")
     ap.add_argument("--device-rounds", type=int, default=-1, help="CSR worklist rounds driven from the device: 0 never, "
@@ -668,6 +693,11 @@ def main():
     dense = bool(eng.stats()["dense"])
     codec = (shard.EngineRowCodec(eng, stream_of=lambda: torch.cuda.current_stream(dev).cuda_stream)
              if world > 1 and dense and args.exchange == "packed" else None)
+    # sparse graphs: no pair is rebuilt from the replica; the hop counts travel as 16-bit
+    # halves (shard.EngineHopCodec: 18 B per pair instead of 20, the high halves only if a
+    # count reaches 2^16)
+    hops16 = (shard.EngineHopCodec(eng, stream_of=lambda: torch.cuda.current_stream(dev).cuda_stream)
+              if world > 1 and not dense and args.exchange == "packed" else None)
     chunks = args.chunks or (2 if world >= 8 and codec is None else 1)
 
     def compute(a, z, lat, rel, hops):
@@ -679,7 +709,8 @@ def main():
     run = run_sharded(dist, world, rank, dev, A, compute, args.steps, args.warmup, chunks,
                       on_timed_start=eng.reset_stats, on_timed_end=lambda: st.update(eng.stats()),
                       # engine creation -> first finished matrix rows on the device
-                      on_first_step=lambda: cold.update(ms=(time.perf_counter() - t_cold) * 1e3), codec=codec)
+                      on_first_step=lambda: cold.update(ms=(time.perf_counter() - t_cold) * 1e3), codec=codec,
+                      hops16=hops16)
     cold_start_ms = cold["ms"]
     elapsed = run["elapsed_s"]
     total_sources = A if world > 1 else rows  # every rank's rows per step
@@ -688,7 +719,8 @@ def main():
 
     # roofline of the dominant kernel, timed with HIP events on the engine's stream around
     # every launch
-    roofline = roofline_of(st, g, args.config, args.scale, world, rows, args.steps, args.dense_variant)
+    roofline = roofline_of(st, g, args.config, args.scale, world, rows, args.steps, args.dense_variant,
+                           step_ms=ms_per_step)
 
     # SURVEY.md 8(d)'s matrix build time "delivered to host": the same steps with the rows
     # landing in page-locked host memory (PCIe included), beside the device-resident figure
@@ -726,7 +758,8 @@ def main():
 
     # the row exchange: at N > 1 what the timed steps moved; at N = 1 (dense) a probe packing
     # this rank's rows once, after the timing, for the packed-to-raw ratio the N-rank runs see
-    exchange = {"mode": "packed" if codec is not None else ("raw" if world > 1 else None)}
+    exchange = {"mode": "packed" if codec is not None else ("hops16" if hops16 is not None else
+                                                            ("raw" if world > 1 else None))}
     if world > 1:
         exchange.update(gathered_bytes_per_step=run["allgather_bytes"],
                         raw_bytes_per_step=sum(p.numel() for p in run["exchange"].packs) * world,
@@ -747,7 +780,7 @@ def main():
         eng.close()
         eng = None
         try:
-            north = north_star_c4(dev, dist, world, rank, chunks=chunks)
+            north = north_star_c4(dev, dist, world, rank, chunks=chunks, hops16=args.exchange == "packed")
         except Exception as e:  # report, never fake
             north = {"error": f"{type(e).__name__}: {e}"}
 

@@ -157,6 +157,13 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_HOST_GROUPS 36       /* rows into page-locked host memory: computed in this many batch groups, each
                                               group's copy behind the next group's rounds; 0 (default) = automatic (one
                                               group unless the rows outweigh the rounds). Results are identical. */
+#define SHADOWTOPO_OPT_SWEEP_STATS 37       /* diagnostics: 1 = after each pruned two-part sweep, the chunks its blocks staged
+                                              are summed into stats.sweep_chunks (one host synchronisation per sweep;
+                                              0 = off, the default) */
+#define SHADOWTOPO_OPT_SWEEP_WINDOWS 38     /* pruned dense sweep: the chunk windows whose skip masks are evaluated at once:
+                                              bits 0-7 = the neighbour window after the tile's own chunk (default 8,
+                                              0 = none), bits 8-15 = the far windows' size (default 0 = 64).
+                                              Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
@@ -250,6 +257,8 @@ typedef struct shadowtopo_stats {
     int64_t lean_groups;     /* batch groups computed with lean sparse rounds (OPT_CSR_LEAN) */
     int64_t spec_composes;   /* dense: composes enqueued behind the round that found convergence (OPT_SPEC_COMPOSE) */
     int64_t spec_composes_lost; /* dense: such composes redone because that round still changed pairs */
+    int64_t sweep_chunks;       /* OPT_SWEEP_STATS: 32-row chunks the pruned sweeps' blocks staged */
+    int64_t sweep_chunk_slots;  /* OPT_SWEEP_STATS: blocks x chunks of those sweeps (the unpruned count) */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */
@@ -334,6 +343,16 @@ int shadowtopo_self_rule_paths(shadowtopo_engine* eng, double* lat, double* rel,
    for the stream).  shadowtopo_unpack_rows rebuilds the rows, bit-identical, on any engine
    created from the same graph and attached set.  Not part of the reference's interface:
    the exchange step SURVEY.md 8(e) adds, with 1/15 of C2's bytes at 8 ranks. */
+/* Sparse row exchange (shard.RowExchange, any engine): hop counts (u32, device, n entries)
+   narrowed to their low 16 bits `lo` (and the high 16 bits into `hi` when not NULL) for the
+   all-gather, 18 instead of 20 bytes per pair; any count >= 2^16 ORs 1 into the device word
+   *overflow (the exchange then moves `hi` too).  shadowtopo_hops_widen rebuilds the u32 counts
+   (hi NULL: high halves zero).  Both are enqueued on `stream` (NULL: the engine's) without a
+   wait.  Not part of the reference's interface. */
+int shadowtopo_hops_narrow(shadowtopo_engine* eng, const uint32_t* hops, int64_t n, uint16_t* lo, uint16_t* hi,
+                           uint32_t* overflow, void* stream);
+int shadowtopo_hops_widen(shadowtopo_engine* eng, const uint16_t* lo, const uint16_t* hi, int64_t n, uint32_t* hops,
+                          void* stream);
 size_t shadowtopo_packed_capacity(int32_t rows, int32_t A);
 int shadowtopo_pack_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t row_end, const double* lat,
                          const double* rel, const uint32_t* hops, void* out, size_t cap, size_t* out_bytes,

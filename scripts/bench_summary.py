@@ -9,7 +9,8 @@ for p in sys.argv[1:]:
     d = json.load(open(p))
     c, r, e = d["config"], d["roofline"], d["engine"]
     print(f"{p}: {c['workload'][:40]} ms/step {d['ms_per_step']:.3f} host {c.get('matrix_build_host_ms') or 0:.3f} "
-          f"value {d['value']:.0f} frac {r['frac']:.4f} kernel {r['kernel']} {r['avg_launch_ms']:.3f} ms "
+          f"value {d['value']:.0f} frac {r['frac']:.4f} ({r['bound']}; hbm {(r.get('hbm') or r).get('frac') or 0:.4f}, "
+          f"step {(r.get('hbm') or r).get('frac_step') or 0:.4f}) kernel {r['kernel']} {r['avg_launch_ms']:.3f} ms "
           f"rounds {e['rounds_per_step']:.1f} cold {e['cold_start_ms']:.1f} ms fresh {c.get('matrix_build_fresh_ms') or 0:.3f} "
           f"compose {e.get('compose_kernel_ms_per_step') or 0:.3f} ms")
     n = d.get("north_star")

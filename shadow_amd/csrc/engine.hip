@@ -1469,20 +1469,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     __syncthreads();
     int32_t cur_win = -1;
     unsigned long long cur_live = 0ull;
-    // win1 > 0: window 1 is the win1 chunks next in the order (the tile's nearest
-    // neighbours), so the far windows are evaluated with the thresholds they left
-    const int32_t w1 = win1 > 0 && win1 < 64 ? win1 : 0;
+    // win1 (bits 0-7) > 0: window 1 is the win1 chunks next in the order (the tile's nearest
+    // neighbours), so the far windows are evaluated with the thresholds they left; bits 8-15:
+    // the far windows' size (0 = 64, the live mask's width)
+    const int32_t w1 = (win1 & 0xff) < 64 ? (win1 & 0xff) : 0;
+    const int32_t wf = ((win1 >> 8) & 0xff) > 0 && ((win1 >> 8) & 0xff) < 64 ? (win1 >> 8) & 0xff : 64;
     auto win_of = [&](int32_t j) {
         if (j == 0) return 0;
-        if (w1) return j <= w1 ? 1 : 2 + (j - 1 - w1) / 64;
-        return 1 + (j - 1) / 64;
+        if (w1) return j <= w1 ? 1 : 2 + (j - 1 - w1) / wf;
+        return 1 + (j - 1) / wf;
     };
     auto win_base = [&](int32_t wi) {
         if (wi == 0) return 0;
-        if (w1) return wi == 1 ? 1 : 1 + w1 + (wi - 2) * 64;
-        return 1 + (wi - 1) * 64;
+        if (w1) return wi == 1 ? 1 : 1 + w1 + (wi - 2) * wf;
+        return 1 + (wi - 1) * wf;
     };
-    auto win_size = [&](int32_t wi) { return wi == 0 ? 1 : (w1 && wi == 1 ? w1 : 64); };
+    auto win_size = [&](int32_t wi) { return wi == 0 ? 1 : (w1 && wi == 1 ? w1 : wf); };
     constexpr int WG = 4;  // chunks whose bounds are in flight at once in a window evaluation (8: 64 SGPRs of
                            // minW, 149 SGPR spills reloaded by readlane in the chunk loop, sweep +6 %)
     auto eval_window = [&](int32_t wi) -> unsigned long long {
@@ -3476,7 +3478,8 @@ struct shadowtopo_engine {
     int32_t opt_delta_live_div = 64;   // "sparse": changed pairs <= pairs / this
     int32_t opt_delta_colbound = 2;    // pruned delta: per-destination chunk bounds (1), + per-chunk source masks (2)
     int32_t opt_sweep_spiral = 1;      // pruned sweep: chunks outward from the tile on both sides (1) or upward, wrapping (0)
-    int32_t opt_sweep_win1 = 8;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none)
+    int32_t opt_sweep_win1 = 8;        // pruned sweep: size of the neighbour window after the tile's chunk (0: none);
+                                       // bits 8-15: the far windows' size (0 = 64)
     int32_t opt_sweep_split = 1;       // pruned sweep as two kernels (chunk loop; exact pass + epilogue)
     int32_t opt_sweep_parts = 2;       // the split sweep's two kernels per part of the batches, one stream per part
     hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
@@ -3502,6 +3505,7 @@ struct shadowtopo_engine {
     size_t pk_scratch_n = 0;
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
+    int32_t opt_sweep_stats = 0;      // diagnostics: staged chunks of the pruned sweeps (OPT_SWEEP_STATS)
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
@@ -3937,6 +3941,17 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                         if (e == hipSuccess) e = hipStreamWaitEvent(s, eng->ev_hp[k], 0);
                     }
                     if (e != hipSuccess) return e;
+                    if (eng->opt_sweep_stats && sort_any) {  // diagnostics: the chunks this sweep staged
+                        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+                        for (int k = 0; k < parts && k < 4; ++k) {
+                            if (!ha.w[k]) continue;
+                            std::vector<uint32_t> wk((size_t)ha.slots[k] * 8);
+                            if ((e = hipMemcpy(wk.data(), ha.w[k], wk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+                                return e;
+                            for (uint32_t x : wk) eng->st.sweep_chunks += x;
+                            eng->st.sweep_chunk_slots += (int64_t)(bound(k + 1) - bound(k)) * ntb * (int64_t)nchunks;
+                        }
+                    }
                     return hipGetLastError();
                 }
             }
@@ -6284,6 +6299,14 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value < 0 || value > 1024) return fail(SHADOWTOPO_EINVAL, "host groups must be in [0, 1024]");
             eng->opt_host_groups = (int32_t)value;
             return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SWEEP_WINDOWS:
+            if (value < 0 || (value & 0xff) >= 64 || ((value >> 8) & 0xff) >= 64 || value >= (1 << 16))
+                return fail(SHADOWTOPO_EINVAL, "sweep windows: bits 0-7 and 8-15 must each be in [0, 63]");
+            eng->opt_sweep_win1 = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SWEEP_STATS:
+            eng->opt_sweep_stats = value ? 1 : 0;
+            return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SPIN_US:
             if (value < 0 || value > 10000000) return fail(SHADOWTOPO_EINVAL, "spin must be in [0, 1e7] us");
             eng->opt_spin_us = (int32_t)value;
@@ -6716,6 +6739,55 @@ int shadowtopo_unpack_rows(shadowtopo_engine* eng, int32_t row_begin, int32_t ro
                        reinterpret_cast<const unsigned long long*>(o + pk_mask_off()),
                        reinterpret_cast<const uint32_t*>(o + pk_prefix_off(nw)), o + pk_entry_off(nw), lat, rel, hops,
                        nw);
+    HIP_TRY(hipGetLastError());
+    return SHADOWTOPO_OK;
+}
+
+// Sparse row exchange (r06, shard.RowExchange with hops16): no pair of a sparse graph's rows is
+// rebuilt from the receiver's replica, so the exchange moves lat and rel in full and the hop
+// counts as their low 16 bits -- 18 B per pair instead of 20.  A hop count >= 2^16 (a path
+// longer than 65 535 arcs) sets the overflow word; the exchange then moves the high halves too.
+namespace {
+__global__ __launch_bounds__(256) void k_hops_narrow(const uint32_t* __restrict__ hops, int64_t n,
+                                                     uint16_t* __restrict__ lo, uint16_t* __restrict__ hi,
+                                                     uint32_t* __restrict__ overflow) {
+    bool over = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t h = hops[i];
+        lo[i] = (uint16_t)(h & 0xffffu);
+        if (hi) hi[i] = (uint16_t)(h >> 16);
+        over |= (h >> 16) != 0u;
+    }
+    if (__ballot(over) && (threadIdx.x & 63) == 0) atomicOr(overflow, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_hops_widen(const uint16_t* __restrict__ lo, const uint16_t* __restrict__ hi,
+                                                    int64_t n, uint32_t* __restrict__ hops) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        hops[i] = (uint32_t)lo[i] | (hi ? (uint32_t)hi[i] << 16 : 0u);
+}
+
+uint32_t hops_grid(int64_t n) { return (uint32_t)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
+}  // namespace
+
+int shadowtopo_hops_narrow(shadowtopo_engine* eng, const uint32_t* hops, int64_t n, uint16_t* lo, uint16_t* hi,
+                           uint32_t* overflow, void* stream) {
+    if (!eng || n < 0 || (n > 0 && (!hops || !lo || !overflow))) return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    if (n == 0) return SHADOWTOPO_OK;
+    HIP_TRY(hipSetDevice(eng->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
+    hipLaunchKernelGGL(k_hops_narrow, dim3(hops_grid(n)), dim3(256), 0, s, hops, n, lo, hi, overflow);
+    HIP_TRY(hipGetLastError());
+    return SHADOWTOPO_OK;
+}
+
+int shadowtopo_hops_widen(shadowtopo_engine* eng, const uint16_t* lo, const uint16_t* hi, int64_t n, uint32_t* hops,
+                          void* stream) {
+    if (!eng || n < 0 || (n > 0 && (!lo || !hops))) return fail(SHADOWTOPO_EINVAL, "bad arguments");
+    if (n == 0) return SHADOWTOPO_OK;
+    HIP_TRY(hipSetDevice(eng->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : eng->own_stream;
+    hipLaunchKernelGGL(k_hops_widen, dim3(hops_grid(n)), dim3(256), 0, s, lo, hi, n, hops);
     HIP_TRY(hipGetLastError());
     return SHADOWTOPO_OK;
 }

@@ -60,6 +60,8 @@ OPT_CSR_INCREMENTAL = 31  # lean rounds: visits of vertices with more than n in-
 OPT_SPEC_COMPOSE = 33  # dense: compose enqueued behind each delta round, kept at convergence (1, default)
 OPT_SPIN_US = 35  # host waits poll this many microseconds before blocking (default 20000)
 OPT_HOST_GROUPS = 36  # page-locked host rows: batch groups (0 = automatic)
+OPT_SWEEP_WINDOWS = 38  # pruned dense sweep: neighbour window (bits 0-7, default 8) | far window size << 8 (0 = 64)
+OPT_SWEEP_STATS = 37  # diagnostics: chunks staged by the pruned sweeps into stats sweep_chunks / sweep_chunk_slots
 OPT_PART0_PERMILLE = 29  # two sweep parts: part 0's share of the batches, per mille (default 562)
 OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order
 # testing: the failure paths a convergence bug or a full device would take (SHADOWTOPO_EINTERNAL /
@@ -77,6 +79,7 @@ ENGINE_SYMBOLS = (
     "shadowtopo_get_stats", "shadowtopo_reset_stats", "shadowtopo_is_complete", "shadowtopo_get_eid",
     "shadowtopo_host_alloc", "shadowtopo_host_free", "shadowtopo_self_rule_paths",
     "shadowtopo_packed_capacity", "shadowtopo_pack_rows", "shadowtopo_unpack_rows",
+    "shadowtopo_hops_narrow", "shadowtopo_hops_widen",
 )
 
 
@@ -110,6 +113,7 @@ class Stats(ctypes.Structure):
         ("compose_kernel_ms", ctypes.c_double), ("walk_targets", ctypes.c_int64),
         ("attach_prep_ms", ctypes.c_double), ("lean_groups", ctypes.c_int64),
         ("spec_composes", ctypes.c_int64), ("spec_composes_lost", ctypes.c_int64),
+        ("sweep_chunks", ctypes.c_int64), ("sweep_chunk_slots", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -149,6 +153,8 @@ def lib():
         L.shadowtopo_pack_rows.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_size_t,
                                            ctypes.POINTER(ctypes.c_size_t), vp]
         L.shadowtopo_unpack_rows.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]
+        L.shadowtopo_hops_narrow.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, vp]
+        L.shadowtopo_hops_widen.argtypes = [vp, vp, vp, ctypes.c_int64, vp, vp]
         L.shadowtopo_reset_stats.argtypes = [vp]
         L.shadowtopo_is_complete.argtypes = [vp]
         L.shadowtopo_get_eid.restype = ctypes.c_int64
@@ -334,6 +340,18 @@ class Engine:
         vp = ctypes.c_void_p
         _check(lib().shadowtopo_unpack_rows(self._h, int(row_begin), int(row_end), vp(in_ptr), vp(lat_ptr),
                                             vp(rel_ptr), vp(hops_ptr), vp(stream) if stream else None))
+
+    def hops_narrow(self, hops_ptr, n, lo_ptr, hi_ptr, overflow_ptr, stream=None):
+        """device hop counts -> low / high 16-bit halves, OR 1 into *overflow_ptr if any count
+        is >= 2^16 (the sparse row exchange; enqueued, no wait)"""
+        vp = ctypes.c_void_p
+        _check(lib().shadowtopo_hops_narrow(self._h, vp(hops_ptr), int(n), vp(lo_ptr), vp(hi_ptr) if hi_ptr else None,
+                                            vp(overflow_ptr), vp(stream) if stream else None))
+
+    def hops_widen(self, lo_ptr, hi_ptr, n, hops_ptr, stream=None):
+        vp = ctypes.c_void_p
+        _check(lib().shadowtopo_hops_widen(self._h, vp(lo_ptr), vp(hi_ptr) if hi_ptr else None, int(n), vp(hops_ptr),
+                                           vp(stream) if stream else None))
 
     def sssp(self, sources):
         s = np.ascontiguousarray(sources, np.int32)

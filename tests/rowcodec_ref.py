@@ -103,3 +103,22 @@ class RefRowCodec:
         lat.reshape(-1)[:pairs] = torch.from_numpy(L)
         rel.reshape(-1)[:pairs] = torch.from_numpy(R)
         hops.reshape(-1)[:pairs] = torch.from_numpy(H.view(np.int32))
+
+
+class RefHopCodec:
+    """CPU stand-in of shard.EngineHopCodec (shadowtopo_hops_narrow / _widen): u32 hop counts
+    -> low / high 16-bit halves, overflow word OR-ed with 1 when a count is >= 2^16"""
+
+    def narrow(self, hops, lo, hi, overflow):
+        h = hops.reshape(-1).numpy().view(np.uint32)
+        lo.reshape(-1).numpy().view(np.uint16)[:] = (h & 0xFFFF).astype(np.uint16)
+        if hi is not None:
+            hi.reshape(-1).numpy().view(np.uint16)[:] = (h >> 16).astype(np.uint16)
+        if (h >> 16).any():
+            overflow[0] |= 1
+
+    def widen(self, lo, hi, out):
+        v = lo.reshape(-1).numpy().view(np.uint16).astype(np.uint32)
+        if hi is not None:
+            v |= hi.reshape(-1).numpy().view(np.uint16).astype(np.uint32) << 16
+        out.reshape(-1).numpy().view(np.uint32)[:] = v

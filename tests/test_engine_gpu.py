@@ -427,6 +427,81 @@ def test_row_exchange_with_engine_device_rows():
     assert_bitexact("hops", hops.astype(np.uint32), hops_o)
 
 
+@pytest.mark.parametrize("big", [False, True])
+def test_hops16_codec_round_trip(big):
+    """shadowtopo_hops_narrow / _widen (shard.EngineHopCodec, the sparse row exchange): u32 hop
+    counts -> 16-bit halves and back, bit-exact; the overflow word is set exactly when a count
+    reaches 2^16, and widening without the high halves keeps the low ones"""
+    import torch
+
+    from shadow_amd import shard
+    g = synth.random_sparse(V=300, avg_deg=4, seed=55)
+    eng = E.Engine.from_synth(g)
+    dev = torch.device("cuda:0")
+    codec = shard.EngineHopCodec(eng)
+    n = 3 * 65536 + 77  # past one grid-stride pass of the narrowing kernel
+    rng = np.random.default_rng(8)
+    h = rng.integers(0, 1 << 16 if not big else 1 << 20, n, dtype=np.int64)
+    hops = torch.from_numpy(h.astype(np.uint32).view(np.int32)).to(dev)
+    lo = torch.empty(n, dtype=torch.int16, device=dev)
+    hi = torch.empty(n, dtype=torch.int16, device=dev)
+    ovf = torch.zeros(2, dtype=torch.int32, device=dev)
+    codec.narrow(hops, lo, hi, ovf)
+    back = torch.empty(n, dtype=torch.int32, device=dev)
+    codec.widen(lo, hi, back)
+    low = torch.empty(n, dtype=torch.int32, device=dev)
+    codec.widen(lo, None, low)
+    torch.cuda.synchronize(dev)
+    eng.close()
+    assert int(ovf[0].item()) == (1 if big else 0) and int(ovf[1].item()) == 0
+    assert np.array_equal(back.cpu().numpy().view(np.uint32).astype(np.int64), h)
+    assert np.array_equal(low.cpu().numpy().view(np.uint32).astype(np.int64), h & 0xFFFF)
+
+
+def test_row_exchange_hops16_with_engine_device_rows():
+    """RowExchange's 16-bit hop path with the engine's device rows and kernels, as rank 0 of
+    two with a one-process stand-in of the collective: rank 0's assembled rows equal the
+    oracle's (the two-rank exchange itself runs on gloo in tests/test_shard_gloo.py)"""
+    import torch
+
+    from shadow_amd import shard
+
+    class OneRank:
+        def all_gather_into_tensor(self, out, inp, async_op=False):
+            k = out.numel() // inp.numel()
+            out.view(k, -1).copy_(inp.reshape(1, -1).expand(k, -1))
+
+            class W:
+                def wait(self):
+                    pass
+            return W() if async_op else None
+
+    g = synth.random_sparse(V=600, avg_deg=5, seed=57, A=300)
+    lat_o, rel_o, hops_o, _, _ = oracle_matrix(g)
+    eng = E.Engine.from_synth(g)
+    eng.set_attached(g.attached)
+    dev = torch.device("cuda:0")
+    # force the 16-bit path at one rank (the constructor enables it from two ranks on)
+    ex2 = shard.RowExchange(OneRank(), len(g.attached), 2, 0, dev, chunks=2, hops16=shard.EngineHopCodec(eng))
+    assert ex2.hop_bytes == 2
+
+    def compute(a, z, lat, rel, hops):
+        eng.compute_rows_device(a, z, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(),
+                                stream=torch.cuda.current_stream(dev).cuda_stream)
+
+    # two ranks' worth of rows computed by this one process: rank 1's half is gathered as a copy
+    # of rank 0's buffer, so only rank 0's rows are checked
+    ex2.step(compute)
+    torch.cuda.synchronize(dev)
+    lat, rel, hops = (x.cpu().numpy() for x in ex2.full())
+    eng.close()
+    r1 = ex2.r1
+    assert_bitexact("latency", lat[:r1], lat_o[:r1])
+    assert_bitexact("reliability", rel[:r1], rel_o[:r1])
+    assert_bitexact("hops", hops[:r1].astype(np.uint32), hops_o[:r1])
+    assert ex2.overflowed == 0
+
+
 @pytest.mark.parametrize("live", ["0", "1"])
 @pytest.mark.parametrize("case", ["ties", "geometric", "directed", "vloss_prefer"])
 def test_dense_delta_live_chunks(case, live):

@@ -330,3 +330,75 @@ def test_two_rank_packed_row_exchange(A_sel, chunks):
     assert [(r, ok) for r, ok, _, _ in res] == [(0, True), (1, True)]
     for _, _, sent, raw in res:
         assert sent * 4 < raw, (sent, raw)  # most pairs are the single arc: rebuilt, not sent
+
+
+def _worker_hops16(rank, world, port, A_sel, chunks, big, q):
+    """shard.RowExchange with 16-bit hop counts (the sparse exchange, RefHopCodec standing in
+    for the engine's kernels): 18 B per pair, every rank's matrices bit-exact after the
+    step; `big` adds 2^16 to some hop counts (a path longer than 65 535 arcs), so the high
+    halves are all-gathered too and still round-trip"""
+    import sys
+
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+    from shadow_amd import synth
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from rowcodec_ref import RefHopCodec
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = synth.random_sparse(V=160, avg_deg=4, seed=83, A=A_sel)
+    og = O.OracleGraph(g.n, g.src, g.dst, g.latency, g.packetloss, g.vertex_packetloss)
+    flags = og.flags()
+    A = len(g.attached)
+    full = list(og.pair_rows(flags, g.attached))
+    want_h = full[2].astype(np.int64)
+    if big:
+        want_h[::7, ::3] += (1 << 16) + 5  # only in the rows of some ranks' chunks
+    ex = shard.RowExchange(dist, A, world, rank, "cpu", chunks, hops16=RefHopCodec())
+    ok = ex.hop_bytes == 2
+    ok &= all(p.numel() == shard.packed_bytes(n, A, 2) for p, (_, n) in zip(ex.packs, ex.bounds))
+
+    def compute(a, z, lat, rel, hops):
+        l, r, _, _, _ = og.pair_rows(flags, g.attached, a, z)
+        lat[:z - a] = torch.from_numpy(l)
+        rel[:z - a] = torch.from_numpy(r)
+        hops[:z - a] = torch.from_numpy(want_h[a:z].astype(np.uint32).view(np.int32))
+
+    for _ in range(2):
+        ex.step(compute)
+        lat, rel, hops = ex.full()
+        ok &= np.array_equal(lat.numpy().view(np.uint64), full[0].view(np.uint64))
+        ok &= np.array_equal(rel.numpy().view(np.uint64), full[1].view(np.uint64))
+        ok &= np.array_equal(hops.numpy().view(np.uint32).astype(np.int64), want_h)
+    ok &= ex.overflowed == (2 * len(ex.bounds) if big else 0)
+    q.put((rank, bool(ok)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("A_sel,chunks,big", [(160, 1, False), (131, 2, False), (150, 2, True)])
+def test_two_rank_hops16_exchange(A_sel, chunks, big):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_hops16, args=(r, 2, port, A_sel, chunks, big, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert res == [(0, True), (1, True)]
+
+
+def test_hops16_packed_bytes():
+    """18 B per pair (+ the overflow word, 256-byte padded) against 20 B raw; f64 views aligned"""
+    for rows, A in ((1, 1), (63, 157), (1250, 10_000)):
+        raw, h16 = shard.packed_bytes(rows, A), shard.packed_bytes(rows, A, 2)
+        assert h16 % 256 == 0 and h16 >= rows * A * 18 + 8 and h16 <= rows * A * 18 + 8 + 256 + 8
+        assert rows * A < 100 or h16 < raw
+    buf = torch.zeros(shard.packed_bytes(3, 5, 2), dtype=torch.uint8)
+    lat, rel, lo, ovf = shard.pack_views(buf, 3, 5, 2)
+    assert lat.shape == (3, 5) and rel.shape == (3, 5) and lo.dtype == torch.int16 and ovf.numel() == 2
