@@ -45,9 +45,11 @@ def rounds(srcs, D0=None):
     changed = np.zeros((V, L), bool)
     changed[srcs, np.arange(L)] = True
     rows = segs = visits = 0.0
+    pushes = 0.0  # push form: rows of the out-neighbours read for every (vertex, batch) that changed
     nr = 0
     for r in range(400):
         anych = changed.any(1)
+        pushes += outdeg[anych].sum()
         act = np.zeros(V, bool)
         act[d[anych[s]]] = True
         visits += act.sum()
@@ -66,30 +68,31 @@ def rounds(srcs, D0=None):
         nr += 1
         if not changed.any():
             break
-    return D, nr, visits / V, rows / V, segs / V
+    return D, nr, visits / V, rows / V, segs / V, pushes / V
 
 
 rng = np.random.default_rng(1)
 att = np.asarray(g.attached)
 H = np.argsort(-outdeg)[:NH]
-Dh, nrh, vh, rh, _ = rounds(H)                                # hub distances [V, NH] (one batch)
+Dh, nrh, vh, rh, _, _ = rounds(H)                                # hub distances [V, NH] (one batch)
 print(f"{CFG}: V={V} arcs={len(s)} hubs={NH}; hub batch {nrh} rounds, {rh:.2f} row reads per vertex")
-tot = {"plain": np.zeros(4), "seeded": np.zeros(4)}
+tot = {"plain": np.zeros(5), "seeded": np.zeros(5)}
 for bi in range(NB):
     srcs = np.sort(rng.choice(att, 64, replace=False))
-    Dex, nr0, v0, r0, s0 = rounds(srcs)
+    Dex, nr0, v0, r0, s0, p0 = rounds(srcs)
     UB = np.min(Dh[srcs][:, None, :] + Dh[None, :, :], axis=2).T * (1 + 1e-9)   # [V, 64]
     fin = np.isfinite(Dex) & (Dex > 0)
     tight = np.mean(UB[fin] <= Dex[fin] * 1.001), np.mean(UB[fin] <= Dex[fin] * 1.01)
-    D1, nr1, v1, r1, s1 = rounds(srcs, D0=UB)
+    D1, nr1, v1, r1, s1, p1 = rounds(srcs, D0=UB)
     assert np.array_equal(D1, Dex), "seeded rounds reach another fixed point"
     print(f" batch {bi}: UB within 0.1% {tight[0]:.3f}, 1% {tight[1]:.3f}; rounds {nr0} -> {nr1}; "
           f"visits/vertex {v0:.2f} -> {v1:.2f}; row reads/vertex {r0:.2f} -> {r1:.2f}; "
-          f"changed-segment reads/vertex {s0:.2f} -> {s1:.2f} (of 8 per row)")
-    tot["plain"] += (nr0, v0, r0, s0)
-    tot["seeded"] += (nr1, v1, r1, s1)
+          f"changed-segment reads/vertex {s0:.2f} -> {s1:.2f} (of 8 per row); push row reads/vertex {p0:.2f} -> {p1:.2f}")
+    tot["plain"] += (nr0, v0, r0, s0, p0)
+    tot["seeded"] += (nr1, v1, r1, s1, p1)
 p, q = tot["plain"] / NB, tot["seeded"] / NB
 print(f"mean: rounds {p[0]:.1f} -> {q[0]:.1f}; visits {p[1]:.2f} -> {q[1]:.2f}; row reads {p[2]:.2f} -> {q[2]:.2f} "
-      f"({100 * (1 - q[2] / p[2]):.1f} % fewer); segment reads {p[3]:.2f} -> {q[3]:.2f} ({100 * (1 - q[3] / p[3]):.1f} % fewer)")
+      f"({100 * (1 - q[2] / p[2]):.1f} % fewer); segment reads {p[3]:.2f} -> {q[3]:.2f} ({100 * (1 - q[3] / p[3]):.1f} % fewer); "
+      f"push row reads {p[4]:.2f} -> {q[4]:.2f} (one pull pass: {len(s) / V:.2f})")
 print(f"seeding cost: one hub batch ({rh:.2f} row reads per vertex, once per attached set) + a min-plus "
       f"product of depth {NH} per (vertex, source): {NH} f64 add+min per pair")

@@ -1236,7 +1236,12 @@ constexpr int FTDT = 8;  // f32 full sweep: destinations per wave (block: 4 * FT
 // (8 blocks per CU instead of 6) and half the table (202 MB on C2, inside the Infinity Cache).
 // W16 <= W32 <= w keeps the filter conservative; a passing row tightens the
 // thresholds with an upper bound of w (one fp16 ulp up; +inf past the saturation).
-template <int TDT, int XR, int TB, bool PR, int PH = 0, int NW = 4, bool H16 = false>
+// GL (r06, OPT_SWEEP_GLDS, chunk loop only): the chunk's D32 rows and W32 slab go straight from
+// global memory into the LDS slot with global_load_lds_dwordx4 (LDS-DMA), issued for chunk
+// k + 1 into the free slot right after the barrier that ends chunk k - 1; the same two slots and
+// the same LDS image as the register staging (one wave-instruction fills 4 contiguous D32 rows,
+// or 8 W32 slab rows), no staging VGPRs and no ds_write pass.
+template <int TDT, int XR, int TB, bool PR, int PH = 0, int NW = 4, bool H16 = false, bool GL = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1 ? (NW == 8 ? 8 : 6) : 1))) void k_relax_dense_f(const float* __restrict__ W32, const double* __restrict__ W,
                                                        const int32_t* __restrict__ WI, int32_t Vp,
                                                        const double* __restrict__ in_r, Pools pools, int32_t V,
@@ -1270,6 +1275,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     // then needs all 8 waves dead, so more chunks are staged.)
     static_assert(NW == 4 || (NW == 8 && PH == 1), "8-wave blocks only for the chunk loop");
     static_assert(!H16 || (PH == 1 && PR && TB == 1 && NW == 4 && TDT == 8), "W16: the pruned chunk loop alone");
+    static_assert(!GL || (PH == 1 && PR && TB == 1 && NW == 4 && !H16), "LDS-DMA staging: the pruned f32 chunk loop alone");
     constexpr int NT = 64 * NW;  // threads per block
     constexpr int BW = NW * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
@@ -1352,7 +1358,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     constexpr int DQ = SRS * KL / 4 / NT;       // float4 of one batch's D32 chunk per thread
     constexpr int WQT = (SRS * WQ + NT - 1) / NT;  // float4 of W32 per thread
     static_assert(DQ * NT * 4 == SRS * KL, "the D32 chunk is whole float4s per thread");
-    f4 pd[TB][DQ], pw[WQT];
+    f4 pd[TB][DQ], pw[WQT];  // register staging (unused with GL)
     // W16: a chunk's W16 slab is SRS rows x BW halves = SRS * BW / 8 16-byte pieces
     constexpr int WQ16 = BW / 8;
     constexpr int WQT16 = (SRS * WQ16 + NT - 1) / NT;
@@ -1385,7 +1391,29 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     };
     // fetch the chunk of order index j into registers (rows in the locality order: prow
     // holds each row's vertex, from perm_of)
+    // GL: the same chunk straight into LDS slot `buf` (wave-uniform LDS bases, lane-linear)
+    auto fetch_gl = [&](int32_t j, const int32_t* prow, int buf) {
+        if constexpr (GL) {
+            typedef __attribute__((address_space(1))) void gv;
+            typedef __attribute__((address_space(3))) void lv;
+            const int32_t c = chunk_of(j);
+            const int32_t u0 = c * SRS;
+            const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+            for (int i = 0; i < DQ; ++i)  // rows w*4 + 16i .. +3: 1 KB of the slot per wave-instruction
+                __builtin_amdgcn_global_load_lds((gv*)(B[0].D32 + (size_t)prow[i] * KL + (size_t)(l % (KL / 4)) * 4),
+                                                 (lv*)&sD[buf][0][(w * 4 + 16 * i) * KL], 16, 0, 0);
+            static_assert(WQT == 1 && SRS * WQ == NT, "one W32 slab piece per thread");
+            __builtin_amdgcn_global_load_lds((gv*)((const gfloat*)W32 + (size_t)(u0 + (int)threadIdx.x / WQ) * Vp + vb +
+                                                   ((int)threadIdx.x % WQ) * 4),
+                                             (lv*)&sW[buf][w * 256], 16, 0, 0);
+            mdn[0] = minD[((size_t)(live[0] ? b0 : first) * nchunks + c) * KL + lane];
+#pragma unroll
+            for (int t = 0; t < TDT; ++t) mwn[t] = minW[(size_t)c * ncol + v0 + t];
+        }
+    };
     auto fetch = [&](int32_t j, const int32_t* prow) {
+        if constexpr (GL) return;
         const int32_t c = chunk_of(j);
         const int32_t u0 = c * SRS;
 #pragma unroll
@@ -1427,6 +1455,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         }
     };
     auto stash = [&](int buf) {
+        if constexpr (GL) return;
 #pragma unroll
         for (int k = 0; k < TB; ++k)
 #pragma unroll
@@ -1550,6 +1579,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     int32_t itc = next_live(0);
     if (itc >= 0) {
         perm_of(itc, prow_n);
+        if constexpr (GL) fetch_gl(itc, prow_n, 0);
         fetch(itc, prow_n);
         stash(0);
         advance();
@@ -1563,7 +1593,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         const int32_t u0 = c * SRS;
         const int cur = bufc;
         const bool more = itn >= 0;
-        if (more) fetch(itn, prow_n);
+        if (more) {
+            if constexpr (GL) fetch_gl(itn, prow_n, cur ^ 1);  // slot cur ^ 1: read last iteration, before its barrier
+            fetch(itn, prow_n);
+        }
         // block-uniform (a window evaluation holds a barrier); a window evaluated one chunk
         // earlier uses slightly older thresholds, which only skips less
         const int32_t itn2 = more ? next_live(itn + 1) : -1;
@@ -3505,6 +3538,7 @@ struct shadowtopo_engine {
     size_t pk_scratch_n = 0;
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
+    int32_t opt_sweep_glds = 1;       // pruned sweep chunk loop: LDS-DMA staging (OPT_SWEEP_GLDS; r06: sweep -1.1 %)
     int32_t opt_sweep_stats = 0;      // diagnostics: staged chunks of the pruned sweeps (OPT_SWEEP_STATS)
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
@@ -3897,6 +3931,14 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                             }
                         }
                         const int32_t* ord = heavy && eng->heavy_key[k] == key ? eng->d_border[k][cur] : nullptr;
+                        if (eng->opt_sweep_glds)
+                            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1, 4, false, true>), dim3((uint32_t)nbl),
+                                               dim3(256), 0, st, eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
+                                               P, eng->V, n, ntb, par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl,
+                                               eng->d_perm, eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp,
+                                               eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr, ord,
+                                               heavy ? eng->d_bweight[k] : nullptr);
+                        else
                         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1>), dim3((uint32_t)nbl), dim3(256), 0, st,
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
@@ -6303,6 +6345,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
             if (value < 0 || (value & 0xff) >= 64 || ((value >> 8) & 0xff) >= 64 || value >= (1 << 16))
                 return fail(SHADOWTOPO_EINVAL, "sweep windows: bits 0-7 and 8-15 must each be in [0, 63]");
             eng->opt_sweep_win1 = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SWEEP_GLDS:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "sweep glds must be 0 or 1");
+            eng->opt_sweep_glds = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SWEEP_STATS:
             eng->opt_sweep_stats = value ? 1 : 0;

@@ -1007,3 +1007,30 @@ def test_late_walk_table_keeps_heavy_first_buffers():
     st = eng.stats()
     eng.close()
     assert st["walk_targets"] == 0  # the last set is loss-free again
+
+
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
+def test_dense_sweep_glds_staging(case):
+    """OPT_SWEEP_GLDS: the pruned chunk loop staged by LDS-DMA (global_load_lds, the default)
+    or through registers, two sweep parts, heavy-first from the second computation: the
+    oracle's matrices bit for bit every time"""
+    if case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=6)
+    elif case == "vloss_prefer":
+        g = synth.geometric_complete_ish(V=600, A=200)
+        rng = np.random.default_rng(3)
+        g.vertex_packetloss = np.where(rng.random(g.n) < 0.3, rng.uniform(0, 0.05, g.n), np.nan)
+        g.prefer_direct = True
+    else:
+        g = synth.geometric_complete_ish(V=900, A=330)
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    eng = E.Engine.from_synth(g, layout="dense")
+    eng.set_attached(g.attached)
+    for step in range(4):
+        eng.set_option(E.OPT_SWEEP_GLDS, 0 if step == 2 else 1)  # register staging once, between
+        lat, rel, hops, kind = eng.compute_rows()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"step {step} {name}", x, y)
+    eng.close()
