@@ -821,6 +821,13 @@ def main():
             "data": "synthetic (SURVEY.md 8d generator, fixed seeds)",
             "config": {"workload": desc, "n_vertices": g.n, "n_edges": g.m, "n_arcs": st["n_arcs"],
                        "attached": A, "sources_per_gpu": rows, "matrix_build_ms": ms_per_step,
+                       # a source-path is one source's row over all A attached targets, by shortest
+                       # paths over the relaxation graph: the pendant-pruned view where one exists
+                       # (C5; a peeled pendant vertex lies on no attached pair's path)
+                       "relaxation_vertices": g.n - st.get("pruned_vertices", 0),
+                       "unit_note": ("source-paths over the pendant-pruned view (%d of %d vertices)"
+                                     % (g.n - st["pruned_vertices"], g.n)) if st.get("pruned_vertices") else
+                                    "source-paths over every vertex",
                        "matrix_build_host_ms": build_host_ms, "matrix_build_fresh_ms": fresh_ms,
                        "fresh_attach_prep_ms": fresh_prep_ms,
                        "matrix_build_note": "matrix_build_ms: rows left in HBM (the timed steps above: every "
