@@ -592,6 +592,8 @@ def main():
     ap.add_argument("--dense-variant", type=int, default=0, help="0 = f32-filtered kernels (default), 1 = f64 kernels")
     ap.add_argument("--chunks", type=int, default=0, help="row chunks per step (0 = 2 at N>=8, else 1): "
                     "chunk c's all-gather overlaps chunk c+1's computation")
+    ap.add_argument("--sweep-glds", type=int, default=-1, help="pruned dense sweep: chunk loop staged by LDS-DMA (1) "
+                    "or through registers (0); -1 = engine default")
     ap.add_argument("--dense-w16", type=int, default=-1, help="pruned dense sweep: 16-bit filter weights (1), f32 (0); -1 = engine default")
     ap.add_argument("--dense-spec", type=int, default=-1, help="dense: leading rounds with no host read-back (0..4); -1 = engine default")
     ap.add_argument("--sweep-parts", type=int, default=0, help="pruned dense sweep: batches in 1 .. 4 parts on their own streams (0 = engine default)")
@@ -664,6 +666,8 @@ def main():
         eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, args.dense_tb)
     if args.dense_w16 >= 0:
         eng.set_option(E.OPT_DENSE_W16, args.dense_w16)
+    if args.sweep_glds >= 0:
+        eng.set_option(E.OPT_SWEEP_GLDS, args.sweep_glds)
     if args.dense_spec >= 0:
         eng.set_option(E.OPT_DENSE_SPEC, args.dense_spec)
     if args.sweep_parts:

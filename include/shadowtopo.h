@@ -165,7 +165,7 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               0 = none), bits 8-15 = the far windows' size (default 0 = 64).
                                               Results are identical. */
 #define SHADOWTOPO_OPT_SWEEP_GLDS 39        /* pruned dense sweep: the chunk loop stages its D32 rows and W32 slab by LDS-DMA
-                                              (global_load_lds, 1, the default) or through registers (0). Results are identical. */
+                                              (global_load_lds, 1) or through registers (0, the default). Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL

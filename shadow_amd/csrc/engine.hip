@@ -1279,8 +1279,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     constexpr int NT = 64 * NW;  // threads per block
     constexpr int BW = NW * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
-    __shared__ __attribute__((aligned(16))) float sD[2][TB][SRS * KL];
-    __shared__ __attribute__((aligned(16))) float sW[2][H16 ? SRS * BW / 2 : SRS * BW];
+    // all of the kernel's LDS in ONE __shared__ object: beside LDS-DMA (GL), a second object
+    // made hipcc wait for every outstanding DMA (vmcnt(0)) before the chunk's first LDS read
+    struct SweepLds {
+        float d[2][TB][SRS * KL];
+        float w[2][H16 ? SRS * BW / 2 : SRS * BW];
+        unsigned long long win[2];
+    };
+    __shared__ __attribute__((aligned(16))) SweepLds slds;
+    auto& sD = slds.d;
+    auto& sW = slds.w;
     int32_t grp, vt;
     // heavy-first (PH 1): border maps the hardware block to a (batch, tile) item of the same
     // XCD, the items of each XCD in decreasing chunk counts of the previous sweep (k_heavy_order),
@@ -1493,7 +1501,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     // newest thresholds).  Window 0 is the block's own chunk alone (it tightens the
     // thresholds most), then windows of 64.  A dead chunk's hit log entries are zeroed at
     // the evaluation.
-    __shared__ unsigned long long sWin[2];
+    auto& sWin = slds.win;
     if (PR && threadIdx.x == 0) sWin[0] = sWin[1] = 0ull;
     __syncthreads();
     int32_t cur_win = -1;
@@ -1520,11 +1528,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         const int32_t base = win_base(wi);
         const int32_t nw = nchunks - base < win_size(wi) ? nchunks - base : win_size(wi);
         unsigned long long wm = 0ull;
+        // lane i's chunk of the window, computed once in VGPRs (r06: the spiral order's index
+        // arithmetic per chunk in SGPRs was ~50 scalar instructions, about a third of the
+        // chunk loop's instruction stream); each chunk's index is then one readlane
+        const int32_t cl = chunk_of(base + (lane < nw ? lane : 0));
         for (int32_t j0 = 0; j0 < nw; j0 += WG) {
             float md[TB][WG], mw8[WG][TDT];
 #pragma unroll
             for (int jj = 0; jj < WG; ++jj) {
-                const int32_t c = chunk_of(base + (j0 + jj < nw ? j0 + jj : 0));
+                const int32_t c = __builtin_amdgcn_readlane(cl, j0 + jj < nw ? j0 + jj : 0);
 #pragma unroll
                 for (int k = 0; k < TB; ++k)
                     md[k][jj] = minD[((size_t)(live[k] ? b0 + k : first) * nchunks + c) * KL + lane];
@@ -1551,7 +1563,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
             ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sWin[wi & 1] >> 32)) << 32) |
             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sWin[wi & 1]);
         if (lane < nw && !((lv >> lane) & 1ull)) {
-            const int32_t c = chunk_of(base + lane);
+            const int32_t c = cl;
 #pragma unroll
             for (int k = 0; k < TB; ++k) hitlog[hl_at(k) + c] = 0u;
         }
@@ -3538,7 +3550,7 @@ struct shadowtopo_engine {
     size_t pk_scratch_n = 0;
     int32_t* h_cnt_spec = nullptr;    // pinned: those rounds' change counts [round][nb]
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
-    int32_t opt_sweep_glds = 1;       // pruned sweep chunk loop: LDS-DMA staging (OPT_SWEEP_GLDS; r06: sweep -1.1 %)
+    int32_t opt_sweep_glds = 0;       // pruned sweep chunk loop: LDS-DMA staging (OPT_SWEEP_GLDS; r06: ties register staging)
     int32_t opt_sweep_stats = 0;      // diagnostics: staged chunks of the pruned sweeps (OPT_SWEEP_STATS)
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)

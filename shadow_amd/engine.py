@@ -61,7 +61,7 @@ OPT_SPEC_COMPOSE = 33  # dense: compose enqueued behind each delta round, kept a
 OPT_SPIN_US = 35  # host waits poll this many microseconds before blocking (default 20000)
 OPT_HOST_GROUPS = 36  # page-locked host rows: batch groups (0 = automatic)
 OPT_SWEEP_WINDOWS = 38  # pruned dense sweep: neighbour window (bits 0-7, default 8) | far window size << 8 (0 = 64)
-OPT_SWEEP_GLDS = 39  # pruned dense sweep chunk loop: LDS-DMA staging (1, default) or register staging (0)
+OPT_SWEEP_GLDS = 39  # pruned dense sweep chunk loop: LDS-DMA staging (1) or register staging (0, default)
 OPT_SWEEP_STATS = 37  # diagnostics: chunks staged by the pruned sweeps into stats sweep_chunks / sweep_chunk_slots
 OPT_PART0_PERMILLE = 29  # two sweep parts: part 0's share of the batches, per mille (default 562)
 OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order

@@ -1011,8 +1011,8 @@ def test_late_walk_table_keeps_heavy_first_buffers():
 
 @pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
 def test_dense_sweep_glds_staging(case):
-    """OPT_SWEEP_GLDS: the pruned chunk loop staged by LDS-DMA (global_load_lds, the default)
-    or through registers, two sweep parts, heavy-first from the second computation: the
+    """OPT_SWEEP_GLDS: the pruned chunk loop staged by LDS-DMA (global_load_lds) or through
+    registers (the default), two sweep parts, heavy-first from the second computation: the
     oracle's matrices bit for bit every time"""
     if case == "ties":
         g = synth.integer_grid(rows=14, cols=15, seed=6)
@@ -1028,7 +1028,7 @@ def test_dense_sweep_glds_staging(case):
     eng = E.Engine.from_synth(g, layout="dense")
     eng.set_attached(g.attached)
     for step in range(4):
-        eng.set_option(E.OPT_SWEEP_GLDS, 0 if step == 2 else 1)  # register staging once, between
+        eng.set_option(E.OPT_SWEEP_GLDS, 0 if step == 2 else 1)  # register staging (the default) once, between
         lat, rel, hops, kind = eng.compute_rows()
         for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
                            ("reliability", rel, orel)):
