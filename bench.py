@@ -784,7 +784,10 @@ def main():
         eng.close()
         eng = None
         try:
-            north = north_star_c4(dev, dist, world, rank, chunks=chunks, hops16=args.exchange == "packed")
+            # C4 is sparse: no row codec, so its own chunking (2 overlapped chunks at N >= 8, where
+            # every GPU takes in ~1.6 GB), not the headline's (1 chunk beside C2's packed rows)
+            north = north_star_c4(dev, dist, world, rank, chunks=args.chunks or (2 if world >= 8 else 1),
+                                  hops16=args.exchange == "packed")
         except Exception as e:  # report, never fake
             north = {"error": f"{type(e).__name__}: {e}"}
 
