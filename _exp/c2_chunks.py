@@ -33,7 +33,7 @@ for rep in range(REPS):
         eng.compute_rows(want_kind=False)
         st = eng.stats()
         print(f"rep {rep} {' '.join(opts) or 'default'}: staged {st['sweep_chunks'] / max(1, st['sweep_chunk_slots']):.4f} "
-              f"of block-chunks; sweep {t['full_ms'] / max(1, t['full_sweeps']):.3f} ms, delta {t['delta_ms'] / N:.3f} ms, "
+              f"of block-chunks, {st['sweep_hit_rows']} logged rows ({st['sweep_hit_rows'] / max(1, st['sweep_chunk_slots'] // 313 * 4):.1f} per wave); sweep {t['full_ms'] / max(1, t['full_sweeps']):.3f} ms, delta {t['delta_ms'] / N:.3f} ms, "
               f"wall {t['wall_ms'] / N:.3f} ms per computation", flush=True)
         eng.set_option(E.OPT_SWEEP_WINDOWS, 8)
         eng.set_option(E.OPT_SWEEP_GLDS, 0)

@@ -166,6 +166,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
                                               Results are identical. */
 #define SHADOWTOPO_OPT_SWEEP_GLDS 39        /* pruned dense sweep: the chunk loop stages its D32 rows and W32 slab by LDS-DMA
                                               (global_load_lds, 1) or through registers (0, the default). Results are identical. */
+#define SHADOWTOPO_OPT_SWEEP_REFILTER 40    /* pruned dense sweep: the exact f64 pass first re-tests the rows the chunk loop
+                                              logged against its FINAL f32 thresholds and drops those no lane passes
+                                              (1) or evaluates every logged row (0, the default). Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL
@@ -261,6 +264,7 @@ typedef struct shadowtopo_stats {
     int64_t spec_composes_lost; /* dense: such composes redone because that round still changed pairs */
     int64_t sweep_chunks;       /* OPT_SWEEP_STATS: 32-row chunks the pruned sweeps' blocks staged */
     int64_t sweep_chunk_slots;  /* OPT_SWEEP_STATS: blocks x chunks of those sweeps (the unpruned count) */
+    int64_t sweep_hit_rows;     /* OPT_SWEEP_STATS: rows the chunk loops logged for the exact f64 passes */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

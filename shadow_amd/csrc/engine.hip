@@ -1259,7 +1259,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        const double* __restrict__ vfac, int32_t spiral,
                                                        int32_t win1, float* __restrict__ mdc_out,
                                                        const int32_t* __restrict__ border = nullptr,
-                                                       uint32_t* __restrict__ bweight = nullptr) {
+                                                       uint32_t* __restrict__ bweight = nullptr,
+                                                       float* __restrict__ thr_io = nullptr) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -1754,6 +1755,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         ++nvis;
     }
     if (PH == 1 && bweight && threadIdx.x == 0) bweight[Lb] = nvis;
+    // refilter (OPT_SWEEP_REFILTER): the final f32 thresholds go to the exact pass, which
+    // re-tests every logged row against them first (rows logged while a threshold was still
+    // falling mostly no longer pass)
+    if (PH == 1 && thr_io) {
+#pragma unroll
+        for (int t = 0; t < TDT; ++t) thr_io[(hl_at(0) / nchunks * TDT + t) * KL + lane] = thr[0][t];
+    }
     }  // PH != 2
     if constexpr (PH == 1) return;
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
@@ -1765,6 +1773,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         if (!live[k]) continue;
         const uint32_t* hl = hitlog + hl_at(k);
         const gdouble* Dl = B[k].D + lane;
+        float thr_f[TDT];  // refilter: the chunk loop's final thresholds of this lane
+#pragma unroll
+        for (int t = 0; t < TDT; ++t)
+            thr_f[t] = (PH == 2 && thr_io) ? thr_io[(hl_at(k) / nchunks * TDT + t) * KL + lane] : 0.0f;
         for (int32_t c0 = 0; c0 < nchunks; c0 += 64) {
             const uint32_t e = (c0 + lane < nchunks) ? hl[c0 + lane] : 0u;
             unsigned long long cm = __ballot(e != 0u);
@@ -1773,6 +1785,39 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                 cm &= cm - 1;
                 unsigned long long hrows = (uint32_t)__builtin_amdgcn_readlane((int)e, ci);
                 const int32_t u0 = (c0 + ci) * SRS;
+                if (PH == 2 && PR && TB == 1 && thr_io) {
+                    // drop the logged rows that no lane passes under the chunk loop's FINAL
+                    // thresholds (D32(u) <= max_t fl32(thr_t - W32(u, v_t)), the chunk loop's own
+                    // filter): every row whose exact candidate meets or beats the final key
+                    // passes (thr_final >= f32_thr(bc_final), k_relax_dense_f's invariant), so
+                    // the rows dropped cannot change the final lexicographic state; 4 rows' loads
+                    // in flight per step
+                    unsigned long long keep = 0ull, todo = hrows;
+                    while (todo) {
+                        int32_t rr[4];
+                        float dq[4], wq[4][TDT];
+#pragma unroll
+                        for (int x = 0; x < 4; ++x) {
+                            rr[x] = -1;
+                            if (todo) {
+                                rr[x] = __builtin_ctzll(todo);
+                                todo &= todo - 1;
+                            }
+                            const int32_t rp = u0 + (rr[x] >= 0 ? rr[x] : 0);
+                            dq[x] = B[k].D32[(size_t)perm[rp] * KL + lane];
+#pragma unroll
+                            for (int t = 0; t < TDT; ++t) wq[x][t] = W32[(size_t)rp * Vp + v0 + t];
+                        }
+#pragma unroll
+                        for (int x = 0; x < 4; ++x) {
+                            float g = thr_f[0] - wq[x][0];
+#pragma unroll
+                            for (int t = 1; t < TDT; ++t) g = fmaxf(g, thr_f[t] - wq[x][t]);
+                            if (rr[x] >= 0 && __ballot(dq[x] <= g)) keep |= 1ull << rr[x];
+                        }
+                    }
+                    hrows = keep;
+                }
                 if (prof && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hrows));
                 while (hrows) {
                     int32_t ur[XR], rp[XR];
@@ -3552,6 +3597,10 @@ struct shadowtopo_engine {
     int32_t opt_dense_spec = 2;       // dense: leading rounds enqueued without a host read-back
     int32_t opt_sweep_glds = 0;       // pruned sweep chunk loop: LDS-DMA staging (OPT_SWEEP_GLDS; r06: ties register staging)
     int32_t opt_sweep_stats = 0;      // diagnostics: staged chunks of the pruned sweeps (OPT_SWEEP_STATS)
+    unsigned long long* d_sweep_hits = nullptr;  // OPT_SWEEP_STATS: the exact passes' logged rows
+    int32_t opt_sweep_refilter = 0;   // exact pass re-tests logged rows against the final thresholds (OPT_SWEEP_REFILTER)
+    float* d_thrio = nullptr;         // refilter: the chunk loops' final thresholds [batch][Vp][64]
+    size_t thrio_n = 0;
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
     int32_t opt_csr_lean = 2;         // OPT_CSR_LEAN: sparse rounds with D + P32 only (1), the tree fold (0), auto (2)
     bool lean_next = false;           // the layout the next pool allocation takes (decided per computation)
@@ -3915,6 +3964,21 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                     // buffer `cur` (sorted after the previous sweep of the same shape), the
                     // blocks record their chunk counts, and the sort for the next sweep writes
                     // buffer cur ^ 1 (no running sweep reads it)
+                    if (eng->opt_sweep_stats && !eng->d_sweep_hits &&
+                        (e = hipMalloc((void**)&eng->d_sweep_hits, 2 * sizeof(unsigned long long))) != hipSuccess)
+                        return e;
+                    if (eng->opt_sweep_stats && (e = hipMemsetAsync(eng->d_sweep_hits, 0, 2 * sizeof(unsigned long long), s)) != hipSuccess)
+                        return e;
+                    if (eng->opt_sweep_refilter) {
+                        const size_t need_t = (size_t)nbg * eng->Vp * KL;
+                        if (eng->thrio_n < need_t) {
+                            if (eng->d_thrio) (void)hipFree(eng->d_thrio);
+                            eng->d_thrio = nullptr;
+                            eng->thrio_n = 0;
+                            if ((e = hipMalloc((void**)&eng->d_thrio, need_t * sizeof(float))) != hipSuccess) return e;
+                            eng->thrio_n = need_t;
+                        }
+                    }
                     const int cur = eng->heavy_buf;
                     HeavyArgs ha{};
                     bool sort_any = false;
@@ -3943,20 +4007,21 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                             }
                         }
                         const int32_t* ord = heavy && eng->heavy_key[k] == key ? eng->d_border[k][cur] : nullptr;
+                        float* tio = eng->opt_sweep_refilter ? eng->d_thrio + (size_t)b0 * eng->Vp * KL : nullptr;
                         if (eng->opt_sweep_glds)
                             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1, 4, false, true>), dim3((uint32_t)nbl),
                                                dim3(256), 0, st, eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
                                                P, eng->V, n, ntb, par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl,
                                                eng->d_perm, eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp,
                                                eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr, ord,
-                                               heavy ? eng->d_bweight[k] : nullptr);
+                                               heavy ? eng->d_bweight[k] : nullptr, tio);
                         else
                         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1>), dim3((uint32_t)nbl), dim3(256), 0, st,
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
                                            par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
                                            eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr, ord,
-                                           heavy ? eng->d_bweight[k] : nullptr);
+                                           heavy ? eng->d_bweight[k] : nullptr, tio);
                         if (heavy) {
                             ha.w[k] = eng->d_bweight[k];
                             ha.o[k] = eng->d_border[k][cur ^ 1];
@@ -3968,10 +4033,12 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                         }
                         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 2>), dim3((uint32_t)nbl), dim3(256), 0, st,
                                            eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, P, eng->V, n, ntb,
-                                           par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl, eng->d_perm,
+                                           par, thresh, cnt_prev + b0, cnt_cur + b0,
+                                           eng->opt_sweep_stats ? eng->d_sweep_hits : nullptr, hl, eng->d_perm,
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
                                            eng->opt_sweep_spiral, eng->opt_sweep_win1,
-                                           mdc_out ? mdc_out + (size_t)b0 * (eng->Vp / KL) * KL : nullptr);
+                                           mdc_out ? mdc_out + (size_t)b0 * (eng->Vp / KL) * KL : nullptr, nullptr,
+                                           nullptr, tio);
                         if (tail && e == hipSuccess) e = (*tail)(st, b0, n, k);
                     };
                     auto bound = [&](int k) {
@@ -4005,6 +4072,9 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                             for (uint32_t x : wk) eng->st.sweep_chunks += x;
                             eng->st.sweep_chunk_slots += (int64_t)(bound(k + 1) - bound(k)) * ntb * (int64_t)nchunks;
                         }
+                        unsigned long long hits = 0;
+                        if ((e = hipMemcpy(&hits, eng->d_sweep_hits, sizeof hits, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+                        eng->st.sweep_hit_rows += (int64_t)hits;
                     }
                     return hipGetLastError();
                 }
@@ -6164,6 +6234,8 @@ void shadowtopo_destroy(shadowtopo_engine* eng) {
     for (int k = 0; k < 4; ++k)
         for (void* q : {(void*)eng->d_bweight[k], (void*)eng->d_border[k][0], (void*)eng->d_border[k][1]})
             if (q) (void)hipFree(q);
+    if (eng->d_sweep_hits) (void)hipFree(eng->d_sweep_hits);
+    if (eng->d_thrio) (void)hipFree(eng->d_thrio);
     if (eng->stage) (void)hipFree(eng->stage);
     if (eng->d_hitlog) (void)hipFree(eng->d_hitlog);
     if (eng->d_perm) (void)hipFree(eng->d_perm);
@@ -6361,6 +6433,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_SWEEP_GLDS:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "sweep glds must be 0 or 1");
             eng->opt_sweep_glds = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SWEEP_REFILTER:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "sweep refilter must be 0 or 1");
+            eng->opt_sweep_refilter = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SWEEP_STATS:
             eng->opt_sweep_stats = value ? 1 : 0;

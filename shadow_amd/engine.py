@@ -62,6 +62,7 @@ OPT_SPIN_US = 35  # host waits poll this many microseconds before blocking (defa
 OPT_HOST_GROUPS = 36  # page-locked host rows: batch groups (0 = automatic)
 OPT_SWEEP_WINDOWS = 38  # pruned dense sweep: neighbour window (bits 0-7, default 8) | far window size << 8 (0 = 64)
 OPT_SWEEP_GLDS = 39  # pruned dense sweep chunk loop: LDS-DMA staging (1) or register staging (0, default)
+OPT_SWEEP_REFILTER = 40  # pruned dense sweep: exact pass re-tests logged rows against the final f32 thresholds (1) or not (0, default)
 OPT_SWEEP_STATS = 37  # diagnostics: chunks staged by the pruned sweeps into stats sweep_chunks / sweep_chunk_slots
 OPT_PART0_PERMILLE = 29  # two sweep parts: part 0's share of the batches, per mille (default 562)
 OPT_HEAVY_FIRST = 27  # pruned sweep parts: heavy-first block order from the previous sweep (1, default) or grid order
@@ -114,7 +115,7 @@ class Stats(ctypes.Structure):
         ("compose_kernel_ms", ctypes.c_double), ("walk_targets", ctypes.c_int64),
         ("attach_prep_ms", ctypes.c_double), ("lean_groups", ctypes.c_int64),
         ("spec_composes", ctypes.c_int64), ("spec_composes_lost", ctypes.c_int64),
-        ("sweep_chunks", ctypes.c_int64), ("sweep_chunk_slots", ctypes.c_int64),
+        ("sweep_chunks", ctypes.c_int64), ("sweep_chunk_slots", ctypes.c_int64), ("sweep_hit_rows", ctypes.c_int64),
     ]
 
     def as_dict(self):

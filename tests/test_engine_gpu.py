@@ -1034,3 +1034,32 @@ def test_dense_sweep_glds_staging(case):
                            ("reliability", rel, orel)):
             assert_bitexact(f"step {step} {name}", x, y)
     eng.close()
+
+
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer", "directed"])
+def test_dense_sweep_refilter(case):
+    """OPT_SWEEP_REFILTER: the exact pass drops the logged rows that no lane passes under the
+    chunk loop's final f32 thresholds; every computation (grid order, then heavy-first, with
+    and without the refilter) equals the oracle's matrices bit for bit"""
+    if case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=6)
+    elif case == "directed":
+        g = synth.random_sparse(V=300, avg_deg=40, seed=9, directed=True)
+    elif case == "vloss_prefer":
+        g = synth.geometric_complete_ish(V=600, A=200)
+        rng = np.random.default_rng(3)
+        g.vertex_packetloss = np.where(rng.random(g.n) < 0.3, rng.uniform(0, 0.05, g.n), np.nan)
+        g.prefer_direct = True
+    else:
+        g = synth.geometric_complete_ish(V=900, A=330)
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    eng = E.Engine.from_synth(g, layout="dense")
+    eng.set_attached(g.attached)
+    for step in range(4):
+        eng.set_option(E.OPT_SWEEP_REFILTER, 0 if step == 2 else 1)
+        lat, rel, hops, kind = eng.compute_rows()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"step {step} {name}", x, y)
+    eng.close()
