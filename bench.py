@@ -79,13 +79,17 @@ def dense_sweep_compulsory(Vp, st):
     return total / L
 
 
-def sparse_step_compulsory(V, n_arcs, sources):
+def sparse_step_compulsory(V, n_arcs, sources, state_bytes=24):
     """Compulsory HBM bytes of one matrix build on a sparse graph, batched Dijkstra-
     equivalent: per 64-source batch every in-arc's tail distances once (64 x 8 B), the CSR
     once (row pointer 8 B, tail 4 B + latency 8 B per arc) and every (vertex, source) state
-    written once."""
+    written once -- 12 B for the lean rounds (distance + predecessor arc), 24 B for the
+    tree-fold rounds (distance + the {R, H, P} record).  V and n_arcs are the graph the rounds
+    run on (C5: the pendant-pruned view).  (r06: up to r05 every state was priced at the dense
+    sweep's 36 B and C5 at its full graph, which overstated the compulsory bytes, so the
+    fraction, by ~28 % on C4.)"""
     nb = -(-sources // 64)
-    return nb * (n_arcs * 64 * 8 + (V + 1) * 8 + n_arcs * 12 + V * 64 * STATE_BYTES)
+    return nb * (n_arcs * 64 * 8 + (V + 1) * 8 + n_arcs * 12 + V * 64 * state_bytes)
 
 
 VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMD-32s, one wave64 instruction per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md)
@@ -153,7 +157,8 @@ def roofline_of(st, g, config, scale, world, rows, steps, dense_variant=0, step_
         # step's compulsory bytes / the relax kernels' time in the step
         kname = "k_push+k_pred_pass+k_fold" if st.get("push_rounds") else "k_relax"
         launches, kms = max(1, st["relax_launches"]), st["relax_ms"]
-        bytes_per_launch = sparse_step_compulsory(g.n, st["n_arcs"], rows) * steps / launches
+        bytes_per_launch = sparse_step_compulsory(st.get("relax_vertices") or g.n, st.get("relax_arcs") or st["n_arcs"],
+                                                  rows, 12 if st.get("lean_groups") else 24) * steps / launches
         batches_per_launch = st["relax_batches"] / launches
     avg_launch_s = kms / launches / 1e3
     achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None

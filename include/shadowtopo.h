@@ -265,6 +265,8 @@ typedef struct shadowtopo_stats {
     int64_t sweep_chunks;       /* OPT_SWEEP_STATS: 32-row chunks the pruned sweeps' blocks staged */
     int64_t sweep_chunk_slots;  /* OPT_SWEEP_STATS: blocks x chunks of those sweeps (the unpruned count) */
     int64_t sweep_hit_rows;     /* OPT_SWEEP_STATS: rows the chunk loops logged for the exact f64 passes */
+    int64_t relax_vertices;     /* vertices of the graph the rounds run on (the pendant-pruned view, if any) */
+    int64_t relax_arcs;         /* its arcs */
 } shadowtopo_stats;
 
 /* Number of visible HIP devices (0 if none). */

@@ -6956,6 +6956,10 @@ int shadowtopo_get_stats(const shadowtopo_engine* eng, shadowtopo_stats* out) {
     if (!eng || !out) return fail(SHADOWTOPO_EINVAL, "NULL argument");
     *out = eng->st;
     out->pruned_vertices = eng->prune_ready ? eng->pruned_vertices : 0;
+    // the graph the relaxation rounds run on (the pendant-pruned view where one is in use)
+    const bool view = eng->prune_ready && eng->rg == &eng->gp;
+    out->relax_vertices = view ? (int64_t)eng->gp.V : (int64_t)eng->V;
+    out->relax_arcs = view ? eng->gp_arcs : eng->n_arcs;
     return SHADOWTOPO_OK;
 }
 

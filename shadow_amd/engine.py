@@ -116,6 +116,7 @@ class Stats(ctypes.Structure):
         ("attach_prep_ms", ctypes.c_double), ("lean_groups", ctypes.c_int64),
         ("spec_composes", ctypes.c_int64), ("spec_composes_lost", ctypes.c_int64),
         ("sweep_chunks", ctypes.c_int64), ("sweep_chunk_slots", ctypes.c_int64), ("sweep_hit_rows", ctypes.c_int64),
+        ("relax_vertices", ctypes.c_int64), ("relax_arcs", ctypes.c_int64),
     ]
 
     def as_dict(self):
