@@ -49,6 +49,13 @@ def _case(seed):
     if layout != "dense" and opts.get("csr_variant") != 2:
         opts["csr_lean"] = lean
         opts["csr_incremental"] = inc
+    # r06 dense-sweep options, drawn after everything else (earlier seeds keep their draws)
+    glds, refilter = int(rng.integers(0, 2)), int(rng.integers(0, 2))
+    windows = int(rng.choice([8, 4 | (16 << 8), 16 | (8 << 8), 0]))
+    if layout != "csr":
+        opts["sweep_glds"] = glds
+        opts["sweep_refilter"] = refilter
+        opts["sweep_windows"] = windows
     return g, layout, opts
 
 
@@ -80,6 +87,9 @@ def _big_case(seed):
     opts = {"batches_in_flight": int(rng.integers(1, 4))} if rng.random() < 0.5 else {}
     opts["csr_lean"] = int(rng.integers(0, 3))  # (dense graphs ignore it)
     opts["csr_incremental"] = int(rng.choice([0, 1, 8]))
+    # r06 dense-sweep options (sparse graphs ignore them), drawn last
+    opts["sweep_glds"] = int(rng.integers(0, 2))
+    opts["sweep_refilter"] = int(rng.integers(0, 2))
     return g, opts
 
 
