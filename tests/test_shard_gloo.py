@@ -196,7 +196,7 @@ def test_two_rank_row_exchange_step(A_sel, chunks):
     assert res == [(0, True), (1, True)]
 
 
-def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False):
+def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False, hops16=False):
     """bench.py's run_sharded -- the timed step of both the headline line and the north-star
     C4 record at every GPU count (barriers, max-over-ranks timing, all-gather-only leg) --
     with the oracle as the compute stand-in on gloo"""
@@ -223,14 +223,17 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False):
         rel[:z - a] = torch.from_numpy(r)
         hops[:z - a] = torch.from_numpy(h.astype(np.int32))
 
-    codec = None
+    codec = hc = None
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if packed:
-        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from rowcodec_ref import RefRowCodec
         codec = RefRowCodec(g)
+    if hops16:  # the sparse exchange: 16-bit hop counts (RefHopCodec stands in for the engine's kernels)
+        from rowcodec_ref import RefHopCodec
+        hc = RefHopCodec()
     run = bench.run_sharded(dist, world, rank, torch.device("cpu"), A, compute, steps=3, warmup=2, chunks=chunks,
                             on_timed_start=lambda: hooks.append("start"), on_timed_end=lambda: hooks.append("end"),
-                            on_first_step=lambda: hooks.append("first"), codec=codec)
+                            on_first_step=lambda: hooks.append("first"), codec=codec, hops16=hc)
     lat, rel, hops = run["exchange"].full()
     full = og.pair_rows(flags, g.attached)
     ok = np.array_equal(lat.numpy().view(np.uint64), full[0].view(np.uint64))
@@ -242,6 +245,7 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False):
         ok &= 0 < run["allgather_bytes"] <= sum(p.numel() for p in run["exchange"].packs) * world * 2
     else:
         ok &= run["allgather_bytes"] == sum(p.numel() for p in run["exchange"].packs) * world
+    ok &= run["exchange"].hop_bytes == (2 if hops16 else 4)
     # the N-rank fields the bench line carries (sharded_report): each rank's relax time and
     # rows, the exchange alone and its bytes, the same on every rank
     rep = bench.sharded_report(dist, world, run, 3, relax_ms_per_step=1.0 + rank, rows=run["exchange"].rows)
@@ -259,12 +263,14 @@ def _worker_bench_sharded(rank, world, port, A_sel, chunks, q, packed=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("A_sel,chunks,packed", [(170, 1, False), (149, 2, False), (150, 1, True)])
-def test_two_rank_bench_run_sharded(A_sel, chunks, packed):
+@pytest.mark.parametrize("A_sel,chunks,packed,hops16", [(170, 1, False, False), (149, 2, False, False),
+                                                        (150, 1, True, False), (149, 2, False, True)])
+def test_two_rank_bench_run_sharded(A_sel, chunks, packed, hops16):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_bench_sharded, args=(r, 2, port, A_sel, chunks, q, packed)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_bench_sharded, args=(r, 2, port, A_sel, chunks, q, packed, hops16))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
