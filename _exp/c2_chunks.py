@@ -37,4 +37,6 @@ for rep in range(REPS):
               f"wall {t['wall_ms'] / N:.3f} ms per computation", flush=True)
         eng.set_option(E.OPT_SWEEP_WINDOWS, 8)
         eng.set_option(E.OPT_SWEEP_GLDS, 0)
+        eng.set_option(E.OPT_SWEEP_WAVES, 4)
+        eng.set_option(E.OPT_SWEEP_REFILTER, 0)
 eng.close()

@@ -169,6 +169,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_SWEEP_REFILTER 40    /* pruned dense sweep: the exact f64 pass first re-tests the rows the chunk loop
                                               logged against its FINAL f32 thresholds and drops those no lane passes
                                               (1) or evaluates every logged row (0, the default). Results are identical. */
+#define SHADOWTOPO_OPT_SWEEP_WAVES 41       /* pruned dense sweep: the chunk loop's blocks are 4 waves x 8 destinations
+                                              (4, the default) or 8 waves x 8 (8: one staged chunk serves 64 columns).
+                                              Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL

@@ -1276,7 +1276,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     // then needs all 8 waves dead, so more chunks are staged.)
     static_assert(NW == 4 || (NW == 8 && PH == 1), "8-wave blocks only for the chunk loop");
     static_assert(!H16 || (PH == 1 && PR && TB == 1 && NW == 4 && TDT == 8), "W16: the pruned chunk loop alone");
-    static_assert(!GL || (PH == 1 && PR && TB == 1 && NW == 4 && !H16), "LDS-DMA staging: the pruned f32 chunk loop alone");
+    static_assert(!GL || (PH == 1 && PR && TB == 1 && !H16), "LDS-DMA staging: the pruned f32 chunk loop alone");
     constexpr int NT = 64 * NW;  // threads per block
     constexpr int BW = NW * TDT;  // block columns
     constexpr int WQ = BW / 4;   // float4 per W32 chunk row
@@ -1636,7 +1636,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
         for (int k = 0; k < TB; ++k) hits[k] = 0;
         // PH 1 (the chunk loop alone has VGPRs to spare): each row's LDS reads are issued one
         // row ahead, so they are in flight while the previous row is filtered and votes
-        constexpr bool RP = PH == 1 && NW == 4 && !H16;
+        constexpr bool RP = PH == 1 && !H16;
         f4 wn[TDT / 4];
         float dn[TB];
         // W16: the row's 8 halves (one 16-byte LDS read), widened to f32
@@ -3598,6 +3598,7 @@ struct shadowtopo_engine {
     int32_t opt_sweep_glds = 0;       // pruned sweep chunk loop: LDS-DMA staging (OPT_SWEEP_GLDS; r06: ties register staging)
     int32_t opt_sweep_stats = 0;      // diagnostics: staged chunks of the pruned sweeps (OPT_SWEEP_STATS)
     unsigned long long* d_sweep_hits = nullptr;  // OPT_SWEEP_STATS: the exact passes' logged rows
+    int32_t opt_sweep_waves = 4;      // pruned sweep chunk loop: waves per block, 4 or 8 (OPT_SWEEP_WAVES)
     int32_t opt_sweep_refilter = 0;   // exact pass re-tests logged rows against the final thresholds (OPT_SWEEP_REFILTER)
     float* d_thrio = nullptr;         // refilter: the chunk loops' final thresholds [batch][Vp][64]
     size_t thrio_n = 0;
@@ -3987,28 +3988,48 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                         uint32_t* hl = eng->d_hitlog + (size_t)b0 * (size_t)(eng->Vp / TDT) * nchunks;
                         const float* mD = eng->d_minD + (size_t)b0 * nchunks * KL;
                         const int64_t nbl = 8 * (((int64_t)n * ntb + 7) / 8);
-                        const int64_t key = ((int64_t)b0 << 42) | ((int64_t)n << 21) | ntb;
-                        bool heavy = eng->opt_heavy_first && k < 4 && nbl / 8 <= HEAVY_MAX;
-                        if (heavy && eng->heavy_cap[k] < (size_t)nbl) {
+                        // the chunk loop's blocks: 4 waves x 8 destinations, or (OPT_SWEEP_WAVES 8)
+                        // 8 waves x 8: 64 destinations per block, one staged D32 chunk for twice
+                        // the columns; the exact pass keeps 4-wave blocks (hit logs are per wave tile)
+                        const bool w8 = eng->opt_sweep_waves == 8;
+                        const int32_t ntb1 = w8 ? (eng->V + 8 * TDT - 1) / (8 * TDT) : ntb;
+                        const int64_t nbl1 = 8 * (((int64_t)n * ntb1 + 7) / 8);
+                        const int64_t key = ((int64_t)b0 << 42) | ((int64_t)n << 21) | ((int64_t)w8 << 20) | ntb1;
+                        bool heavy = eng->opt_heavy_first && k < 4 && nbl1 / 8 <= HEAVY_MAX;
+                        if (heavy && eng->heavy_cap[k] < (size_t)nbl1) {
                             for (void* q : {(void*)eng->d_bweight[k], (void*)eng->d_border[k][0], (void*)eng->d_border[k][1]})
                                 if (q) (void)hipFree(q);
                             eng->d_bweight[k] = nullptr;
                             eng->d_border[k][0] = eng->d_border[k][1] = nullptr;
                             eng->heavy_cap[k] = 0;
                             eng->heavy_key[k] = -1;
-                            if (hipMalloc((void**)&eng->d_bweight[k], sizeof(uint32_t) * nbl) != hipSuccess ||
-                                hipMalloc((void**)&eng->d_border[k][0], sizeof(int32_t) * nbl) != hipSuccess ||
-                                hipMalloc((void**)&eng->d_border[k][1], sizeof(int32_t) * nbl) != hipSuccess ||
-                                hipMemsetAsync(eng->d_bweight[k], 0, sizeof(uint32_t) * nbl, st) != hipSuccess) {
+                            if (hipMalloc((void**)&eng->d_bweight[k], sizeof(uint32_t) * nbl1) != hipSuccess ||
+                                hipMalloc((void**)&eng->d_border[k][0], sizeof(int32_t) * nbl1) != hipSuccess ||
+                                hipMalloc((void**)&eng->d_border[k][1], sizeof(int32_t) * nbl1) != hipSuccess ||
+                                hipMemsetAsync(eng->d_bweight[k], 0, sizeof(uint32_t) * nbl1, st) != hipSuccess) {
                                 (void)hipGetLastError();
                                 heavy = false;
                             } else {
-                                eng->heavy_cap[k] = (size_t)nbl;
+                                eng->heavy_cap[k] = (size_t)nbl1;
                             }
                         }
                         const int32_t* ord = heavy && eng->heavy_key[k] == key ? eng->d_border[k][cur] : nullptr;
                         float* tio = eng->opt_sweep_refilter ? eng->d_thrio + (size_t)b0 * eng->Vp * KL : nullptr;
-                        if (eng->opt_sweep_glds)
+                        if (w8 && eng->opt_sweep_glds)
+                            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1, 8, false, true>), dim3((uint32_t)nbl1),
+                                               dim3(512), 0, st, eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
+                                               P, eng->V, n, ntb1, par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl,
+                                               eng->d_perm, eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp,
+                                               eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr, ord,
+                                               heavy ? eng->d_bweight[k] : nullptr, tio);
+                        else if (w8)
+                            hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1, 8, false, false>), dim3((uint32_t)nbl1),
+                                               dim3(512), 0, st, eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
+                                               P, eng->V, n, ntb1, par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl,
+                                               eng->d_perm, eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp,
+                                               eng->g.vfac, eng->opt_sweep_spiral, eng->opt_sweep_win1, nullptr, ord,
+                                               heavy ? eng->d_bweight[k] : nullptr, tio);
+                        else if (eng->opt_sweep_glds)
                             hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, 1, true, 1, 4, false, true>), dim3((uint32_t)nbl),
                                                dim3(256), 0, st, eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r,
                                                P, eng->V, n, ntb, par, thresh, cnt_prev + b0, cnt_cur + b0, nullptr, hl,
@@ -4025,7 +4046,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                         if (heavy) {
                             ha.w[k] = eng->d_bweight[k];
                             ha.o[k] = eng->d_border[k][cur ^ 1];
-                            ha.slots[k] = (int32_t)(nbl / 8);
+                            ha.slots[k] = (int32_t)(nbl1 / 8);
                             eng->heavy_next[k] = key;
                             sort_any = true;
                         } else {
@@ -4070,7 +4091,8 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                             if ((e = hipMemcpy(wk.data(), ha.w[k], wk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess)
                                 return e;
                             for (uint32_t x : wk) eng->st.sweep_chunks += x;
-                            eng->st.sweep_chunk_slots += (int64_t)(bound(k + 1) - bound(k)) * ntb * (int64_t)nchunks;
+                            const int32_t ntbs = eng->opt_sweep_waves == 8 ? (eng->V + 8 * TDT - 1) / (8 * TDT) : ntb;
+                            eng->st.sweep_chunk_slots += (int64_t)(bound(k + 1) - bound(k)) * ntbs * (int64_t)nchunks;
                         }
                         unsigned long long hits = 0;
                         if ((e = hipMemcpy(&hits, eng->d_sweep_hits, sizeof hits, hipMemcpyDeviceToHost)) != hipSuccess) return e;
@@ -6433,6 +6455,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_SWEEP_GLDS:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "sweep glds must be 0 or 1");
             eng->opt_sweep_glds = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SWEEP_WAVES:
+            if (value != 4 && value != 8) return fail(SHADOWTOPO_EINVAL, "sweep waves must be 4 or 8");
+            eng->opt_sweep_waves = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SWEEP_REFILTER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "sweep refilter must be 0 or 1");

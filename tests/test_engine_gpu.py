@@ -1063,3 +1063,33 @@ def test_dense_sweep_refilter(case):
                            ("reliability", rel, orel)):
             assert_bitexact(f"step {step} {name}", x, y)
     eng.close()
+
+
+@pytest.mark.parametrize("glds", [0, 1])
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
+def test_dense_sweep_eight_wave_blocks(case, glds):
+    """OPT_SWEEP_WAVES 8: the chunk loop in 8-wave blocks (64 destinations per staged chunk),
+    the exact pass in 4-wave blocks reading the same per-wave hit logs; grid order, then
+    heavy-first (another block shape: its own order), then 4-wave blocks again -- the oracle's
+    matrices bit for bit every time"""
+    if case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=6)
+    elif case == "vloss_prefer":
+        g = synth.geometric_complete_ish(V=600, A=200)
+        rng = np.random.default_rng(3)
+        g.vertex_packetloss = np.where(rng.random(g.n) < 0.3, rng.uniform(0, 0.05, g.n), np.nan)
+        g.prefer_direct = True
+    else:
+        g = synth.geometric_complete_ish(V=900, A=330)
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    eng = E.Engine.from_synth(g, layout="dense")
+    eng.set_attached(g.attached)
+    eng.set_option(E.OPT_SWEEP_GLDS, glds)
+    for step in range(4):
+        eng.set_option(E.OPT_SWEEP_WAVES, 4 if step == 3 else 8)
+        lat, rel, hops, kind = eng.compute_rows()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"step {step} {name}", x, y)
+    eng.close()
