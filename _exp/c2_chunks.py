@@ -39,4 +39,6 @@ for rep in range(REPS):
         eng.set_option(E.OPT_SWEEP_GLDS, 0)
         eng.set_option(E.OPT_SWEEP_WAVES, 4)
         eng.set_option(E.OPT_SWEEP_REFILTER, 0)
+        eng.set_option(E.OPT_SWEEP_PARTS, 2)
+        eng.set_option(E.OPT_DENSE_BATCHES_PER_WAVE, 1)
 eng.close()
