@@ -358,6 +358,27 @@ def run_sharded(dist, world, rank, device, A, compute, steps, warmup, chunks=1, 
     return out
 
 
+def rehearsal_check(eng, ex, A, device):
+    """SHADOWTOPO_BENCH_ONE_GPU rehearsals (every rank on one device): the matrix the exchange
+    assembled on this rank against the whole A x A matrix computed by this rank's engine alone,
+    bit for bit (None outside a rehearsal)"""
+    if os.environ.get("SHADOWTOPO_BENCH_ONE_GPU") != "1" or ex.world == 1:
+        return None
+    import torch
+    got = ex.full()
+    lat = torch.empty((A, A), dtype=torch.float64, device=device)
+    rel = torch.empty_like(lat)
+    hops = torch.empty((A, A), dtype=torch.int32, device=device)
+    eng.compute_rows_device(0, A, lat.data_ptr(), rel.data_ptr(), hops.data_ptr(),
+                            stream=torch.cuda.current_stream(device).cuda_stream)
+    torch.cuda.synchronize(device)
+    same = [bool(torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
+                             y.view(torch.int64) if y.dtype == torch.float64 else y))
+            for x, y in zip(got, (lat, rel, hops))]
+    del lat, rel, hops
+    return {"rank": ex.rank, "pairs": A * A, "lat_equal": same[0], "rel_equal": same[1], "hops_equal": same[2]}
+
+
 def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=1, project=True, hops16=True):
     """The north-star workload (BASELINE.json configs[3], SURVEY.md 8d C4: a 10^5-vertex
     Barabasi-Albert graph, 10^4 attached hosts) on every rank, timed like the headline
@@ -399,6 +420,7 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
                           on_timed_start=reset, on_timed_end=collect, hops16=hc)
         ex, elapsed, st = run["exchange"], run["elapsed_s"], eng_stats
         timed = run["timed"]
+        check = rehearsal_check(eng, ex, A, device)
         rec = {"workload": desc, "n_gpus": world, "n_vertices": g.n, "n_arcs": st["n_arcs"], "attached": A,
                "steps": steps, "warmup": warmup, "matrix_build_ms": elapsed / steps * 1e3,
                "value": A * steps / elapsed, "unit": "source-paths/s",
@@ -425,6 +447,8 @@ def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=
                   "time_met": rec["matrix_build_ms"] < 1000.0,
                   "frac_compulsory": rec["roofline"]["frac"], "frac_met": rec["roofline"]["frac"] >= 0.5}
         rec["target"] = target
+        if check is not None:
+            rec["rehearsal_check"] = check
         if project and world == 1:
             proj = {}
             lat = torch.empty((A, A), dtype=torch.float64, device=device)
@@ -632,13 +656,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to run a different rank count")
+    # rehearsal of the N-rank path on a one-GPU box: every rank on device 0, gloo instead of
+    # RCCL (RCCL refuses two ranks on one device).  The numbers mean nothing; the code path
+    # (launcher, sharding, codecs, exchange, barriers, the report) is the one N GPUs run.
+    one_gpu = world > 1 and os.environ.get("SHADOWTOPO_BENCH_ONE_GPU") == "1"
+    if one_gpu:
+        local = 0
 
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{local}")
@@ -722,6 +755,7 @@ def main():
                       hops16=hops16)
     cold_start_ms = cold["ms"]
     elapsed = run["elapsed_s"]
+    check = rehearsal_check(eng, run["exchange"], A, dev)
     total_sources = A if world > 1 else rows  # every rank's rows per step
     value = total_sources * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -891,6 +925,9 @@ def main():
                                                "first_step": cold_start_ms - create_ms},
                        "host_buffers_source_paths_per_s": (rows / host_ms * 1e3) if host_ms else None},
         }
+        if one_gpu:
+            out["rehearsal"] = f"{world} ranks on one GPU over gloo (SHADOWTOPO_BENCH_ONE_GPU): not a measurement"
+            out["rehearsal_check"] = check
         print(json.dumps(out), flush=True)
     if eng is not None:
         eng.close()
