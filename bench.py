@@ -376,7 +376,9 @@ def rehearsal_check(eng, ex, A, device):
                              y.view(torch.int64) if y.dtype == torch.float64 else y))
             for x, y in zip(got, (lat, rel, hops))]
     del lat, rel, hops
-    return {"rank": ex.rank, "pairs": A * A, "lat_equal": same[0], "rel_equal": same[1], "hops_equal": same[2]}
+    every = rank_values(ex.dist, ex.world, float(all(same)))
+    return {"rank": ex.rank, "pairs": A * A, "lat_equal": same[0], "rel_equal": same[1], "hops_equal": same[2],
+            "ranks_equal": [bool(v) for v in every]}
 
 
 def north_star_c4(device, dist=None, world=1, rank=0, steps=5, warmup=1, chunks=1, project=True, hops16=True):
