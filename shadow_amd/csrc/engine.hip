@@ -1766,6 +1766,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
     }
     }  // PH != 2
     if constexpr (PH == 1) return;
+#ifdef SHADOWTOPO_EXP_PH2_CAP
+    int32_t exp_rows = 0;
+#endif
     // exact f64 pass over the logged rows of each batch, in row order, XR rows' loads in
     // flight at once: d(u) for the 64 sources and W(u, v0..v0+TDT) (lane j holds column
     // j % TDT, broadcast by readlane).  A source's own row never passes (its D32 is NaN: the
@@ -1787,6 +1790,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                 cm &= cm - 1;
                 unsigned long long hrows = (uint32_t)__builtin_amdgcn_readlane((int)e, ci);
                 const int32_t u0 = (c0 + ci) * SRS;
+                // refilter: bit r = this lane passes row u0 + r (the f64 distance is fetched
+                // only for passing lanes: a failing lane's candidate exceeds the final key)
+                unsigned long long lpass = ~0ull;
                 if (PH == 2 && PR && TB == 1 && thr_io) {
                     // drop the logged rows that no lane passes under the chunk loop's FINAL
                     // thresholds (D32(u) <= max_t fl32(thr_t - W32(u, v_t)), the chunk loop's own
@@ -1795,6 +1801,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                     // the rows dropped cannot change the final lexicographic state; 4 rows' loads
                     // in flight per step
                     unsigned long long keep = 0ull, todo = hrows;
+                    lpass = 0ull;
                     while (todo) {
                         int32_t rr[4];
                         float dq[4], wq[4][TDT];
@@ -1815,12 +1822,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                             float g = thr_f[0] - wq[x][0];
 #pragma unroll
                             for (int t = 1; t < TDT; ++t) g = fmaxf(g, thr_f[t] - wq[x][t]);
-                            if (rr[x] >= 0 && __ballot(dq[x] <= g)) keep |= 1ull << rr[x];
+                            const bool p = rr[x] >= 0 && dq[x] <= g;
+                            if (__ballot(p)) keep |= 1ull << rr[x];
+                            lpass |= p ? 1ull << (rr[x] & 63) : 0ull;
                         }
                     }
                     hrows = keep;
                 }
                 if (prof && lane == 0) atomicAdd(&prof[0], (unsigned long long)__popcll(hrows));
+#ifdef SHADOWTOPO_EXP_PH2_NOROWS
+                hrows = 0;  // timing experiment only (wrong results): the exact pass without its rows
+#endif
+#ifdef SHADOWTOPO_EXP_PH2_CAP
+                // timing experiment only (wrong results): at most CAP exact rows per wave
+                if (exp_rows >= SHADOWTOPO_EXP_PH2_CAP) hrows = 0;
+                exp_rows += __popcll(hrows);
+#endif
                 while (hrows) {
                     int32_t ur[XR], rp[XR];
                     int nr = 0;
@@ -1839,7 +1856,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                     double d64[XR], ws[XR][TDT];
 #pragma unroll
                     for (int x = 0; x < XR; ++x) {
-                        d64[x] = Dl[(size_t)ur[x] * KL];
+                        d64[x] = (lpass >> (rp[x] - u0)) & 1ull ? Dl[(size_t)ur[x] * KL] : dinf();
 #pragma unroll
                         for (int t = 0; t < TDT; ++t) ws[x][t] = W[(size_t)rp[x] * Vp + v0 + t];
                     }
