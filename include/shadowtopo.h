@@ -172,6 +172,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_SWEEP_WAVES 41       /* pruned dense sweep: the chunk loop's blocks are 4 waves x 8 destinations
                                               (4, the default) or 8 waves x 8 (8: one staged chunk serves 64 columns).
                                               Results are identical. */
+#define SHADOWTOPO_OPT_SEED_SKIP 42         /* dense round 0: the exact pass leaves a pair whose seed candidate (the source's
+                                              own arc) won untainted unread and unwritten -- the stored state is the seed's
+                                              (1, the default) -- or re-reads and compares it (0). Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL

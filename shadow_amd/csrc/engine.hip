@@ -1098,7 +1098,7 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
                                                const double* __restrict__ in_r, int32_t parity,
                                                int32_t* __restrict__ cnt, int32_t b,
                                                const int32_t* vids = nullptr, const SeedRows& sr = SeedRows{},
-                                               float* __restrict__ mdc = nullptr) {
+                                               float* __restrict__ mdc = nullptr, bool seeded = false) {
     unsigned long long* chn = B.chm(parity);
     int32_t nch = 0;
     // mdc (the chained rounds' pruned delta round 1): the lane's minimum new D32 over its
@@ -1112,12 +1112,17 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
         bool ch = false;
         if (bu[t] >= 0 && sv >= 0 && sv != v) {
             const size_t idx = (size_t)v * KL + lane;
-            if (sr.WIp && bu[t] == sv) {
+            const uint32_t taint = (((tie >> t) & 1u) || bdu[t] == bc[t]) ? (TAINT | LTIE) : 0u;
+            if (sr.WIp && bu[t] == sv && seeded && !taint) {
+                // the seed candidate won untainted and the stored state is still the seed's
+                // (k_seed_dense_t: d 0 + w, D32, {vfac(s) * WR, h 1, arc}, BDU 0): the record
+                // below would equal it field for field, so nothing is read or written
+            } else if (sr.WIp && bu[t] == sv) {
                 // finish_vertex with hu = 0, ru = vfac(s): h = 1 (+ a local tie), r = vfac(s) * in_r[arc]
                 // (WRp holds in_r of the same arc, the same double)
                 const int32_t arc = sr.WIp[sr.srow + v0 + t];
                 const double r = sr.rs * sr.WRp[sr.srow + v0 + t];
-                const uint32_t h = 1u | ((((tie >> t) & 1u) || bdu[t] == bc[t]) ? (TAINT | LTIE) : 0u);
+                const uint32_t h = 1u | taint;
                 const Rec cur = rec_load(B.Q + idx);
                 if (bc[t] != B.D[idx] || h != cur.h || r != cur.r || arc != cur.p) {
                     B.D[idx] = bc[t];
@@ -1125,13 +1130,14 @@ __device__ __forceinline__ void dense_epilogue(const BatchDev& B, int lane, int3
                     rec_store(B.Q + idx, r, h, arc);
                     ch = true;
                 }
+                B.BDU[idx] = bdu[t];
             } else {
                 const int32_t arc = WI[(size_t)bu[t] * Vp + v];
                 const Rec cur = rec_load(B.Q + idx);
                 ch = finish_vertex(B, lane, v, arc, bu[t], bc[t], bdu[t], (tie >> t) & 1u, in_r, B.D[idx],
                                    cur.h, cur.r, cur.p);
+                B.BDU[idx] = bdu[t];
             }
-            B.BDU[idx] = bdu[t];
         }
         if (mdc && ch) mlo = fminf(mlo, f32_key(bc[t]));
         const unsigned long long m = __ballot(ch);
@@ -1260,7 +1266,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                                                        int32_t win1, float* __restrict__ mdc_out,
                                                        const int32_t* __restrict__ border = nullptr,
                                                        uint32_t* __restrict__ bweight = nullptr,
-                                                       float* __restrict__ thr_io = nullptr) {
+                                                       float* __restrict__ thr_io = nullptr, int32_t seeded = 0) {
     // PR (pruned): rows, columns, W32 and W are in the locality order `perm` (W32 and W here are
     // the permuted copies W32p[i][j] = W32[perm i][perm j], Wp likewise; ipos = perm's inverse):
     // a lane's seed weights W(s, v_t) over the wave's 8 destinations are then one 64-byte
@@ -1891,7 +1897,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(TB == 1
                 }
                 dense_epilogue<TDT>(B[k], lane, sv[k], v0, V, bc[k], bdu[k], bu[k], tie[k], WI, Vp, in_r, parity,
                                     cnt, b0 + k, vid, sr,
-                                    mdc_out ? mdc_out + ((size_t)(b0 + k) * (Vp / KL) + v0 / KL) * KL : nullptr);
+                                    mdc_out ? mdc_out + ((size_t)(b0 + k) * (Vp / KL) + v0 / KL) * KL : nullptr,
+                                    seeded != 0);
             }
     }
 }
@@ -3619,6 +3626,7 @@ struct shadowtopo_engine {
     unsigned long long* d_sweep_hits = nullptr;  // OPT_SWEEP_STATS: the exact passes' logged rows
     int32_t opt_sweep_waves = 4;      // pruned sweep chunk loop: waves per block, 4 or 8 (OPT_SWEEP_WAVES)
     int32_t opt_sweep_refilter = 0;   // exact pass re-tests logged rows against the final thresholds (OPT_SWEEP_REFILTER)
+    int32_t opt_seed_skip = 1;        // round-0 exact pass leaves untainted seed winners unread (OPT_SEED_SKIP)
     float* d_thrio = nullptr;         // refilter: the chunk loops' final thresholds [batch][Vp][64]
     size_t thrio_n = 0;
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
@@ -3916,7 +3924,7 @@ using PartTail = std::function<hipError_t(hipStream_t, int32_t, int32_t, int)>;
 template <int TB>
 hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
                            const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail,
-                           float* mdc_out) {
+                           float* mdc_out, int32_t seeded) {
     constexpr int TDT = FTDT, XR = 2;
     const int32_t ntb = (eng->V + 4 * TDT - 1) / (4 * TDT);
     const int32_t ngroups = (nbg + TB - 1) / TB;
@@ -4078,7 +4086,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                            eng->d_minW, mD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac,
                                            eng->opt_sweep_spiral, eng->opt_sweep_win1,
                                            mdc_out ? mdc_out + (size_t)b0 * (eng->Vp / KL) * KL : nullptr, nullptr,
-                                           nullptr, tio);
+                                           nullptr, tio, seeded);
                         if (tail && e == hipSuccess) e = (*tail)(st, b0, n, k);
                     };
                     auto bound = [&](int k) {
@@ -4133,7 +4141,7 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
                                eng->d_W32p, eng->d_Wp, eng->d_WI, eng->Vp, eng->g.in_r, eng->pools, eng->V, nbg, ntb,
                                par, thresh, cnt_prev, cnt_cur, eng->d_prof, eng->d_hitlog, eng->d_perm, eng->d_minW,
                                eng->d_minD, eng->d_pos, eng->d_WIp, eng->d_WRp, eng->g.vfac, eng->opt_sweep_spiral,
-                               eng->opt_sweep_win1, nullptr);
+                               eng->opt_sweep_win1, nullptr, nullptr, nullptr, nullptr, seeded);
             return hipGetLastError();
         }
         hipLaunchKernelGGL((k_relax_dense_f<TDT, XR, TB, true>), dim3((uint32_t)nblocks), dim3(256), 0, s,
@@ -4149,13 +4157,16 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
     return hipGetLastError();
 }
 
+// seeded: every batch's state is k_seed_dense_t's (round 0 after the fused seed), so an exact
+// pass whose seed candidate won untainted leaves the pair alone without reading it
 hipError_t launch_dense_f(shadowtopo_engine* eng, int32_t nbg, int32_t par, int32_t thresh,
                           const int32_t* cnt_prev, int32_t* cnt_cur, hipStream_t s, const PartTail* tail = nullptr,
-                          float* mdc_out = nullptr) {
+                          float* mdc_out = nullptr, bool seeded = false) {
+    const int32_t sd = seeded && eng->opt_seed_skip;
     switch (eng->opt_dense_tb) {
-        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out);
-        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out);
-        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out);
+        case 1: return launch_dense_ft<1>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out, sd);
+        case 4: return launch_dense_ft<4>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out, sd);
+        default: return launch_dense_ft<2>(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, tail, mdc_out, sd);
     }
 }
 
@@ -4622,9 +4633,10 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s, const std::fu
                     if (std::find(full_b.begin(), full_b.end(), 0) != full_b.end() || any_delta)
                         return fail(SHADOWTOPO_EINTERNAL, "chained rounds: round 0 is not a full sweep of every batch");
                     HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, &chain_tail,
-                                           fuse_mindc ? eng->d_minDc : nullptr));
+                                           fuse_mindc ? eng->d_minDc : nullptr, fused_seed));
                 } else
-                    HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s));
+                    HIP_TRY(launch_dense_f(eng, nbg, par, thresh, cnt_prev, cnt_cur, s, nullptr, nullptr,
+                                           fused_seed && round == 0));
                 eng->st.full_sweeps++;
                 for (int32_t b = 0; b < nbg; ++b) eng->st.full_batches += full_b[b];
             }
@@ -6478,6 +6490,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_SWEEP_WAVES:
             if (value != 4 && value != 8) return fail(SHADOWTOPO_EINVAL, "sweep waves must be 4 or 8");
             eng->opt_sweep_waves = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_SEED_SKIP:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "seed skip must be 0 or 1");
+            eng->opt_seed_skip = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SWEEP_REFILTER:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "sweep refilter must be 0 or 1");

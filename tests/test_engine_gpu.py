@@ -1065,6 +1065,45 @@ def test_dense_sweep_refilter(case):
     eng.close()
 
 
+@pytest.mark.parametrize("mode", ["chained", "host_rounds", "full_sweeps"])
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer", "directed"])
+def test_dense_seed_skip(case, mode):
+    """OPT_SEED_SKIP: round 0's exact pass leaves the pairs whose seed candidate won untainted
+    unread (their stored state is k_seed_dense_t's); later full sweeps (OPT_DELTA_PERMILLE 0:
+    every round a full sweep) must not.  Chained part rounds, host-driven rounds and full
+    sweeps only, each with and without the skip and across two attached sets, equal the
+    oracle's matrices bit for bit"""
+    if case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=6)
+    elif case == "directed":
+        g = synth.random_sparse(V=300, avg_deg=40, seed=9, directed=True)
+    elif case == "vloss_prefer":
+        g = synth.geometric_complete_ish(V=600, A=200)
+        rng = np.random.default_rng(3)
+        g.vertex_packetloss = np.where(rng.random(g.n) < 0.3, rng.uniform(0, 0.05, g.n), np.nan)
+        g.prefer_direct = True
+    else:
+        g = synth.geometric_complete_ish(V=900, A=330)
+    other = np.sort(np.random.default_rng(21).choice(g.n, size=len(g.attached), replace=False)).astype(np.int32)
+    eng = E.Engine.from_synth(g, layout="dense")
+    if mode == "host_rounds":
+        eng.set_option(E.OPT_DENSE_SPEC, 0)
+    elif mode == "full_sweeps":
+        eng.set_option(E.OPT_DELTA_PERMILLE, 0)
+    for att in (g.attached, other):
+        g.attached = att
+        olat, orel, ohops, okind, og = oracle_matrix(g)
+        og.close()
+        eng.set_attached(att)
+        for skip in (1, 0, 1):
+            eng.set_option(E.OPT_SEED_SKIP, skip)
+            lat, rel, hops, kind = eng.compute_rows()
+            for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                               ("reliability", rel, orel)):
+                assert_bitexact(f"skip {skip} {name}", x, y)
+    eng.close()
+
+
 @pytest.mark.parametrize("glds", [0, 1])
 @pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
 def test_dense_sweep_eight_wave_blocks(case, glds):
