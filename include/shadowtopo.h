@@ -175,6 +175,9 @@ typedef struct shadowtopo_engine shadowtopo_engine;
 #define SHADOWTOPO_OPT_SEED_SKIP 42         /* dense round 0: the exact pass leaves a pair whose seed candidate (the source's
                                               own arc) won untainted unread and unwritten -- the stored state is the seed's
                                               (1, the default) -- or re-reads and compares it (0). Results are identical. */
+#define SHADOWTOPO_OPT_DELTA_W16 43         /* pruned dense delta rounds: the filter's W slabs in fp16 (W rounded toward -inf:
+                                              half the slab bytes, a looser but still conservative filter; 1, the
+                                              default) or f32 (0). Results are identical. */
 #define SHADOWTOPO_OPT_PART0_PERMILLE 29   /* pruned dense sweep in two parts: per mille of the batches part 0 (launched first)
                                               takes (default 562). Results are identical. */
 /* testing: the failure paths a convergence bug would take, reported as SHADOWTOPO_EINTERNAL

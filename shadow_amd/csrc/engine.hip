@@ -2316,7 +2316,7 @@ constexpr int RING_S = 512;  // ring segment (int16 entries): a chunk's pairs of
 
 constexpr int PR_CHUNKS = 640;  // pruned delta: live-chunk list capacity (dense mode keeps Vp <= 38 730: 606 chunks)
 
-template <bool PR>
+template <bool PR, bool H16 = false>
 __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __restrict__ W32,
                                                                  const double* __restrict__ W,
                                                                  const int32_t* __restrict__ WI, int32_t Vp,
@@ -2344,10 +2344,17 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
     // destination instead: the chunk is dead when minDc(chunk, s) > max_v fl32(sT[s][v] -
     // mWc(chunk, v)) for every s, mWc(chunk, v) = min W32 of the chunk's rows into v -- the
     // same argument (W32(u, v) >= mWc(chunk, v)), and never looser than the tile bound.
+    // H16 (PR only, OPT_DELTA_W16, r06): the slab comes from W16p (W32p rounded toward -inf to
+    // fp16, NaN kept; k_w16), half the bytes; the filter's slacks fl32(sT - W16) are >= the
+    // W32 ones, so it stays conservative and the exact settle decides as before.
+    static_assert(!H16 || PR, "fp16 slabs: the pruned delta round only");
     constexpr int SW = KL / DW;  // sources per wave
-    constexpr int PF = KL * KL / 4 / (64 * DW);  // float4 of one W32 slab per thread
+    constexpr int PF = KL * KL / (H16 ? 8 : 4) / (64 * DW);  // 16-byte pieces of one slab per thread
+    constexpr int SWH = KL + 8;  // H16: LDS row stride (halves) of the slab
     __shared__ __attribute__((aligned(16))) float sT[KL * SWS];  // [s][v] thresholds
-    __shared__ __attribute__((aligned(16))) float sW[KL * SWS];
+    // the slab (H16: halves, half the LDS; the per-destination bounds below borrow 16 rows)
+    __shared__ __attribute__((aligned(16))) float sW[H16 ? KL * SWH / 2 : KL * SWS];
+    static_assert(!H16 || KL * SWH / 2 >= 4 * DW * SWS, "the bounds' column minima fit the fp16 slab");
     __shared__ int16_t sP[DW][RING_S];  // (row in chunk << 6) | s
     __shared__ int16_t sL[PR ? PR_CHUNKS : 1];  // PR: the block's live chunks, ascending
     __shared__ int32_t sNL;
@@ -2482,7 +2489,11 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             const int e = threadIdx.x + i * 64 * DW;  // float4 index within the slab: row e / 16, column 4 (e % 16)
-            pwa[i] = (gf4*)(W32g + (size_t)(u0 + (e >> 4)) * Vp + v0 + 4 * (e & 15));
+            if constexpr (H16)  // 8 halves per piece: row e / 8, column 8 (e % 8)
+                pwa[i] = (gf4*)((const __attribute__((address_space(1))) uint16_t*)W32g + (size_t)(u0 + (e >> 3)) * Vp +
+                                v0 + 8 * (e & 7));
+            else
+                pwa[i] = (gf4*)(W32g + (size_t)(u0 + (e >> 4)) * Vp + v0 + 4 * (e & 15));
             pw[i] = *pwa[i];
         }
     };
@@ -2495,8 +2506,16 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             const int e = threadIdx.x + i * 64 * DW;
-            *(f4*)&sW[(e >> 4) * SWS + 4 * (e & 15)] = pw[i];
+            if constexpr (H16)
+                *(f4*)((uint16_t*)sW + (e >> 3) * SWH + 8 * (e & 7)) = pw[i];
+            else
+                *(f4*)&sW[(e >> 4) * SWS + 4 * (e & 15)] = pw[i];
         }
+    };
+    // the staged slab's weight of row r into column c (H16: fp16 -> f32, exact)
+    auto slab_w = [&](int r, int c) -> float {
+        if constexpr (H16) return (float)__builtin_bit_cast(_Float16, ((const uint16_t*)sW)[r * SWH + c]);
+        else return sW[r * SWS + c];
     };
 
     // filter n <= 64 listed pairs starting at ring[h] (lane = pair), settle the passing ones;
@@ -2508,20 +2527,40 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
         const int32_t ur = PR ? __shfl(urow, r) : u0 + r;
         const gfloat* dua = D32 + (size_t)ur * KL + sp;
         const float du = *dua;
-        const float* wrow = &sW[r * SWS];
         const float* trow = &sT[sp * SWS];
         // slacks two at a time (v_pk_add_f32), their maximum as a v_max3 chain; both rows are
         // read at immediate offsets from one base each
         typedef float f2 __attribute__((ext_vector_type(2)));
         float g = __int_as_float(0x7fc00000);
+        if constexpr (H16) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            typedef _Float16 hh2 __attribute__((ext_vector_type(2)));
+            const uint16_t* wrow = (const uint16_t*)sW + r * SWH;
 #pragma unroll
-        for (int j = 0; j < KL / 4; ++j) {
-            const f4 w4 = *(const f4*)&wrow[4 * j];
-            const f4 t4 = *(const f4*)&trow[4 * j];
-            const f2 a = f2{t4.x, t4.y} - f2{w4.x, w4.y};
-            const f2 c = f2{t4.z, t4.w} - f2{w4.z, w4.w};
-            g = fmaxf(fmaxf(g, a.x), a.y);
-            g = fmaxf(fmaxf(g, c.x), c.y);
+            for (int j = 0; j < KL / 8; ++j) {
+                const u4 w8 = *(const u4*)&wrow[8 * j];
+                const f4 ta = *(const f4*)&trow[8 * j];
+                const f4 tb = *(const f4*)&trow[8 * j + 4];
+                const float tv[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t word = w8[k];  // a local copy: hipcc 7.2 mis-reads a bit_cast component lvalue
+                    const hh2 h = __builtin_bit_cast(hh2, word);
+                    const f2 a = f2{tv[2 * k], tv[2 * k + 1]} - f2{(float)h.x, (float)h.y};
+                    g = fmaxf(fmaxf(g, a.x), a.y);
+                }
+            }
+        } else {
+            const float* wrow = &sW[r * SWS];
+#pragma unroll
+            for (int j = 0; j < KL / 4; ++j) {
+                const f4 w4 = *(const f4*)&wrow[4 * j];
+                const f4 t4 = *(const f4*)&trow[4 * j];
+                const f2 a = f2{t4.x, t4.y} - f2{w4.x, w4.y};
+                const f2 c = f2{t4.z, t4.w} - f2{w4.z, w4.w};
+                g = fmaxf(fmaxf(g, a.x), a.y);
+                g = fmaxf(fmaxf(g, c.x), c.y);
+            }
         }
         unsigned long long pm = __ballot(valid && du <= g);
         asm volatile("" ::"v"(dua));
@@ -2532,7 +2571,7 @@ __global__ __launch_bounds__(64 * DW) void k_relax_dense_delta_s(const float* __
             const int32_t rr = pe >> 6, ss = pe & 63;
             const int32_t uu = PR ? __builtin_amdgcn_readlane(urow, rr) : u0 + rr;
             float* tc = &sT[ss * SWS + lane];
-            const float c32 = D32[(size_t)uu * KL + ss] + sW[rr * SWS + lane];
+            const float c32 = D32[(size_t)uu * KL + ss] + slab_w(rr, lane);
             if (vok && c32 <= *tc) {
                 const double du64 = D[(size_t)uu * KL + ss];
                 const double c = du64 + W[(size_t)uu * Vp + v];
@@ -3627,6 +3666,7 @@ struct shadowtopo_engine {
     int32_t opt_sweep_waves = 4;      // pruned sweep chunk loop: waves per block, 4 or 8 (OPT_SWEEP_WAVES)
     int32_t opt_sweep_refilter = 0;   // exact pass re-tests logged rows against the final thresholds (OPT_SWEEP_REFILTER)
     int32_t opt_seed_skip = 1;        // round-0 exact pass leaves untainted seed winners unread (OPT_SEED_SKIP)
+    int32_t opt_delta_w16 = 1;        // pruned delta rounds filter with fp16 slabs (OPT_DELTA_W16)
     float* d_thrio = nullptr;         // refilter: the chunk loops' final thresholds [batch][Vp][64]
     size_t thrio_n = 0;
     int32_t opt_heavy_first = 1;      // pruned sweep parts: heavy-first block order (k_heavy_order)
@@ -3908,6 +3948,17 @@ Pools pools_from(const Pools& in, int32_t b0) {
     return P;
 }
 
+// W16p (OPT_DENSE_W16's chunk loop, OPT_DELTA_W16's delta slabs): W32p rounded toward -inf
+// to fp16, built once on stream s (W32p never changes after ensure_vperm)
+hipError_t ensure_w16p(shadowtopo_engine* eng, hipStream_t s) {
+    if (eng->d_W16p) return hipSuccess;
+    const size_t n = (size_t)eng->Vp * eng->Vp;
+    hipError_t e = hipMalloc((void**)&eng->d_W16p, n * sizeof(uint16_t));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_w16, dim3(4096), dim3(256), 0, s, eng->d_W32p, eng->d_W16p, n);
+    return hipGetLastError();
+}
+
 // the number of parts (one stream each) the f32 sweep of nbg batches runs in; 1: one launch
 int32_t sweep_parts(const shadowtopo_engine* eng, int32_t nbg) {
     if (eng->opt_dense_variant == SHADOWTOPO_DENSE_F64 || eng->opt_dense_tb != 1 || !eng->vperm_ready ||
@@ -3953,11 +4004,9 @@ hipError_t launch_dense_ft(shadowtopo_engine* eng, int32_t nbg, int32_t par, int
         hipLaunchKernelGGL(k_min_d32, dim3((uint32_t)((nchunks + 3) / 4), nbg), dim3(256), 0, s, eng->pools,
                            eng->d_perm, (int32_t)nchunks, eng->d_minD);
         if (TB <= 2 && eng->opt_sweep_split) {  // the chunk loop, then the exact pass + epilogue
-            if (eng->opt_dense_w16 && !eng->d_W16p) {
-                const size_t n = (size_t)eng->Vp * eng->Vp;
-                hipError_t e = hipMalloc((void**)&eng->d_W16p, n * sizeof(uint16_t));
+            if (eng->opt_dense_w16) {
+                hipError_t e = ensure_w16p(eng, s);
                 if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(k_w16, dim3(4096), dim3(256), 0, s, eng->d_W32p, eng->d_W16p, n);
             }
             bool w16 = false;
             if constexpr (TB == 1 && TDT == 8) {
@@ -4476,6 +4525,7 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s, const std::fu
         return dsparse ? (int)DK_SPARSE : (int)DK_PLAIN;
     };
     const auto delta_bufs = [&](int kind) -> int {
+        if (kind == DK_PRUNED && eng->opt_delta_w16) HIP_TRY(ensure_w16p(eng, s));
         if (kind == DK_PRUNED) {
             const size_t need = (size_t)eng->nb_cap * nvc * KL;
             if (eng->minDc_n < need) {
@@ -4520,10 +4570,16 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s, const std::fu
             if (!mindc_ready)
                 hipLaunchKernelGGL(k_min_d32c, dim3((uint32_t)nvc, n), dim3(256), 0, st, P, eng->d_perm, V, nvc, par,
                                    cprev, thr, mdc);
-            hipLaunchKernelGGL(k_relax_dense_delta_s<true>, dim3(nbl), dim3(64 * DW), 0, st, eng->d_W32p, eng->d_W,
-                               eng->d_WI, eng->Vp, g.in_src, g.in_r, P, V, n, nvc, par, thr, cprev, ccur, nullptr,
-                               nullptr, eng->d_perm, eng->d_minW64, mdc, eng->opt_delta_colbound ? eng->d_minW : nullptr,
-                               cm);
+            if (eng->opt_delta_w16 && eng->d_W16p)
+                hipLaunchKernelGGL((k_relax_dense_delta_s<true, true>), dim3(nbl), dim3(64 * DW), 0, st,
+                                   (const float*)eng->d_W16p, eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, P, V, n,
+                                   nvc, par, thr, cprev, ccur, nullptr, nullptr, eng->d_perm, eng->d_minW64, mdc,
+                                   eng->opt_delta_colbound ? eng->d_minW : nullptr, cm);
+            else
+                hipLaunchKernelGGL((k_relax_dense_delta_s<true, false>), dim3(nbl), dim3(64 * DW), 0, st, eng->d_W32p,
+                                   eng->d_W, eng->d_WI, eng->Vp, g.in_src, g.in_r, P, V, n, nvc, par, thr, cprev, ccur,
+                                   nullptr, nullptr, eng->d_perm, eng->d_minW64, mdc,
+                                   eng->opt_delta_colbound ? eng->d_minW : nullptr, cm);
             return;
         }
         // a round after one that changed few pairs walks only the chunks holding a changed
@@ -6490,6 +6546,10 @@ int shadowtopo_set_option(shadowtopo_engine* eng, int32_t key, int64_t value) {
         case SHADOWTOPO_OPT_SWEEP_WAVES:
             if (value != 4 && value != 8) return fail(SHADOWTOPO_EINVAL, "sweep waves must be 4 or 8");
             eng->opt_sweep_waves = (int32_t)value;
+            return SHADOWTOPO_OK;
+        case SHADOWTOPO_OPT_DELTA_W16:
+            if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "delta w16 must be 0 or 1");
+            eng->opt_delta_w16 = (int32_t)value;
             return SHADOWTOPO_OK;
         case SHADOWTOPO_OPT_SEED_SKIP:
             if (value != 0 && value != 1) return fail(SHADOWTOPO_EINVAL, "seed skip must be 0 or 1");

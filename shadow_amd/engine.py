@@ -64,6 +64,7 @@ OPT_SWEEP_WINDOWS = 38  # pruned dense sweep: neighbour window (bits 0-7, defaul
 OPT_SWEEP_GLDS = 39  # pruned dense sweep chunk loop: LDS-DMA staging (1) or register staging (0, default)
 OPT_SWEEP_REFILTER = 40  # pruned dense sweep: exact pass re-tests logged rows against the final f32 thresholds (1) or not (0, default)
 OPT_SWEEP_WAVES = 41  # pruned dense sweep chunk loop: 4 (default) or 8 waves per block
+OPT_DELTA_W16 = 43  # pruned dense delta rounds: fp16 slabs in the filter (1, default) or f32 (0)
 OPT_SEED_SKIP = 42  # dense round 0: untainted seed winners left unread by the exact pass (1, default) or compared (0)
 OPT_SWEEP_STATS = 37  # diagnostics: chunks staged by the pruned sweeps into stats sweep_chunks / sweep_chunk_slots
 OPT_PART0_PERMILLE = 29  # two sweep parts: part 0's share of the batches, per mille (default 562)

@@ -1104,6 +1104,39 @@ def test_dense_seed_skip(case, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer", "directed", "wide_latency"])
+def test_dense_delta_w16(case):
+    """OPT_DELTA_W16: the pruned delta rounds filter against fp16 slabs (W rounded toward
+    -inf); with and without it, chained and after the join, the matrices equal the oracle's
+    bit for bit (wide_latency: weights over several decades, where fp16 is coarsest)"""
+    if case == "ties":
+        g = synth.integer_grid(rows=14, cols=15, seed=6)
+    elif case == "directed":
+        g = synth.random_sparse(V=300, avg_deg=40, seed=9, directed=True)
+    elif case == "vloss_prefer":
+        g = synth.geometric_complete_ish(V=600, A=200)
+        rng = np.random.default_rng(3)
+        g.vertex_packetloss = np.where(rng.random(g.n) < 0.3, rng.uniform(0, 0.05, g.n), np.nan)
+        g.prefer_direct = True
+    elif case == "wide_latency":
+        g = synth.geometric_complete_ish(V=700, A=250)
+        g.latency = g.latency * np.exp(np.random.default_rng(8).uniform(0.0, 9.0, len(g.latency)))
+    else:
+        g = synth.geometric_complete_ish(V=900, A=330)
+    olat, orel, ohops, okind, og = oracle_matrix(g)
+    og.close()
+    eng = E.Engine.from_synth(g, layout="dense")
+    eng.set_attached(g.attached)
+    for w16, chain in ((1, 1), (0, 1), (1, 0)):
+        eng.set_option(E.OPT_DELTA_W16, w16)
+        eng.set_option(E.OPT_CHAIN_PARTS, chain)
+        lat, rel, hops, kind = eng.compute_rows()
+        for name, x, y in (("kind", kind, okind), ("latency", lat, olat), ("hops", hops, ohops),
+                           ("reliability", rel, orel)):
+            assert_bitexact(f"w16 {w16} chain {chain} {name}", x, y)
+    eng.close()
+
+
 @pytest.mark.parametrize("glds", [0, 1])
 @pytest.mark.parametrize("case", ["geometric", "ties", "vloss_prefer"])
 def test_dense_sweep_eight_wave_blocks(case, glds):
