@@ -56,6 +56,11 @@ def _case(seed):
         opts["sweep_glds"] = glds
         opts["sweep_refilter"] = refilter
         opts["sweep_windows"] = windows
+    # r06 round-0 seed skip and fp16 delta slabs (defaults on), drawn after everything else
+    skip, w16 = int(rng.random() < 0.8), int(rng.random() < 0.8)
+    if layout != "csr":
+        opts["seed_skip"] = skip
+        opts["delta_w16"] = w16
     return g, layout, opts
 
 
@@ -90,6 +95,8 @@ def _big_case(seed):
     # r06 dense-sweep options (sparse graphs ignore them), drawn last
     opts["sweep_glds"] = int(rng.integers(0, 2))
     opts["sweep_refilter"] = int(rng.integers(0, 2))
+    opts["seed_skip"] = int(rng.random() < 0.8)
+    opts["delta_w16"] = int(rng.random() < 0.8)
     return g, opts
 
 
