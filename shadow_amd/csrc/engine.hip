@@ -3953,10 +3953,16 @@ Pools pools_from(const Pools& in, int32_t b0) {
 hipError_t ensure_w16p(shadowtopo_engine* eng, hipStream_t s) {
     if (eng->d_W16p) return hipSuccess;
     const size_t n = (size_t)eng->Vp * eng->Vp;
-    hipError_t e = hipMalloc((void**)&eng->d_W16p, n * sizeof(uint16_t));
+    uint16_t* p = nullptr;
+    hipError_t e = hipMalloc((void**)&p, n * sizeof(uint16_t));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_w16, dim3(4096), dim3(256), 0, s, eng->d_W32p, eng->d_W16p, n);
-    return hipGetLastError();
+    hipLaunchKernelGGL(k_w16, dim3(4096), dim3(256), 0, s, eng->d_W32p, p, n);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        (void)hipFree(p);
+        return e;
+    }
+    eng->d_W16p = p;  // published only once its fill is enqueued
+    return hipSuccess;
 }
 
 // the number of parts (one stream each) the f32 sweep of nbg batches runs in; 1: one launch
@@ -4525,7 +4531,8 @@ int run_rounds(shadowtopo_engine* eng, int32_t nbg, hipStream_t s, const std::fu
         return dsparse ? (int)DK_SPARSE : (int)DK_PLAIN;
     };
     const auto delta_bufs = [&](int kind) -> int {
-        if (kind == DK_PRUNED && eng->opt_delta_w16) HIP_TRY(ensure_w16p(eng, s));
+        // fp16 slabs when their table can be had; without it (HBM taken) the f32 slabs serve
+        if (kind == DK_PRUNED && eng->opt_delta_w16 && ensure_w16p(eng, s) != hipSuccess) (void)hipGetLastError();
         if (kind == DK_PRUNED) {
             const size_t need = (size_t)eng->nb_cap * nvc * KL;
             if (eng->minDc_n < need) {
