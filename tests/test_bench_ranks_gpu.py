@@ -9,6 +9,7 @@ counts) keep it to seconds; the full-size C2 and C4 rehearsals at 2 and 4
 ranks are recorded in profiles/r06z2_rank_rehearsal/."""
 import json
 import os
+import signal
 import subprocess
 import sys
 
@@ -24,10 +25,18 @@ def test_bench_rank_rehearsal_assembles_the_exact_matrix(config, scale, ranks, m
     env = dict(os.environ, SHADOWTOPO_BENCH_ONE_GPU="1")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(ranks), "--steps", "2", "--warmup", "1",
            "--config", config, "--scale", str(scale), "--no-north-star", "--no-fresh", "--no-host-rate"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
-    assert p.returncode == 0, p.stderr[-3000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert lines, p.stdout[-2000:]
+    # its own process group: a hung run is ended with every rank the launcher started
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=110)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        pytest.fail("the rank rehearsal did not finish in 110 s")
+    assert p.returncode == 0, err[-3000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out[-2000:]
     out = json.loads(lines[-1])
     assert out["n_gpus"] == ranks and "rehearsal" in out
     chk = out["rehearsal_check"]
