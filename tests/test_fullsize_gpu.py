@@ -105,6 +105,24 @@ def test_c2_pruned_equals_unpruned_full_matrix():
         assert_bitexact(name, x, y)
 
 
+def test_c2_r06_step_options_full_matrix():
+    """The whole 1000x1000 bench matrix with r06's step defaults (round 0's exact pass leaving
+    the untainted seed winners unread, fp16 delta slabs) and without either, bit for bit
+    (the defaults are checked against the oracle in test_c2_whole_matrix_vs_oracle)"""
+    g = synth.geometric_complete_ish(V=10_000, A=1_000)
+    mats = []
+    for skip, w16 in ((1, 1), (0, 0), (1, 0), (0, 1)):
+        eng = E.Engine.from_synth(g)
+        eng.set_option(E.OPT_SEED_SKIP, skip)
+        eng.set_option(E.OPT_DELTA_W16, w16)
+        eng.set_attached(g.attached)
+        mats.append(eng.compute_rows())
+        eng.close()
+    for other in mats[1:]:
+        for name, x, y in zip(("latency", "reliability", "hops", "kind"), mats[0], other):
+            assert_bitexact(name, x, y)
+
+
 def test_c2_geometric_f64_kernels():
     g = synth.geometric_complete_ish(V=10_000, A=1_000)
     st = _run(g, 0, 192, sample=[5, 130], dense_variant=E.DENSE_F64)
